@@ -1,0 +1,116 @@
+/*
+ * mpcr.h — C ABI of libmpcr, the MI355X rollout engine behind the drop-in
+ * cem_planner (manipulator_mujoco_amd/planner.py).
+ *
+ * Plain C: pointers + sizes, no torch/HIP types in the signatures.  Every
+ * function returns 0 on success or a negative MPCR_E* code; the message of
+ * the last failure on the calling thread is available from
+ * mpcr_last_error().  Engines are independent (one per host thread / stream);
+ * there is no global mutable state besides the thread-local error string.
+ *
+ * Reference interface each entry point replaces (file:line in
+ * /root/reference/sampling_based_planner/):
+ *   mpcr_model_*          MjModel.from_xml_path + mjx.put_model/put_data +
+ *                         jit(mjx.forward) template          mjx_planner.py:100-108
+ *   mpcr_engine_create    cem_planner.__init__ (basis P/Pdot, mask, ids)
+ *                                                             mjx_planner.py:19-126
+ *   mpcr_rollout_cost     A_thetadot @ xi + compute_rollout_batch (vmap of
+ *                         compute_rollout_single / lax.scan of mjx_step) +
+ *                         compute_cost_batch                  mjx_planner.py:348-354,
+ *                                                             251-303
+ *   best_key / mpcr_argmin / mpcr_best_key_decode
+ *                         idx_min = argmin(cost_batch[-1])    mjx_planner.py:395
+ *   mpcr_topk             compute_ellite_samples argsort     mjx_planner.py:305-310
+ */
+#ifndef MPCR_H_
+#define MPCR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mpcr_model.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCR_ABI_VERSION 1
+
+enum {
+  MPCR_OK = 0,
+  MPCR_EINVAL = -1,   /* bad argument / shape                      */
+  MPCR_EMODEL = -2,   /* model blob invalid or over capacity        */
+  MPCR_EHIP = -3,     /* HIP runtime error                          */
+  MPCR_ENOMEM = -4,
+  MPCR_ENODEV = -5    /* no gfx950 device                           */
+};
+
+/* input layouts for mpcr_rollout_cost */
+enum {
+  MPCR_LAYOUT_XI = 0,       /* n x (nctrl*nbasis) Bernstein coefficients,
+                               joint-major (xi_filtered, mjx_planner.py:348) */
+  MPCR_LAYOUT_THETADOT = 1  /* n x (nctrl*H) joint velocities, joint-major */
+};
+
+/* flags */
+enum {
+  MPCR_F_DEVICE_PTRS = 1 << 0, /* every array argument is a device pointer  */
+  MPCR_F_RESET_BEST  = 1 << 1, /* set *best_key to UINT64_MAX before launch */
+  MPCR_F_SYNC        = 1 << 2  /* block until the stream is idle           */
+};
+
+typedef struct mpcr_model mpcr_model;   /* opaque host model handle */
+typedef struct mpcr_engine mpcr_engine; /* opaque device engine      */
+
+const char* mpcr_last_error(void);
+int mpcr_abi_version(void);
+/* gfx target name of `device` (e.g. "gfx950") into buf */
+int mpcr_device_arch(int device, char* buf, int buflen);
+
+/* models: a serialised mpcr_model_t (see mpcr_model.h) */
+int mpcr_model_from_blob(const void* blob, size_t nbytes, mpcr_model** out);
+int mpcr_model_load(const char* path, double timestep, mpcr_model** out);
+int mpcr_model_set_timestep(mpcr_model* m, double timestep);
+int mpcr_model_info(const mpcr_model* m, int* nq, int* nv, int* nslot, int* nctrl, int* npair);
+void mpcr_model_free(mpcr_model* m);
+
+/* engines: device copy of the model + the Pdot basis (horizon x nbasis,
+   row-major fp32, bernstein_coeff_ordern_new(..)[1]) + scratch for max_n. */
+int mpcr_engine_create(const mpcr_model* m, int device, int max_n, int horizon, const float* pdot,
+                       int nbasis, mpcr_engine** out);
+void mpcr_engine_free(mpcr_engine* e);
+
+/* Fused basis -> H MuJoCo-semantics steps -> cost for n candidates.
+   q0[nctrl]            initial joint positions (init_pos)
+   w[3]                 (w_pos, w_rot, w_col)
+   ptgt[3], qtgt[4]     target position / orientation (wxyz)
+   cost4 [n x 4]        (cost, cost_g, cost_r, cost_c)          (required)
+   theta [n x nctrl*H]  post-step joint positions, joint-major    (nullable)
+   thetadot [n x nctrl*H] the applied joint velocities           (nullable)
+   best_key             device uint64: atomic-min of
+                        (ordered(cost) << 32 | (index_base + i)), NaN first (nullable)
+   status [n]           per-candidate flags (bit0: constraint rows truncated,
+                        bit1: non-finite state)                  (nullable)
+   stream               hipStream_t or NULL (default stream)                  */
+int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
+                      const float* w, const float* ptgt, const float* qtgt, float* cost4, float* theta,
+                      float* thetadot, uint64_t* best_key, int index_base, int* status, int flags,
+                      void* stream);
+
+/* argmin over cost[i*stride] with NaN-first / first-index semantics
+   (jnp.argmin).  key_out (device, nullable) receives the packed key. */
+int mpcr_argmin(mpcr_engine* e, const float* cost, int stride, int n, int index_base, uint64_t* key_out,
+                int* idx_out, float* val_out, int flags, void* stream);
+
+/* decode a packed best key */
+void mpcr_best_key_decode(uint64_t key, int* idx, float* cost);
+
+/* indices of the k smallest costs, ascending, NaN last, ties by index
+   (jnp.argsort is stable): compute_ellite_samples. */
+int mpcr_topk(mpcr_engine* e, const float* cost, int stride, int n, int k, int* idx_out, int flags,
+              void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCR_H_ */

@@ -1,0 +1,187 @@
+/*
+ * mpcr_model.h — flat, POD "compiled model" consumed by the rollout engine
+ * (libmpcr) and by the CPU oracle (oracle/).
+ *
+ * The reference hands an mjx.Model pytree to every rollout
+ * (SBP/mjx_planner.py:100-108: MjModel.from_xml_path -> mjx.put_model).  Our
+ * boundary instead takes this fixed-capacity C struct, produced on the host by
+ * manipulator_mujoco_amd/mjcf.py (the MJCF compiler) and serialised as a raw
+ * little-endian blob (".mpcrm").  All quantities are SI / radians, quaternions
+ * are (w, x, y, z), matrices row-major.  fp64 here; the engine builds its own
+ * fp32 device mirror.
+ *
+ * Field names follow MuJoCo's mjModel so that the oracle and the kernels read
+ * like the engine whose semantics they restate.
+ */
+#ifndef MPCR_MODEL_H_
+#define MPCR_MODEL_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCR_MODEL_MAGIC   0x4d504352u /* 'MPCR' */
+#define MPCR_MODEL_VERSION 3
+
+#define MPCR_MAX_BODY   32
+#define MPCR_MAX_JNT    24
+#define MPCR_MAX_DOF    32
+#define MPCR_MAX_NQ     40
+#define MPCR_MAX_GEOM   64
+#define MPCR_MAX_SITE   16
+#define MPCR_MAX_PAIR   256
+#define MPCR_MAX_EQ     8
+#define MPCR_MAX_SLOT   512  /* robot-masked contact slots (cost_c) */
+#define MPCR_MAX_CTRL   8    /* planner-controlled dofs (num_dof) */
+
+/* joint types (MuJoCo mjtJoint) */
+enum { MPCR_JNT_FREE = 0, MPCR_JNT_BALL = 1, MPCR_JNT_SLIDE = 2, MPCR_JNT_HINGE = 3 };
+/* geom types (MuJoCo mjtGeom order; only these collide here) */
+enum { MPCR_GEOM_PLANE = 0, MPCR_GEOM_SPHERE = 2, MPCR_GEOM_CAPSULE = 3, MPCR_GEOM_BOX = 6, MPCR_GEOM_MESH = 7 };
+/* narrow-phase functions; pair_ncon gives the contact slots each one owns */
+enum {
+  MPCR_COL_PLANE_CAPSULE = 0, /* 2 slots: one per capsule end        */
+  MPCR_COL_PLANE_BOX     = 1, /* 4 slots: the 4 deepest corners      */
+  MPCR_COL_CAPSULE_CAPSULE = 2, /* 1 slot: closest segment points    */
+  MPCR_COL_CAPSULE_BOX   = 3, /* 2 slots: closest point + far end    */
+  MPCR_COL_BOX_BOX       = 4, /* 4 slots: SAT + face clipping        */
+  MPCR_COL_PLANE_SPHERE  = 5, /* 1 slot                              */
+  MPCR_COL_SPHERE_SPHERE = 6, /* 1 slot                              */
+  MPCR_COL_SPHERE_CAPSULE = 7, /* 1 slot                             */
+  MPCR_COL_SPHERE_BOX    = 8, /* 1 slot                              */
+  MPCR_COL_NTYPES        = 9
+};
+/* equality types */
+enum { MPCR_EQ_JOINT = 2 };
+/* disable flags (subset of mjtDisableBit semantics) */
+enum {
+  MPCR_DSBL_EULERDAMP = 1 << 0,
+  MPCR_DSBL_REFSAFE   = 1 << 1,
+  MPCR_DSBL_WARMSTART = 1 << 2,
+  MPCR_DSBL_GRAVITY   = 1 << 3,
+  MPCR_DSBL_CONTACT   = 1 << 4,
+  MPCR_DSBL_LIMIT     = 1 << 5,
+  MPCR_DSBL_EQUALITY  = 1 << 6,
+  MPCR_DSBL_PASSIVE   = 1 << 7,
+  MPCR_DSBL_FILTERPARENT = 1 << 8
+};
+
+typedef struct mpcr_model_t {
+  uint32_t magic, version, nbytes, pad0;
+
+  /* sizes */
+  int32_t nbody, njnt, nq, nv, ngeom, nsite, npair, neq;
+  int32_t ncon;        /* total contact slots (sum of pair_ncon)            */
+  int32_t nslot;       /* robot-masked slots, i.e. S of SURVEY §8a-A6        */
+  int32_t nctrl;       /* planner-controlled dofs (num_dof, = 6 for UR5e)    */
+  int32_t hande_body;  /* body whose xquat is the eef rotation (-1: none)    */
+  int32_t tcp_site;    /* site whose xpos is the eef position  (-1: none)    */
+  int32_t iterations, ls_iterations, disableflags;
+  int32_t integrator, cone;  /* 0 = Euler, 0 = pyramidal (only these built) */
+  int32_t ntree;       /* kinematic trees (roots with dofs)                  */
+
+  /* options (mjOption) and statistics */
+  double timestep, tolerance, ls_tolerance, impratio, meaninertia;
+  double gravity[3];
+  double pad1;
+
+  /* bodies (topological order, 0 = world) */
+  int32_t body_parentid[MPCR_MAX_BODY];
+  int32_t body_rootid[MPCR_MAX_BODY];
+  int32_t body_weldid[MPCR_MAX_BODY];
+  int32_t body_jntnum[MPCR_MAX_BODY];
+  int32_t body_jntadr[MPCR_MAX_BODY];
+  int32_t body_dofnum[MPCR_MAX_BODY];
+  int32_t body_dofadr[MPCR_MAX_BODY];
+  uint32_t body_dofmask[MPCR_MAX_BODY]; /* dofs on the path body..root      */
+  double body_pos[MPCR_MAX_BODY][3];
+  double body_quat[MPCR_MAX_BODY][4];
+  double body_ipos[MPCR_MAX_BODY][3];
+  double body_iquat[MPCR_MAX_BODY][4];
+  double body_mass[MPCR_MAX_BODY];
+  double body_inertia[MPCR_MAX_BODY][3];
+  double body_gravcomp[MPCR_MAX_BODY];
+  double body_invweight0[MPCR_MAX_BODY][2];
+
+  /* joints */
+  int32_t jnt_type[MPCR_MAX_JNT];
+  int32_t jnt_qposadr[MPCR_MAX_JNT];
+  int32_t jnt_dofadr[MPCR_MAX_JNT];
+  int32_t jnt_bodyid[MPCR_MAX_JNT];
+  int32_t jnt_limited[MPCR_MAX_JNT];
+  double jnt_pos[MPCR_MAX_JNT][3];
+  double jnt_axis[MPCR_MAX_JNT][3];
+  double jnt_range[MPCR_MAX_JNT][2];
+  double jnt_solref[MPCR_MAX_JNT][2];
+  double jnt_solimp[MPCR_MAX_JNT][5];
+  double jnt_margin[MPCR_MAX_JNT];
+
+  /* dofs */
+  int32_t dof_bodyid[MPCR_MAX_DOF];
+  int32_t dof_jntid[MPCR_MAX_DOF];
+  int32_t dof_parentid[MPCR_MAX_DOF];
+  int32_t dof_treeid[MPCR_MAX_DOF];
+  double dof_armature[MPCR_MAX_DOF];
+  double dof_damping[MPCR_MAX_DOF];
+  double dof_invweight0[MPCR_MAX_DOF];
+
+  /* reference / template state (mjx_data after forward at qpos0,
+     SBP/mjx_planner.py:105-107) */
+  double qpos0[MPCR_MAX_NQ];
+  double qpos_init[MPCR_MAX_NQ];
+  double qvel_init[MPCR_MAX_DOF];
+
+  /* geoms */
+  int32_t geom_type[MPCR_MAX_GEOM];
+  int32_t geom_bodyid[MPCR_MAX_GEOM];
+  int32_t geom_contype[MPCR_MAX_GEOM];
+  int32_t geom_conaffinity[MPCR_MAX_GEOM];
+  int32_t geom_condim[MPCR_MAX_GEOM];
+  int32_t geom_robot[MPCR_MAX_GEOM];   /* 1 if named robot_0..robot_9      */
+  double geom_pos[MPCR_MAX_GEOM][3];
+  double geom_quat[MPCR_MAX_GEOM][4];
+  double geom_size[MPCR_MAX_GEOM][3];
+  double geom_rbound[MPCR_MAX_GEOM];
+
+  /* sites */
+  int32_t site_bodyid[MPCR_MAX_SITE];
+  double site_pos[MPCR_MAX_SITE][3];
+  double site_quat[MPCR_MAX_SITE][4];
+
+  /* collision pairs (static candidate list after contype/weld/parent/exclude
+     filtering, sorted by narrow-phase function) and their mixed parameters */
+  int32_t pair_geom1[MPCR_MAX_PAIR];
+  int32_t pair_geom2[MPCR_MAX_PAIR];
+  int32_t pair_func[MPCR_MAX_PAIR];
+  int32_t pair_ncon[MPCR_MAX_PAIR];
+  int32_t pair_conadr[MPCR_MAX_PAIR];   /* first contact slot              */
+  int32_t pair_slotadr[MPCR_MAX_PAIR];  /* first robot slot, -1 if unmasked */
+  int32_t pair_condim[MPCR_MAX_PAIR];
+  int32_t pad2;
+  double pair_friction[MPCR_MAX_PAIR];  /* sliding friction (condim 3)     */
+  double pair_solref[MPCR_MAX_PAIR][2];
+  double pair_solimp[MPCR_MAX_PAIR][5];
+  double pair_margin[MPCR_MAX_PAIR];
+  double pair_gap[MPCR_MAX_PAIR];
+
+  /* equality constraints */
+  int32_t eq_type[MPCR_MAX_EQ];
+  int32_t eq_obj1[MPCR_MAX_EQ];
+  int32_t eq_obj2[MPCR_MAX_EQ];
+  int32_t pad3;
+  double eq_data[MPCR_MAX_EQ][5];
+  double eq_solref[MPCR_MAX_EQ][2];
+  double eq_solimp[MPCR_MAX_EQ][5];
+
+  /* planner-controlled dofs: qpos/qvel addresses of the num_dof joints
+     (SBP/mjx_planner.py:254,267-270 use qpos[:num_dof], qvel[:num_dof]) */
+  int32_t ctrl_qposadr[MPCR_MAX_CTRL];
+  int32_t ctrl_dofadr[MPCR_MAX_CTRL];
+} mpcr_model_t;
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCR_MODEL_H_ */

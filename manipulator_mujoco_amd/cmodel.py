@@ -1,0 +1,132 @@
+"""ctypes mirror of ``mpcr_model_t`` (include/mpcr_model.h) and the packer.
+
+Kept field-for-field identical to the C header; ``tests/test_model.py`` checks
+``ctypes.sizeof`` against the size the C library reports.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+MAGIC = 0x4D504352
+VERSION = 3
+
+MAX_BODY, MAX_JNT, MAX_DOF, MAX_NQ = 32, 24, 32, 40
+MAX_GEOM, MAX_SITE, MAX_PAIR, MAX_EQ = 64, 16, 256, 8
+MAX_SLOT, MAX_CTRL = 512, 8
+
+COL_PLANE_CAPSULE, COL_PLANE_BOX, COL_CAPSULE_CAPSULE, COL_CAPSULE_BOX, COL_BOX_BOX = 0, 1, 2, 3, 4
+COL_PLANE_SPHERE, COL_SPHERE_SPHERE, COL_SPHERE_CAPSULE, COL_SPHERE_BOX = 5, 6, 7, 8
+EQ_JOINT = 2
+
+DSBL_EULERDAMP, DSBL_REFSAFE, DSBL_WARMSTART, DSBL_GRAVITY = 1, 2, 4, 8
+DSBL_CONTACT, DSBL_LIMIT, DSBL_EQUALITY, DSBL_PASSIVE, DSBL_FILTERPARENT = 16, 32, 64, 128, 256
+
+_i, _u, _d = ctypes.c_int32, ctypes.c_uint32, ctypes.c_double
+
+
+def _a(t, *dims):
+    for n in reversed(dims):
+        t = t * n
+    return t
+
+
+class mpcr_model_t(ctypes.Structure):
+    _fields_ = [
+        ("magic", _u), ("version", _u), ("nbytes", _u), ("pad0", _u),
+        ("nbody", _i), ("njnt", _i), ("nq", _i), ("nv", _i), ("ngeom", _i), ("nsite", _i),
+        ("npair", _i), ("neq", _i), ("ncon", _i), ("nslot", _i), ("nctrl", _i),
+        ("hande_body", _i), ("tcp_site", _i), ("iterations", _i), ("ls_iterations", _i),
+        ("disableflags", _i), ("integrator", _i), ("cone", _i), ("ntree", _i),
+        ("timestep", _d), ("tolerance", _d), ("ls_tolerance", _d), ("impratio", _d),
+        ("meaninertia", _d), ("gravity", _a(_d, 3)), ("pad1", _d),
+        ("body_parentid", _a(_i, MAX_BODY)), ("body_rootid", _a(_i, MAX_BODY)),
+        ("body_weldid", _a(_i, MAX_BODY)), ("body_jntnum", _a(_i, MAX_BODY)),
+        ("body_jntadr", _a(_i, MAX_BODY)), ("body_dofnum", _a(_i, MAX_BODY)),
+        ("body_dofadr", _a(_i, MAX_BODY)), ("body_dofmask", _a(_u, MAX_BODY)),
+        ("body_pos", _a(_d, MAX_BODY, 3)), ("body_quat", _a(_d, MAX_BODY, 4)),
+        ("body_ipos", _a(_d, MAX_BODY, 3)), ("body_iquat", _a(_d, MAX_BODY, 4)),
+        ("body_mass", _a(_d, MAX_BODY)), ("body_inertia", _a(_d, MAX_BODY, 3)),
+        ("body_gravcomp", _a(_d, MAX_BODY)), ("body_invweight0", _a(_d, MAX_BODY, 2)),
+        ("jnt_type", _a(_i, MAX_JNT)), ("jnt_qposadr", _a(_i, MAX_JNT)),
+        ("jnt_dofadr", _a(_i, MAX_JNT)), ("jnt_bodyid", _a(_i, MAX_JNT)),
+        ("jnt_limited", _a(_i, MAX_JNT)),
+        ("jnt_pos", _a(_d, MAX_JNT, 3)), ("jnt_axis", _a(_d, MAX_JNT, 3)),
+        ("jnt_range", _a(_d, MAX_JNT, 2)), ("jnt_solref", _a(_d, MAX_JNT, 2)),
+        ("jnt_solimp", _a(_d, MAX_JNT, 5)), ("jnt_margin", _a(_d, MAX_JNT)),
+        ("dof_bodyid", _a(_i, MAX_DOF)), ("dof_jntid", _a(_i, MAX_DOF)),
+        ("dof_parentid", _a(_i, MAX_DOF)), ("dof_treeid", _a(_i, MAX_DOF)),
+        ("dof_armature", _a(_d, MAX_DOF)), ("dof_damping", _a(_d, MAX_DOF)),
+        ("dof_invweight0", _a(_d, MAX_DOF)),
+        ("qpos0", _a(_d, MAX_NQ)), ("qpos_init", _a(_d, MAX_NQ)), ("qvel_init", _a(_d, MAX_DOF)),
+        ("geom_type", _a(_i, MAX_GEOM)), ("geom_bodyid", _a(_i, MAX_GEOM)),
+        ("geom_contype", _a(_i, MAX_GEOM)), ("geom_conaffinity", _a(_i, MAX_GEOM)),
+        ("geom_condim", _a(_i, MAX_GEOM)), ("geom_robot", _a(_i, MAX_GEOM)),
+        ("geom_pos", _a(_d, MAX_GEOM, 3)), ("geom_quat", _a(_d, MAX_GEOM, 4)),
+        ("geom_size", _a(_d, MAX_GEOM, 3)), ("geom_rbound", _a(_d, MAX_GEOM)),
+        ("site_bodyid", _a(_i, MAX_SITE)), ("site_pos", _a(_d, MAX_SITE, 3)),
+        ("site_quat", _a(_d, MAX_SITE, 4)),
+        ("pair_geom1", _a(_i, MAX_PAIR)), ("pair_geom2", _a(_i, MAX_PAIR)),
+        ("pair_func", _a(_i, MAX_PAIR)), ("pair_ncon", _a(_i, MAX_PAIR)),
+        ("pair_conadr", _a(_i, MAX_PAIR)), ("pair_slotadr", _a(_i, MAX_PAIR)),
+        ("pair_condim", _a(_i, MAX_PAIR)), ("pad2", _i),
+        ("pair_friction", _a(_d, MAX_PAIR)), ("pair_solref", _a(_d, MAX_PAIR, 2)),
+        ("pair_solimp", _a(_d, MAX_PAIR, 5)), ("pair_margin", _a(_d, MAX_PAIR)),
+        ("pair_gap", _a(_d, MAX_PAIR)),
+        ("eq_type", _a(_i, MAX_EQ)), ("eq_obj1", _a(_i, MAX_EQ)), ("eq_obj2", _a(_i, MAX_EQ)),
+        ("pad3", _i), ("eq_data", _a(_d, MAX_EQ, 5)), ("eq_solref", _a(_d, MAX_EQ, 2)),
+        ("eq_solimp", _a(_d, MAX_EQ, 5)),
+        ("ctrl_qposadr", _a(_i, MAX_CTRL)), ("ctrl_dofadr", _a(_i, MAX_CTRL)),
+    ]
+
+
+_LIMITS = dict(nbody=MAX_BODY, njnt=MAX_JNT, nv=MAX_DOF, nq=MAX_NQ, ngeom=MAX_GEOM,
+               nsite=MAX_SITE, npair=MAX_PAIR, neq=MAX_EQ, nslot=MAX_SLOT, nctrl=MAX_CTRL)
+
+# struct field -> Model attribute (when the names differ)
+_ALIASES = {}
+
+
+def _fill(dst, src):
+    src = np.asarray(src)
+    if src.size == 0:
+        return
+    flat = np.ravel(src)
+    if isinstance(dst[0], ctypes.Array):
+        inner = len(dst[0])
+        rows = flat.reshape(-1, inner)
+        for r in range(rows.shape[0]):
+            for c in range(inner):
+                dst[r][c] = type(dst[r][c])(rows[r, c]) if not isinstance(dst[r][c], float) else float(rows[r, c])
+    else:
+        for k, v in enumerate(flat):
+            dst[k] = int(v) if isinstance(dst[k], int) else float(v)
+
+
+def pack(m) -> mpcr_model_t:
+    for k, lim in _LIMITS.items():
+        if getattr(m, k) > lim:
+            raise ValueError(f"model {k}={getattr(m, k)} exceeds capacity {lim}")
+    s = mpcr_model_t()
+    s.magic = MAGIC
+    s.version = VERSION
+    s.nbytes = ctypes.sizeof(mpcr_model_t)
+    scalars = ("nbody", "njnt", "nq", "nv", "ngeom", "nsite", "npair", "neq", "ncon", "nslot",
+               "nctrl", "hande_body", "tcp_site", "iterations", "ls_iterations", "disableflags",
+               "ntree", "timestep", "tolerance", "ls_tolerance", "impratio", "meaninertia")
+    for k in scalars:
+        setattr(s, k, getattr(m, k))
+    s.integrator = 0
+    s.cone = 0
+    for k in range(3):
+        s.gravity[k] = float(m.gravity[k])
+    for name, _ in mpcr_model_t._fields_:
+        if name in scalars or name.startswith("pad") or name in ("magic", "version", "nbytes",
+                                                                 "gravity", "integrator", "cone"):
+            continue
+        attr = _ALIASES.get(name, name)
+        if hasattr(m, attr):
+            _fill(getattr(s, name), getattr(m, attr))
+    return s

@@ -1,0 +1,577 @@
+// engine.hip — host side of the C ABI (include/mpcr.h): model blobs, the
+// fp32 device model with its derived tables, engines, launches.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mpcr.h"
+#include "mpcr_device.h"
+
+namespace mpcr {
+struct RolloutArgs;
+}
+
+// kernels (rollout.hip)
+#include "rollout.hip"
+
+using namespace mpcr;
+
+struct mpcr_model {
+  mpcr_model_t m;
+};
+
+struct mpcr_engine {
+  int device = 0, max_n = 0, H = 0, nbasis = 0;
+  mpcr_model_t host;
+  DevModel dev;
+  DevModel* d_model = nullptr;
+  float* d_pdot = nullptr;
+  // staging (host-pointer calls)
+  float* d_in = nullptr;
+  float* d_cost = nullptr;
+  float* d_theta = nullptr;
+  float* d_thetadot = nullptr;
+  unsigned long long* d_key = nullptr;
+  int* d_status = nullptr;
+  int* d_idx = nullptr;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) return fail(MPCR_EHIP, "%s: %s", #x, hipGetErrorString(e_));  \
+  } while (0)
+
+extern "C" const char* mpcr_last_error(void) { return g_err.c_str(); }
+extern "C" int mpcr_abi_version(void) { return MPCR_ABI_VERSION; }
+
+extern "C" int mpcr_device_arch(int device, char* buf, int buflen) {
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  snprintf(buf, buflen, "%s", prop.gcnArchName);
+  return MPCR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// models
+
+static int check_model(const mpcr_model_t& m) {
+  if (m.magic != MPCR_MODEL_MAGIC) return fail(MPCR_EMODEL, "bad model magic 0x%x", m.magic);
+  if (m.version != MPCR_MODEL_VERSION) return fail(MPCR_EMODEL, "model version %u != %d", m.version, MPCR_MODEL_VERSION);
+  if (m.nbytes != sizeof(mpcr_model_t)) return fail(MPCR_EMODEL, "model size %u != %zu", m.nbytes, sizeof(mpcr_model_t));
+  if (m.nbody > MPCR_MAX_BODY || m.njnt > MPCR_MAX_JNT || m.nv > MPCR_MAX_DOF || m.nq > MPCR_MAX_NQ ||
+      m.ngeom > MPCR_MAX_GEOM || m.npair > MPCR_MAX_PAIR || m.neq > MPCR_MAX_EQ || m.nctrl > MPCR_MAX_CTRL)
+    return fail(MPCR_EMODEL, "model exceeds blob capacity");
+  if (m.integrator != 0 || m.cone != 0) return fail(MPCR_EMODEL, "only Euler + pyramidal supported");
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_model_from_blob(const void* blob, size_t nbytes, mpcr_model** out) {
+  if (!blob || !out) return fail(MPCR_EINVAL, "null argument");
+  if (nbytes != sizeof(mpcr_model_t)) return fail(MPCR_EMODEL, "blob size %zu != %zu", nbytes, sizeof(mpcr_model_t));
+  auto* h = new mpcr_model;
+  std::memcpy(&h->m, blob, sizeof(mpcr_model_t));
+  int rc = check_model(h->m);
+  if (rc) { delete h; return rc; }
+  *out = h;
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_model_load(const char* path, double timestep, mpcr_model** out) {
+  if (!path || !out) return fail(MPCR_EINVAL, "null argument");
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail(MPCR_EINVAL, "cannot open %s", path);
+  std::vector<char> buf(sizeof(mpcr_model_t) + 1);
+  size_t n = fread(buf.data(), 1, buf.size(), f);
+  fclose(f);
+  int rc = mpcr_model_from_blob(buf.data(), n, out);
+  if (rc) return rc;
+  if (timestep > 0) (*out)->m.timestep = timestep;
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_model_set_timestep(mpcr_model* m, double timestep) {
+  if (!m || !(timestep > 0)) return fail(MPCR_EINVAL, "bad timestep");
+  m->m.timestep = timestep;
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_model_info(const mpcr_model* m, int* nq, int* nv, int* nslot, int* nctrl, int* npair) {
+  if (!m) return fail(MPCR_EINVAL, "null model");
+  if (nq) *nq = m->m.nq;
+  if (nv) *nv = m->m.nv;
+  if (nslot) *nslot = m->m.nslot;
+  if (nctrl) *nctrl = m->m.nctrl;
+  if (npair) *npair = m->m.npair;
+  return MPCR_OK;
+}
+
+extern "C" void mpcr_model_free(mpcr_model* m) { delete m; }
+
+// ---------------------------------------------------------------------------
+// device model
+
+static void h_qmul(double r[4], const double a[4], const double b[4]) {
+  double t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+                 a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+                 a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+                 a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  std::memcpy(r, t, sizeof(t));
+}
+static void h_q2m(double m[9], const double q[4]) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
+}
+static void h_rot(double r[3], const double q[4], const double v[3]) {
+  double m[9];
+  h_q2m(m, q);
+  for (int i = 0; i < 3; i++) r[i] = m[3 * i] * v[0] + m[3 * i + 1] * v[1] + m[3 * i + 2] * v[2];
+}
+
+static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
+  std::memset(&d, 0, sizeof(d));
+  // dynamic bodies (not welded to the world), in topological order
+  std::vector<int> dmap(m.nbody, -1);
+  int nb = 0;
+  for (int b = 1; b < m.nbody; b++)
+    if (m.body_weldid[b] != 0) dmap[b] = nb++;
+  if (nb > DX_NB) return fail(MPCR_EMODEL, "%d moving bodies > %d", nb, DX_NB);
+  if (m.nv > DX_NV) return fail(MPCR_EMODEL, "nv=%d > %d (kernel solve width)", m.nv, DX_NV);
+  if (m.nq > DX_NQ || m.njnt > DX_NJ || m.neq > DX_NEQ || m.nctrl > DX_NCTRL)
+    return fail(MPCR_EMODEL, "model sizes exceed device capacity");
+  // world poses of static bodies (constant)
+  std::vector<double> wpos(3 * m.nbody, 0.0), wquat(4 * m.nbody, 0.0);
+  wquat[0] = 1;
+  for (int b = 1; b < m.nbody; b++) {
+    if (m.body_weldid[b] != 0) continue;
+    int p = m.body_parentid[b];
+    double r[3];
+    h_rot(r, &wquat[4 * p], m.body_pos[b]);
+    for (int k = 0; k < 3; k++) wpos[3 * b + k] = wpos[3 * p + k] + r[k];
+    h_qmul(&wquat[4 * b], &wquat[4 * p], m.body_quat[b]);
+    double n = std::sqrt(wquat[4 * b] * wquat[4 * b] + wquat[4 * b + 1] * wquat[4 * b + 1] +
+                         wquat[4 * b + 2] * wquat[4 * b + 2] + wquat[4 * b + 3] * wquat[4 * b + 3]);
+    for (int k = 0; k < 4; k++) wquat[4 * b + k] /= n;
+  }
+  const bool no_passive = m.disableflags & MPCR_DSBL_PASSIVE;
+  d.nbody = nb;
+  d.njnt = m.njnt;
+  d.nq = m.nq;
+  d.nv = m.nv;
+  d.neq = m.neq;
+  d.nslot = m.nslot;
+  d.nctrl = m.nctrl;
+  d.iterations = m.iterations;
+  d.ls_iterations = m.ls_iterations;
+  d.disableflags = m.disableflags;
+  d.timestep = (float)m.timestep;
+  d.tolerance = (float)m.tolerance;
+  d.ls_tolerance = (float)m.ls_tolerance;
+  d.meaninertia = (float)m.meaninertia;
+  const bool no_grav = m.disableflags & MPCR_DSBL_GRAVITY;
+  for (int k = 0; k < 3; k++) d.gravity[k] = no_grav ? 0.f : (float)m.gravity[k];
+  // trees
+  std::vector<int> roots;
+  std::vector<int> depth(m.nbody, 0);
+  int maxdepth = 0;
+  for (int b = 1; b < m.nbody; b++) {
+    int i = dmap[b];
+    if (i < 0) continue;
+    int p = m.body_parentid[b];
+    int njnt = m.body_jntnum[b];
+    int j = njnt ? m.body_jntadr[b] : -1;
+    if (njnt > 1) return fail(MPCR_EMODEL, "body %d has %d joints (1 supported)", b, njnt);
+    if (j >= 0 && m.jnt_type[j] == MPCR_JNT_BALL) return fail(MPCR_EMODEL, "ball joints not supported");
+    d.body_jnt[i] = j;
+    d.body_kind[i] = j < 0 ? BK_WELD
+                           : (m.jnt_type[j] == MPCR_JNT_FREE ? BK_FREE
+                                                             : (m.jnt_type[j] == MPCR_JNT_HINGE ? BK_HINGE : BK_SLIDE));
+    double bq[4], bp[3];
+    if (dmap[p] < 0) {  // parent static: fold its constant world pose in
+      double r[3];
+      h_rot(r, &wquat[4 * p], m.body_pos[b]);
+      for (int k = 0; k < 3; k++) bp[k] = wpos[3 * p + k] + r[k];
+      h_qmul(bq, &wquat[4 * p], m.body_quat[b]);
+      d.body_anc[i] = -1;
+      depth[b] = 1;
+    } else {
+      std::memcpy(bp, m.body_pos[b], sizeof(bp));
+      std::memcpy(bq, m.body_quat[b], sizeof(bq));
+      d.body_anc[i] = dmap[p];
+      depth[b] = depth[p] + 1;
+    }
+    if (d.body_kind[i] == BK_FREE) { d.body_anc[i] = -1; depth[b] = 1; }
+    maxdepth = depth[b] > maxdepth ? depth[b] : maxdepth;
+    for (int k = 0; k < 3; k++) d.body_bpos[i][k] = (float)bp[k];
+    for (int k = 0; k < 4; k++) d.body_bquat[i][k] = (float)bq[k];
+    for (int k = 0; k < 3; k++) d.body_ipos[i][k] = (float)m.body_ipos[b][k];
+    double R[9];
+    h_q2m(R, m.body_iquat[b]);
+    double I[9];
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++)
+        I[3 * r + c] = R[3 * r] * m.body_inertia[b][0] * R[3 * c] + R[3 * r + 1] * m.body_inertia[b][1] * R[3 * c + 1] +
+                       R[3 * r + 2] * m.body_inertia[b][2] * R[3 * c + 2];
+    d.body_Iloc[i][0] = (float)I[0]; d.body_Iloc[i][1] = (float)I[4]; d.body_Iloc[i][2] = (float)I[8];
+    d.body_Iloc[i][3] = (float)I[1]; d.body_Iloc[i][4] = (float)I[2]; d.body_Iloc[i][5] = (float)I[5];
+    d.body_mass[i] = (float)m.body_mass[b];
+    d.body_gravcomp[i] = no_passive ? 0.f : (float)m.body_gravcomp[b];
+    d.body_invw[i] = (float)m.body_invweight0[b][0];
+    d.body_dofmask[i] = m.body_dofmask[b];
+    int root = m.body_rootid[b];
+    int t = -1;
+    for (size_t k = 0; k < roots.size(); k++)
+      if (roots[k] == root) t = (int)k;
+    if (t < 0) { roots.push_back(root); t = (int)roots.size() - 1; }
+    if (t >= DX_NTREE) return fail(MPCR_EMODEL, "too many kinematic trees");
+    d.body_tree[i] = t;
+    d.tree_mass[t] += (float)m.body_mass[b];
+  }
+  d.ntree = (int)roots.size();
+  for (int t = 0; t < d.ntree; t++)
+    if (d.tree_mass[t] <= 0) d.tree_mass[t] = 1.f;
+  int rounds = 0;
+  while ((1 << rounds) < maxdepth) rounds++;
+  d.jump_rounds = rounds;
+  // subtree masks (device body indices)
+  for (int b = 1; b < m.nbody; b++) {
+    if (dmap[b] < 0) continue;
+    for (int a = b; a > 0; a = m.body_parentid[a])
+      if (dmap[a] >= 0) d.body_submask[dmap[a]] |= 1u << dmap[b];
+  }
+  // joints
+  for (int j = 0; j < m.njnt; j++) {
+    d.jnt_type[j] = m.jnt_type[j];
+    d.jnt_qposadr[j] = m.jnt_qposadr[j];
+    d.jnt_dofadr[j] = m.jnt_dofadr[j];
+    d.jnt_body[j] = dmap[m.jnt_bodyid[j]];
+    d.jnt_limited[j] = m.jnt_limited[j];
+    for (int k = 0; k < 3; k++) { d.jnt_pos[j][k] = (float)m.jnt_pos[j][k]; d.jnt_axis[j][k] = (float)m.jnt_axis[j][k]; }
+    for (int k = 0; k < 2; k++) { d.jnt_range[j][k] = (float)m.jnt_range[j][k]; d.jnt_solref[j][k] = (float)m.jnt_solref[j][k]; }
+    for (int k = 0; k < 5; k++) d.jnt_solimp[j][k] = (float)m.jnt_solimp[j][k];
+    d.jnt_margin[j] = (float)m.jnt_margin[j];
+    d.jnt_qpos0[j] = (float)m.qpos0[m.jnt_qposadr[j]];
+  }
+  // dofs
+  for (int i = 0; i < m.nv; i++) {
+    int j = m.dof_jntid[i];
+    int b = m.dof_bodyid[i];
+    d.dof_body[i] = dmap[b];
+    d.dof_jnt[i] = j;
+    int sub = i - m.jnt_dofadr[j];
+    switch (m.jnt_type[j]) {
+      case MPCR_JNT_HINGE: d.dof_kind[i] = 0; break;
+      case MPCR_JNT_SLIDE: d.dof_kind[i] = 1; break;
+      default: d.dof_kind[i] = sub < 3 ? 2 : 3; break;
+    }
+    d.dof_sub[i] = sub < 3 ? sub : sub - 3;
+    uint32_t cm = 0;
+    for (int a = i; a >= 0; a = m.dof_parentid[a]) cm |= 1u << a;
+    d.dof_chainmask[i] = cm;
+    int p = m.body_parentid[b];
+    uint32_t pm = p > 0 ? m.body_dofmask[p] : 0u;
+    if (m.jnt_type[j] == MPCR_JNT_FREE) {
+      int d0 = m.jnt_dofadr[j];
+      d.dof_velmask[i] = sub < 3 ? 0u : (pm | (7u << d0));
+    } else {
+      d.dof_velmask[i] = m.body_dofmask[b] & ~(1u << i);
+    }
+    d.dof_armature[i] = (float)m.dof_armature[i];
+    d.dof_damping[i] = no_passive ? 0.f : (float)m.dof_damping[i];
+    d.dof_invweight0[i] = (float)m.dof_invweight0[i];
+  }
+  for (int i = 0; i < m.nq; i++) d.qpos_init[i] = (float)m.qpos_init[i];
+  for (int i = 0; i < m.nv; i++) d.qvel_init[i] = (float)m.qvel_init[i];
+  // collision geoms referenced by pairs
+  std::vector<int> gmap(m.ngeom, -1);
+  int ng = 0;
+  for (int p = 0; p < m.npair; p++)
+    for (int g : {m.pair_geom1[p], m.pair_geom2[p]})
+      if (gmap[g] < 0) gmap[g] = ng++;
+  if (ng > DX_NG) return fail(MPCR_EMODEL, "%d collision geoms > %d", ng, DX_NG);
+  d.ngeom = ng;
+  for (int g = 0; g < m.ngeom; g++) {
+    int i = gmap[g];
+    if (i < 0) continue;
+    int b = m.geom_bodyid[g];
+    d.geom_type[i] = m.geom_type[g];
+    d.geom_rbound[i] = (float)m.geom_rbound[g];
+    for (int k = 0; k < 3; k++) d.geom_size[i][k] = (float)m.geom_size[g][k];
+    if (dmap[b] >= 0) {
+      d.geom_body[i] = dmap[b];
+      for (int k = 0; k < 3; k++) d.geom_pos[i][k] = (float)m.geom_pos[g][k];
+      for (int k = 0; k < 4; k++) d.geom_quat[i][k] = (float)m.geom_quat[g][k];
+    } else {  // static geom: store its world pose
+      d.geom_body[i] = -1;
+      double r[3], q[4];
+      h_rot(r, &wquat[4 * b], m.geom_pos[g]);
+      h_qmul(q, &wquat[4 * b], m.geom_quat[g]);
+      for (int k = 0; k < 3; k++) d.geom_pos[i][k] = (float)(wpos[3 * b + k] + r[k]);
+      for (int k = 0; k < 4; k++) d.geom_quat[i][k] = (float)q[k];
+    }
+  }
+  // pairs
+  if (m.npair > DX_NP) return fail(MPCR_EMODEL, "too many pairs");
+  if (m.nslot > DX_NSLOT) return fail(MPCR_EMODEL, "%d masked slots > %d", m.nslot, DX_NSLOT);
+  d.npair = m.npair;
+  for (int p = 0; p < m.npair; p++) {
+    int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+    d.pair_g1[p] = gmap[g1];
+    d.pair_g2[p] = gmap[g2];
+    d.pair_func[p] = m.pair_func[p];
+    d.pair_ncon[p] = m.pair_ncon[p];
+    d.pair_slotadr[p] = m.pair_slotadr[p];
+    d.pair_condim[p] = m.pair_condim[p];
+    d.pair_friction[p] = (float)m.pair_friction[p];
+    d.pair_margin[p] = (float)(m.pair_margin[p] - m.pair_gap[p]);
+    for (int k = 0; k < 2; k++) d.pair_solref[p][k] = (float)m.pair_solref[p][k];
+    for (int k = 0; k < 5; k++) d.pair_solimp[p][k] = (float)m.pair_solimp[p][k];
+    d.pair_diag[p] = (float)(m.body_invweight0[m.geom_bodyid[g1]][0] + m.body_invweight0[m.geom_bodyid[g2]][0]);
+  }
+  // equalities
+  for (int e = 0; e < m.neq; e++) {
+    if (m.eq_type[e] != MPCR_EQ_JOINT) return fail(MPCR_EMODEL, "only joint equalities supported");
+    d.eq_j1[e] = m.eq_obj1[e];
+    d.eq_j2[e] = m.eq_obj2[e];
+    for (int k = 0; k < 5; k++) { d.eq_data[e][k] = (float)m.eq_data[e][k]; d.eq_solimp[e][k] = (float)m.eq_solimp[e][k]; }
+    for (int k = 0; k < 2; k++) d.eq_solref[e][k] = (float)m.eq_solref[e][k];
+    double diag = m.dof_invweight0[m.jnt_dofadr[m.eq_obj1[e]]];
+    if (m.eq_obj2[e] >= 0) diag += m.dof_invweight0[m.jnt_dofadr[m.eq_obj2[e]]];
+    d.eq_diag[e] = (float)diag;
+  }
+  // planner ids
+  d.hande_body = m.hande_body >= 0 ? dmap[m.hande_body] : -1;
+  d.tcp_body = -1;
+  if (m.tcp_site >= 0) {
+    d.tcp_body = dmap[m.site_bodyid[m.tcp_site]];
+    for (int k = 0; k < 3; k++) d.tcp_pos[k] = (float)m.site_pos[m.tcp_site][k];
+  }
+  for (int k = 0; k < m.nctrl; k++) { d.ctrl_qposadr[k] = m.ctrl_qposadr[k]; d.ctrl_dofadr[k] = m.ctrl_dofadr[k]; }
+  return MPCR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// engines
+
+extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, int horizon, const float* pdot,
+                                  int nbasis, mpcr_engine** out) {
+  if (!m || !out || max_n <= 0 || horizon <= 0 || !pdot || nbasis <= 0 || nbasis > 16)
+    return fail(MPCR_EINVAL, "bad engine arguments");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MPCR_ENODEV, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(MPCR_ENODEV, "device %d out of range (%d)", device, ndev);
+  HIPCHK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(MPCR_ENODEV, "device %d is %s; libmpcr is built for gfx950 only", device, prop.gcnArchName);
+  auto* e = new mpcr_engine;
+  e->device = device;
+  e->max_n = max_n;
+  e->H = horizon;
+  e->nbasis = nbasis;
+  e->host = m->m;
+  int rc = build_dev_model(e->host, e->dev);
+  if (rc) { delete e; return rc; }
+  const int nc = e->host.nctrl;
+  const size_t in_cols = (size_t)nc * (horizon > nbasis ? horizon : nbasis);
+  if (hipMalloc(&e->d_model, sizeof(DevModel)) != hipSuccess ||
+      hipMalloc(&e->d_pdot, sizeof(float) * horizon * nbasis) != hipSuccess ||
+      hipMalloc(&e->d_in, sizeof(float) * max_n * in_cols) != hipSuccess ||
+      hipMalloc(&e->d_cost, sizeof(float) * max_n * 4) != hipSuccess ||
+      hipMalloc(&e->d_theta, sizeof(float) * max_n * nc * horizon) != hipSuccess ||
+      hipMalloc(&e->d_thetadot, sizeof(float) * max_n * nc * horizon) != hipSuccess ||
+      hipMalloc(&e->d_key, sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&e->d_status, sizeof(int) * max_n) != hipSuccess ||
+      hipMalloc(&e->d_idx, sizeof(int) * max_n) != hipSuccess) {
+    mpcr_engine_free(e);
+    return fail(MPCR_ENOMEM, "device allocation failed");
+  }
+  if (hipMemcpy(e->d_model, &e->dev, sizeof(DevModel), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(e->d_pdot, pdot, sizeof(float) * horizon * nbasis, hipMemcpyHostToDevice) != hipSuccess) {
+    mpcr_engine_free(e);
+    return fail(MPCR_EHIP, "model upload failed");
+  }
+  *out = e;
+  return MPCR_OK;
+}
+
+extern "C" void mpcr_engine_free(mpcr_engine* e) {
+  if (!e) return;
+  (void)hipFree(e->d_model);
+  (void)hipFree(e->d_pdot);
+  (void)hipFree(e->d_in);
+  (void)hipFree(e->d_cost);
+  (void)hipFree(e->d_theta);
+  (void)hipFree(e->d_thetadot);
+  (void)hipFree(e->d_key);
+  (void)hipFree(e->d_status);
+  (void)hipFree(e->d_idx);
+  delete e;
+}
+
+static int launch_rollout(mpcr_engine* e, const float* in, int layout, int n, const double* q0, const float* w,
+                          const float* ptgt, const float* qtgt, float* cost4, float* theta, float* thetadot,
+                          unsigned long long* key, int index_base, int* status, float* trace_eef,
+                          float* trace_slots, bool reset_key, hipStream_t st) {
+  RolloutArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.m = e->d_model;
+  a.input = in;
+  a.pdot = e->d_pdot;
+  a.cost4 = cost4;
+  a.theta = theta;
+  a.thetadot = thetadot;
+  a.best_key = key;
+  a.status = status;
+  a.trace_eef = trace_eef;
+  a.trace_slots = trace_slots;
+  a.layout = layout;
+  a.n = n;
+  a.H = e->H;
+  a.nbasis = e->nbasis;
+  a.index_base = index_base;
+  for (int k = 0; k < e->host.nctrl; k++) a.q0[k] = (float)q0[k];
+  for (int k = 0; k < 3; k++) { a.w[k] = w[k]; a.ptgt[k] = ptgt[k]; }
+  float qn = std::sqrt(qtgt[0] * qtgt[0] + qtgt[1] * qtgt[1] + qtgt[2] * qtgt[2] + qtgt[3] * qtgt[3]);
+  for (int k = 0; k < 4; k++) a.qtgt[k] = qtgt[k] / qn;
+  if (key && reset_key) hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, key, ~0ull);
+  hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, st, a);
+  HIPCHK(hipGetLastError());
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
+                                 const float* w, const float* ptgt, const float* qtgt, float* cost4, float* theta,
+                                 float* thetadot, uint64_t* best_key, int index_base, int* status, int flags,
+                                 void* stream) {
+  if (!e || !input || !q0 || !w || !ptgt || !qtgt || !cost4) return fail(MPCR_EINVAL, "null argument");
+  if (n < 0 || n > e->max_n) return fail(MPCR_EINVAL, "n=%d outside [0, max_n=%d]", n, e->max_n);
+  if (layout != MPCR_LAYOUT_XI && layout != MPCR_LAYOUT_THETADOT) return fail(MPCR_EINVAL, "bad layout %d", layout);
+  if (n == 0) return MPCR_OK;
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  auto* key = reinterpret_cast<unsigned long long*>(best_key);
+  const int nc = e->host.nctrl;
+  const size_t cols = layout == MPCR_LAYOUT_XI ? (size_t)nc * e->nbasis : (size_t)nc * e->H;
+  if (flags & MPCR_F_DEVICE_PTRS) {
+    int rc = launch_rollout(e, input, layout, n, q0, w, ptgt, qtgt, cost4, theta, thetadot, key, index_base, status,
+                            nullptr, nullptr, (flags & MPCR_F_RESET_BEST) != 0, st);
+    if (rc) return rc;
+    if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
+    return MPCR_OK;
+  }
+  HIPCHK(hipMemcpyAsync(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice, st));
+  int rc = launch_rollout(e, e->d_in, layout, n, q0, w, ptgt, qtgt, e->d_cost, theta ? e->d_theta : nullptr,
+                          thetadot ? e->d_thetadot : nullptr, best_key ? e->d_key : nullptr, index_base,
+                          status ? e->d_status : nullptr, nullptr, nullptr, true, st);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(cost4, e->d_cost, sizeof(float) * 4 * n, hipMemcpyDeviceToHost, st));
+  if (theta) HIPCHK(hipMemcpyAsync(theta, e->d_theta, sizeof(float) * n * nc * e->H, hipMemcpyDeviceToHost, st));
+  if (thetadot)
+    HIPCHK(hipMemcpyAsync(thetadot, e->d_thetadot, sizeof(float) * n * nc * e->H, hipMemcpyDeviceToHost, st));
+  if (best_key) HIPCHK(hipMemcpyAsync(best_key, e->d_key, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  if (status) HIPCHK(hipMemcpyAsync(status, e->d_status, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return MPCR_OK;
+}
+
+// Debug/parity entry (not part of the stable ABI surface): host pointers,
+// also returns the per-step eef pose (n x H x 7) and masked slot distances
+// (n x H x nslot).
+extern "C" int mpcr_rollout_trace(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
+                                  const float* w, const float* ptgt, const float* qtgt, float* cost4, float* theta,
+                                  float* eef, float* slots) {
+  if (!e || !input || !cost4 || n <= 0 || n > e->max_n) return fail(MPCR_EINVAL, "bad trace arguments");
+  HIPCHK(hipSetDevice(e->device));
+  const int nc = e->host.nctrl;
+  const size_t cols = layout == MPCR_LAYOUT_XI ? (size_t)nc * e->nbasis : (size_t)nc * e->H;
+  float *d_eef = nullptr, *d_slots = nullptr;
+  const int nslot = e->host.nslot > 0 ? e->host.nslot : 1;
+  HIPCHK(hipMalloc(&d_eef, sizeof(float) * n * e->H * 7));
+  HIPCHK(hipMalloc(&d_slots, sizeof(float) * n * e->H * nslot));
+  HIPCHK(hipMemcpy(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice));
+  int rc = launch_rollout(e, e->d_in, layout, n, q0, w, ptgt, qtgt, e->d_cost, e->d_theta, nullptr, nullptr, 0,
+                          e->d_status, d_eef, d_slots, false, nullptr);
+  if (rc == 0) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(cost4, e->d_cost, sizeof(float) * 4 * n, hipMemcpyDeviceToHost));
+    if (theta) HIPCHK(hipMemcpy(theta, e->d_theta, sizeof(float) * n * nc * e->H, hipMemcpyDeviceToHost));
+    if (eef) HIPCHK(hipMemcpy(eef, d_eef, sizeof(float) * n * e->H * 7, hipMemcpyDeviceToHost));
+    if (slots) HIPCHK(hipMemcpy(slots, d_slots, sizeof(float) * n * e->H * nslot, hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(d_eef);
+  (void)hipFree(d_slots);
+  return rc;
+}
+
+extern "C" void mpcr_best_key_decode(uint64_t key, int* idx, float* cost) {
+  uint32_t hi = (uint32_t)(key >> 32);
+  if (idx) *idx = (int)(uint32_t)(key & 0xffffffffu);
+  if (cost) {
+    if (hi == 0u) {
+      *cost = NAN;
+    } else {
+      uint32_t u = (hi & 0x80000000u) ? (hi & 0x7fffffffu) : ~hi;
+      float f;
+      std::memcpy(&f, &u, 4);
+      *cost = f;
+    }
+  }
+}
+
+extern "C" int mpcr_argmin(mpcr_engine* e, const float* cost, int stride, int n, int index_base, uint64_t* key_out,
+                           int* idx_out, float* val_out, int flags, void* stream) {
+  if (!e || !cost || n <= 0 || stride <= 0) return fail(MPCR_EINVAL, "bad argmin arguments");
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  const float* dcost = cost;
+  if (!(flags & MPCR_F_DEVICE_PTRS)) {
+    if (n > e->max_n || stride > 4) return fail(MPCR_EINVAL, "host argmin limited to max_n x 4");
+    HIPCHK(hipMemcpyAsync(e->d_cost, cost, sizeof(float) * (size_t)n * stride, hipMemcpyHostToDevice, st));
+    dcost = e->d_cost;
+  }
+  unsigned long long* key = (flags & MPCR_F_DEVICE_PTRS) && key_out ? reinterpret_cast<unsigned long long*>(key_out)
+                                                                    : e->d_key;
+  hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, key, ~0ull);
+  int blocks = (n + 255) / 256;
+  blocks = blocks > 1024 ? 1024 : blocks;
+  hipLaunchKernelGGL(argmin_kernel, dim3(blocks), dim3(256), 0, st, dcost, stride, n, index_base, key);
+  HIPCHK(hipGetLastError());
+  if (idx_out || val_out || (key_out && !(flags & MPCR_F_DEVICE_PTRS))) {
+    uint64_t k;
+    HIPCHK(hipMemcpyAsync(&k, key, sizeof(k), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    mpcr_best_key_decode(k, idx_out, val_out);
+    if (key_out && !(flags & MPCR_F_DEVICE_PTRS)) *key_out = k;
+  } else if (flags & MPCR_F_SYNC) {
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_topk(mpcr_engine* e, const float* cost, int stride, int n, int k, int* idx_out, int flags,
+                         void* stream) {
+  (void)e; (void)cost; (void)stride; (void)n; (void)k; (void)idx_out; (void)flags; (void)stream;
+  return fail(MPCR_EINVAL, "mpcr_topk: not implemented in this build (host argsort is used; SURVEY 8f-2)");
+}

@@ -1,0 +1,1498 @@
+// rollout.hip — fused basis -> H MuJoCo-semantics steps -> cost kernel for
+// gfx950 (CDNA4).  One 64-lane wavefront (one workgroup) owns one candidate
+// rollout for the whole horizon; per step the lanes run in parallel over
+// bodies (kinematics by pointer jumping along the chain), dofs (cdof, RNE,
+// passive), (dof, dof) entries (CRB mass matrix), collision pairs (narrow
+// phase), (contact, dof) entries (contact Jacobians) and constraint rows
+// (impedance, Newton line search).  The two dense SPD solves per step
+// (M and the Newton Hessian, nv <= 16) are done row-per-lane in registers
+// with v_readlane broadcasts: no LDS round trips inside the factorisation.
+//
+// Semantics restated (same definitions as oracle/mpcr_oracle.c):
+//   rollout / output timing  SBP/mjx_planner.py:251-274
+//   cost                     SBP/mjx_planner.py:276-303
+//   mjx.step                 mujoco-mjx 3.3.1 (third party)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mpcr_device.h"
+
+namespace mpcr {
+
+constexpr float kMinVal = 1e-15f;
+constexpr float kMinImp = 0.0001f;
+constexpr float kMaxImp = 0.9999f;
+
+struct RolloutArgs {
+  const DevModel* m;
+  const float* input;
+  const float* pdot;  // H x nbasis
+  float* cost4;
+  float* theta;
+  float* thetadot;
+  unsigned long long* best_key;
+  int* status;
+  float* trace_eef;    // n x H x 7 (debug)
+  float* trace_slots;  // n x H x nslot (debug)
+  int layout, n, H, nbasis, index_base, pad_;
+  float q0[DX_NCTRL];
+  float w[4];
+  float ptgt[4];
+  float qtgt[4];  // normalised
+};
+
+struct __align__(16) Smem {
+  float xi[DX_NCTRL * 16];
+  float qpos[DX_NQ];
+  float qvel[DX_NV];
+  float qacc[DX_NV];
+  float qws[DX_NV];
+  float qfs[DX_NV];  // qfrc_smooth
+  float qas[DX_NV];  // qacc_smooth
+  float vec0[DX_NV];
+  float vec1[DX_NV];
+  float xpos[DX_NB][4];
+  float xquat[DX_NB][4];
+  float xmat[DX_NB][12];
+  float xipos[DX_NB][4];
+  float com[DX_NTREE][4];
+  float cinert[DX_NB][12];
+  float crb[DX_NB][12];
+  float cvel[DX_NB][8];
+  float cfrc[DX_NB][8];
+  float cdof[DX_NV][8];
+  float cdofdot[DX_NV][8];
+  float fvec[DX_NV][8];
+  float M[DX_NV][DX_NV];
+  float Lsh[DX_NV][DX_NV];  // transpose scratch of the register Cholesky
+  float gxpos[DX_NG][4];
+  float gxmat[DX_NG][12];
+  float con_pos[DX_MAXACT][4];
+  float con_frame[DX_MAXACT][12];
+  float con_dist[DX_MAXACT];
+  int con_pair[DX_MAXACT];
+  float J[DX_MAXEFC][DX_NV];
+  float efc_pos[DX_MAXEFC];
+  float efc_D[DX_MAXEFC];
+  float efc_aref[DX_MAXEFC];
+  float efc_jar[DX_MAXEFC];
+  float efc_jv[DX_MAXEFC];
+  float cprev[DX_NSLOT];   // previous-step masked slot distances (cost_c)
+  int efc_src[DX_MAXEFC];  // (kind << 24) | (index << 4) | side
+  int ncon, nefc, trunc, pad_;
+};
+
+// ---------------------------------------------------------------------------
+// wave helpers
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ int wscan_incl(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ void sync() { __syncthreads(); }
+
+// ---------------------------------------------------------------------------
+// small vector math
+
+__device__ __forceinline__ void qmul(float r[4], const float a[4], const float b[4]) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+__device__ __forceinline__ void q2m(float m[9], const float q[4]) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void mv(float r[3], const float m[9], const float v[3]) {
+  float a = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  float b = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  float c = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = a; r[1] = b; r[2] = c;
+}
+__device__ __forceinline__ void mtv(float r[3], const float m[9], const float v[3]) {
+  float a = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  float b = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  float c = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = a; r[1] = b; r[2] = c;
+}
+__device__ __forceinline__ void cross(float r[3], const float a[3], const float b[3]) {
+  float x = a[1] * b[2] - a[2] * b[1];
+  float y = a[2] * b[0] - a[0] * b[2];
+  float z = a[0] * b[1] - a[1] * b[0];
+  r[0] = x; r[1] = y; r[2] = z;
+}
+__device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+// spatial algebra (MuJoCo layout, see oracle/mpcr_oracle.c)
+__device__ __forceinline__ void mul_inert_vec(float r[6], const float* i, const float* v) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+__device__ __forceinline__ void cross_motion(float r[6], const float v[6], const float u[6]) {
+  float a[3], b[3], c[3];
+  cross(a, v, u);
+  cross(b, v, u + 3);
+  cross(c, v + 3, u);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+__device__ __forceinline__ void cross_force(float r[6], const float v[6], const float f[6]) {
+  float a[3], b[3], c[3];
+  cross(a, v, f);
+  cross(b, v + 3, f + 3);
+  cross(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+
+// ---------------------------------------------------------------------------
+// dense SPD solve, row-per-lane in registers.  Lane i (< DX_NV) holds row i
+// of A in a[]; rows >= n must be identity rows.  On return a[] holds row i of
+// the lower Cholesky factor.  x = A^-1 b for b held one value per lane.
+
+__device__ __forceinline__ void chol_rows(float (&a)[DX_NV], int lane) {
+#pragma unroll
+  for (int k = 0; k < DX_NV; k++) {
+    float dkk = sqrtf(fmaxf(rdlane(a[k], k), kMinVal));
+    float lik = lane == k ? dkk : (lane > k ? a[k] / dkk : 0.f);
+    a[k] = lik;
+#pragma unroll
+    for (int j = k + 1; j < DX_NV; j++) {
+      float ljk = rdlane(lik, j);
+      a[j] = fmaf(-lik, ljk, a[j]);
+    }
+  }
+}
+
+// forward/back substitution; L rows in registers, one rhs value per lane.
+// Uses vtmp (LDS, DX_NV floats) to transpose for the back substitution.
+__device__ __forceinline__ float chol_solve(const float (&l)[DX_NV], float b, int lane,
+                                            float (*Lsh)[DX_NV]) {
+  // forward: y_i = (b_i - sum_{k<i} L_ik y_k) / L_ii
+  float acc = b, y = 0.f;
+#pragma unroll
+  for (int k = 0; k < DX_NV; k++) {
+    float yk_l = acc / l[k];  // valid on lane k
+    float yk = rdlane(yk_l, k);
+    if (lane == k) y = yk;
+    if (lane > k) acc = fmaf(-l[k], yk, acc);
+  }
+  // back: x_i = (y_i - sum_{k>i} L_ki x_k) / L_ii ; need column i of L
+  if (lane < DX_NV) {
+#pragma unroll
+    for (int j = 0; j < DX_NV; j++) Lsh[lane][j] = l[j];
+  }
+  sync();
+  float x = 0.f;
+  acc = y;
+  float lii = lane < DX_NV ? Lsh[lane][lane] : 1.f;
+#pragma unroll
+  for (int k = DX_NV - 1; k >= 0; k--) {
+    float xk_l = acc / lii;
+    float xk = rdlane(xk_l, k);
+    if (lane == k) x = xk;
+    if (lane < k) acc = fmaf(-Lsh[k][lane < DX_NV ? lane : 0], xk, acc);
+  }
+  sync();
+  return x;
+}
+
+// ---------------------------------------------------------------------------
+// narrow phase (contact definitions identical to the oracle's)
+
+__device__ __forceinline__ void seg_seg(const float p1[3], const float d1[3], const float p2[3], const float d2[3],
+                                        float* sc, float* tc) {
+  float r[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+  float a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  float s, t;
+  if (a <= kMinVal && e <= kMinVal) { *sc = 0; *tc = 0; return; }
+  if (a <= kMinVal) {
+    s = 0; t = clampf(f / e, 0, 1);
+  } else {
+    float c = dot3(d1, r);
+    if (e <= kMinVal) {
+      t = 0; s = clampf(-c / a, 0, 1);
+    } else {
+      float b = dot3(d1, d2), den = a * e - b * b;
+      s = den > 1e-12f * a * e ? clampf((b * f - c * e) / den, 0, 1) : 0.f;
+      t = (b * s + f) / e;
+      if (t < 0) { t = 0; s = clampf(-c / a, 0, 1); }
+      else if (t > 1) { t = 1; s = clampf((b - c) / a, 0, 1); }
+    }
+  }
+  *sc = s; *tc = t;
+}
+
+__device__ __forceinline__ float point_box(const float p[3], const float h[3], float nl[3], float q[3]) {
+  float out2 = 0, o[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    q[k] = clampf(p[k], -h[k], h[k]);
+    o[k] = q[k] - p[k];
+    out2 += o[k] * o[k];
+  }
+  if (out2 > 0) {
+    float l = sqrtf(out2);
+#pragma unroll
+    for (int k = 0; k < 3; k++) nl[k] = o[k] / l;
+    return l;
+  }
+  int best = 0;
+  float g = fabsf(p[0]) - h[0];
+  if (fabsf(p[1]) - h[1] > g) { g = fabsf(p[1]) - h[1]; best = 1; }
+  if (fabsf(p[2]) - h[2] > g) { g = fabsf(p[2]) - h[2]; best = 2; }
+  float sg = p[best] >= 0 ? 1.f : -1.f;
+  nl[0] = nl[1] = nl[2] = 0;
+  nl[best] = -sg;
+  q[0] = p[0]; q[1] = p[1]; q[2] = p[2];
+  q[best] = sg * h[best];
+  return g;
+}
+
+// out: dist[4], pos[4][3], nrm[4][3]; returns number of slots written
+__device__ __noinline__ int narrow_phase(const DevModel* __restrict__ m, const Smem& s, int p, float dist[4],
+                            float pos[4][3], float nrm[4][3]) {
+  const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
+  const int func = m->pair_func[p];
+  const float* x1 = s.gxpos[g1];
+  const float* x2 = s.gxpos[g2];
+  const float* R1 = s.gxmat[g1];
+  const float* R2 = s.gxmat[g2];
+  const float* s1 = m->geom_size[g1];
+  const float* s2 = m->geom_size[g2];
+#pragma unroll
+  for (int k = 0; k < 4; k++) dist[k] = 1e30f;
+  if (func == 0) {  // plane - capsule
+    float n[3] = {R1[2], R1[5], R1[8]}, ax[3] = {R2[2], R2[5], R2[8]};
+    float r = s2[0], hl = s2[1];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      float sg = k == 0 ? 1.f : -1.f, e[3], dif[3];
+#pragma unroll
+      for (int c = 0; c < 3; c++) { e[c] = x2[c] + sg * hl * ax[c]; dif[c] = e[c] - x1[c]; }
+      float d = dot3(n, dif) - r;
+      dist[k] = d;
+#pragma unroll
+      for (int c = 0; c < 3; c++) { pos[k][c] = e[c] - n[c] * (r + 0.5f * d); nrm[k][c] = n[c]; }
+    }
+    return 2;
+  }
+  if (func == 1) {  // plane - box: 4 deepest corners
+    float n[3] = {R1[2], R1[5], R1[8]};
+    float cd[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      float l[3] = {(c & 1) ? s2[0] : -s2[0], (c & 2) ? s2[1] : -s2[1], (c & 4) ? s2[2] : -s2[2]}, w[3];
+      mv(w, R2, l);
+      cd[c] = n[0] * (x2[0] + w[0] - x1[0]) + n[1] * (x2[1] + w[1] - x1[1]) + n[2] * (x2[2] + w[2] - x1[2]);
+    }
+    int used = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int best = -1;
+      float bd = 0;
+#pragma unroll
+      for (int c = 0; c < 8; c++)
+        if (!((used >> c) & 1) && (best < 0 || cd[c] < bd)) { best = c; bd = cd[c]; }
+      used |= 1 << best;
+      float l[3] = {(best & 1) ? s2[0] : -s2[0], (best & 2) ? s2[1] : -s2[1], (best & 4) ? s2[2] : -s2[2]}, w[3];
+      mv(w, R2, l);
+      dist[k] = bd;
+#pragma unroll
+      for (int c = 0; c < 3; c++) { pos[k][c] = x2[c] + w[c] - n[c] * 0.5f * bd; nrm[k][c] = n[c]; }
+    }
+    return 4;
+  }
+  if (func == 2) {  // capsule - capsule
+    float a1[3] = {R1[2], R1[5], R1[8]}, a2[3] = {R2[2], R2[5], R2[8]};
+    float p1[3], d1[3], p2[3], d2[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      p1[c] = x1[c] - s1[1] * a1[c]; d1[c] = 2 * s1[1] * a1[c];
+      p2[c] = x2[c] - s2[1] * a2[c]; d2[c] = 2 * s2[1] * a2[c];
+    }
+    float sc, tc, n[3], c1[3];
+    seg_seg(p1, d1, p2, d2, &sc, &tc);
+#pragma unroll
+    for (int c = 0; c < 3; c++) { c1[c] = p1[c] + sc * d1[c]; n[c] = p2[c] + tc * d2[c] - c1[c]; }
+    float len = sqrtf(dot3(n, n));
+    if (len < 1e-12f) {
+      float t[3] = {1, 0, 0};
+      if (fabsf(a1[0]) > 0.9f) { t[0] = 0; t[1] = 1; }
+      cross(n, a1, t);
+      float l = sqrtf(dot3(n, n));
+      n[0] /= l; n[1] /= l; n[2] /= l;
+    } else {
+      n[0] /= len; n[1] /= len; n[2] /= len;
+    }
+    float d = len - s1[0] - s2[0];
+    dist[0] = d;
+#pragma unroll
+    for (int c = 0; c < 3; c++) { pos[0][c] = c1[c] + n[c] * (s1[0] + 0.5f * d); nrm[0][c] = n[c]; }
+    return 1;
+  }
+  if (func == 3) {  // capsule - box
+    float ax[3] = {R1[2], R1[5], R1[8]}, r = s1[0], hl = s1[1];
+    const float* h = s2;
+    float A[3], B[3], a[3], dd[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) { A[c] = x1[c] - hl * ax[c] - x2[c]; B[c] = 2 * hl * ax[c]; }
+    mtv(a, R2, A);
+    mtv(dd, R2, B);
+    float tlo = -1.f, thi = 2.f, flo = 0.f, fhi = 0.f;
+    // knots: 0, 1, (+-h_k - a_k)/dd_k inside (0,1)
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      float t;
+      bool ok = true;
+      if (i == 0) t = 0.f;
+      else if (i == 1) t = 1.f;
+      else {
+        int k = (i - 2) >> 1;
+        float sg = ((i - 2) & 1) ? 1.f : -1.f;
+        ok = fabsf(dd[k]) > kMinVal;
+        t = ok ? (sg * h[k] - a[k]) / dd[k] : 0.f;
+        ok = ok && t > 0.f && t < 1.f;
+      }
+      if (ok) {
+        float fp = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          float x = a[k] + t * dd[k], e = fabsf(x) - h[k];
+          if (e > 0) fp += 2.f * dd[k] * (x > 0 ? e : -e);
+        }
+        if (fp < 0) { if (t > tlo) { tlo = t; flo = fp; } }
+        else { if (t < thi) { thi = t; fhi = fp; } }
+      }
+    }
+    float ts;
+    if (tlo < 0) ts = 0.f;
+    else if (thi > 1) ts = 1.f;
+    else ts = fhi - flo > 0 ? tlo - flo * (thi - tlo) / (fhi - flo) : tlo;
+    float pp[3], q[3], nl[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) pp[c] = a[c] + ts * dd[c];
+    float g = point_box(pp, h, nl, q);
+    if (g <= 0) {
+      // deepest point of g(t) = max_k |x_k(t)| - h_k over its kinks
+      float gbest = 1e30f, tbest = 0.f;
+#pragma unroll
+      for (int i = 0; i < 17; i++) {
+        float t;
+        bool ok = true;
+        if (i == 0) t = 0.f;
+        else if (i == 1) t = 1.f;
+        else if (i < 5) {
+          int k = i - 2;
+          ok = fabsf(dd[k]) > kMinVal;
+          t = ok ? -a[k] / dd[k] : 0.f;
+          ok = ok && t > 0.f && t < 1.f;
+        } else {
+          int q4 = i - 5;        // 0..11: pair (ii,jj) x signs
+          int pr = q4 >> 2;      // 0:(0,1) 1:(0,2) 2:(1,2)
+          int ii = pr == 2 ? 1 : 0, jj = pr == 0 ? 1 : 2;
+          float si = (q4 & 2) ? 1.f : -1.f, sj = (q4 & 1) ? 1.f : -1.f;
+          float den = si * dd[ii] - sj * dd[jj];
+          ok = fabsf(den) > kMinVal;
+          t = ok ? (h[ii] - h[jj] - si * a[ii] + sj * a[jj]) / den : 0.f;
+          ok = ok && t > 0.f && t < 1.f;
+        }
+        if (ok) {
+          float gm = -1e30f;
+#pragma unroll
+          for (int k = 0; k < 3; k++) gm = fmaxf(gm, fabsf(a[k] + t * dd[k]) - h[k]);
+          if (gm < gbest) { gbest = gm; tbest = t; }
+        }
+      }
+      ts = tbest;
+#pragma unroll
+      for (int c = 0; c < 3; c++) pp[c] = a[c] + ts * dd[c];
+      g = point_box(pp, h, nl, q);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      if (k == 1) {
+        float t = ts < 0.5f ? 1.f : 0.f;
+#pragma unroll
+        for (int c = 0; c < 3; c++) pp[c] = a[c] + t * dd[c];
+        g = point_box(pp, h, nl, q);
+      }
+      float n[3], pl[3], tmp[3];
+      mv(n, R2, nl);
+#pragma unroll
+      for (int c = 0; c < 3; c++) pl[c] = 0.5f * (pp[c] + r * nl[c] + q[c]);
+      mv(tmp, R2, pl);
+      dist[k] = g - r;
+#pragma unroll
+      for (int c = 0; c < 3; c++) { pos[k][c] = tmp[c] + x2[c]; nrm[k][c] = n[c]; }
+    }
+    return 2;
+  }
+  if (func == 4) {  // box - box: SAT + reference-face clipping
+    float axA[3][3], axB[3][3], t[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) { axA[i][c] = R1[3 * c + i]; axB[i][c] = R2[3 * c + i]; }
+#pragma unroll
+    for (int c = 0; c < 3; c++) t[c] = x2[c] - x1[c];
+    const float* ha = s1;
+    const float* hb = s2;
+    float best_face = -1e30f, best_edge = -1e30f, Lf[3] = {0, 0, 1}, Le[3] = {0, 0, 1};
+    int face_id = -1, edge_i = -1, edge_j = -1;
+#pragma unroll
+    for (int ax = 0; ax < 6; ax++) {
+      const float* L = ax < 3 ? axA[ax] : axB[ax - 3];
+      float ra = 0, rb = 0;
+#pragma unroll
+      for (int k = 0; k < 3; k++) { ra += ha[k] * fabsf(dot3(axA[k], L)); rb += hb[k] * fabsf(dot3(axB[k], L)); }
+      float sep = fabsf(dot3(t, L)) - ra - rb;
+      if (sep > best_face) { best_face = sep; face_id = ax; Lf[0] = L[0]; Lf[1] = L[1]; Lf[2] = L[2]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        float L[3];
+        cross(L, axA[i], axB[j]);
+        float l = sqrtf(dot3(L, L));
+        if (l >= 1e-6f) {
+          L[0] /= l; L[1] /= l; L[2] /= l;
+          float ra = 0, rb = 0;
+#pragma unroll
+          for (int k = 0; k < 3; k++) { ra += ha[k] * fabsf(dot3(axA[k], L)); rb += hb[k] * fabsf(dot3(axB[k], L)); }
+          float sep = fabsf(dot3(t, L)) - ra - rb;
+          if (sep > best_edge) { best_edge = sep; edge_i = i; edge_j = j; Le[0] = L[0]; Le[1] = L[1]; Le[2] = L[2]; }
+        }
+      }
+    float best = fmaxf(best_face, best_edge);
+    dist[0] = best;
+    const float margin = m->pair_margin[p];
+    if (best >= margin) return 4;
+    bool use_edge = edge_i >= 0 && best_edge > 0.95f * best_face + 1e-5f;
+    const float* L = use_edge ? Le : Lf;
+    float sg = dot3(t, L) >= 0 ? 1.f : -1.f;
+    float n[3] = {sg * L[0], sg * L[1], sg * L[2]};
+    if (use_edge) {
+      float pa[3], pb[3], da[3], db[3];
+#pragma unroll
+      for (int c = 0; c < 3; c++) { pa[c] = x1[c]; pb[c] = x2[c]; }
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        if (k != edge_i) {
+          float s_ = dot3(n, axA[k]) >= 0 ? 1.f : -1.f;
+#pragma unroll
+          for (int c = 0; c < 3; c++) pa[c] += s_ * ha[k] * axA[k][c];
+        }
+        if (k != edge_j) {
+          float s_ = dot3(n, axB[k]) >= 0 ? -1.f : 1.f;
+#pragma unroll
+          for (int c = 0; c < 3; c++) pb[c] += s_ * hb[k] * axB[k][c];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        pa[c] -= ha[edge_i] * axA[edge_i][c]; da[c] = 2 * ha[edge_i] * axA[edge_i][c];
+        pb[c] -= hb[edge_j] * axB[edge_j][c]; db[c] = 2 * hb[edge_j] * axB[edge_j][c];
+      }
+      float sc, uc;
+      seg_seg(pa, da, pb, db, &sc, &uc);
+      dist[0] = best_edge;
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        pos[0][c] = 0.5f * (pa[c] + sc * da[c] + pb[c] + uc * db[c]);
+        nrm[0][c] = n[c];
+      }
+      return 4;
+    }
+    const bool refA = face_id < 3;
+    const int fi = refA ? face_id : face_id - 3;
+    const float* cr = refA ? x1 : x2;
+    const float* ci = refA ? x2 : x1;
+    const float* hr = refA ? ha : hb;
+    const float* hi = refA ? hb : ha;
+    float axR[3][3], axI[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) { axR[i][c] = refA ? axA[i][c] : axB[i][c]; axI[i][c] = refA ? axB[i][c] : axA[i][c]; }
+    float nf[3] = {refA ? n[0] : -n[0], refA ? n[1] : -n[1], refA ? n[2] : -n[2]};
+    int ki = 0;
+    float bestdot = -1;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float v = fabsf(dot3(axI[k], nf));
+      if (v > bestdot) { bestdot = v; ki = k; }
+    }
+    float si = dot3(axI[ki], nf) > 0 ? -1.f : 1.f;
+    int u = ki == 0 ? 1 : (ki == 1 ? 2 : 0), v = ki == 0 ? 2 : (ki == 1 ? 0 : 1);
+    float poly[8][3], tmpp[8][3];
+    int np = 4;
+    const float su[4] = {1, -1, -1, 1}, sv[4] = {1, 1, -1, -1};
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+        poly[c][k] = ci[k] + si * hi[ki] * axI[ki][k] + su[c] * hi[u] * axI[u][k] + sv[c] * hi[v] * axI[v][k];
+    for (int pl = 0; pl < 4 && np > 0; pl++) {
+      int ax = (fi + 1 + (pl >> 1)) % 3;
+      float sgn = (pl & 1) ? -1.f : 1.f;
+      float cra = dot3(cr, axR[ax]);
+      int nn = 0;
+      for (int c = 0; c < np; c++) {
+        const int c2 = c + 1 == np ? 0 : c + 1;
+        float dp = sgn * (dot3(poly[c], axR[ax]) - cra) - hr[ax];
+        float dq = sgn * (dot3(poly[c2], axR[ax]) - cra) - hr[ax];
+        if (dp <= 0) { tmpp[nn][0] = poly[c][0]; tmpp[nn][1] = poly[c][1]; tmpp[nn][2] = poly[c][2]; nn++; }
+        if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
+          float wgt = dp / (dp - dq);
+#pragma unroll
+          for (int k = 0; k < 3; k++) tmpp[nn][k] = poly[c][k] + wgt * (poly[c2][k] - poly[c][k]);
+          nn++;
+        }
+      }
+      np = nn;
+      for (int c = 0; c < np; c++) { poly[c][0] = tmpp[c][0]; poly[c][1] = tmpp[c][1]; poly[c][2] = tmpp[c][2]; }
+    }
+    float depth[8];
+    int keep[8], nkeep = 0;
+    for (int c = 0; c < np; c++) {
+      float rel[3] = {poly[c][0] - cr[0], poly[c][1] - cr[1], poly[c][2] - cr[2]};
+      depth[c] = hr[fi] - dot3(rel, nf);
+      if (-depth[c] < margin) keep[nkeep++] = c;
+    }
+    dist[0] = 1e30f;
+    if (nkeep == 0) return 4;
+    int pick[4], npick;
+    if (nkeep <= 4) {
+      for (int c = 0; c < nkeep; c++) pick[c] = keep[c];
+      npick = nkeep;
+    } else {
+      int d0 = 0;
+      for (int c = 1; c < nkeep; c++)
+        if (depth[keep[c]] > depth[keep[d0]]) d0 = c;
+      for (int k = 0; k < 4; k++) pick[k] = keep[(d0 + k * nkeep / 4) % nkeep];
+      npick = 4;
+    }
+    for (int k = 0; k < npick; k++) {
+      int c = pick[k];
+      dist[k] = -depth[c];
+#pragma unroll
+      for (int e = 0; e < 3; e++) { pos[k][e] = poly[c][e] + nf[e] * 0.5f * depth[c]; nrm[k][e] = n[e]; }
+    }
+    return 4;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ void make_frame(float f[9], const float n[3]) {
+  f[0] = n[0]; f[1] = n[1]; f[2] = n[2];
+  float y[3] = {0.f, 1.f, 0.f};
+  if (fabsf(n[1]) >= 0.5f) { y[1] = 0.f; y[2] = 1.f; }
+  float dd = dot3(n, y);
+  y[0] -= dd * n[0]; y[1] -= dd * n[1]; y[2] -= dd * n[2];
+  float ny = sqrtf(dot3(y, y));
+  f[3] = y[0] / ny; f[4] = y[1] / ny; f[5] = y[2] / ny;
+  cross(f + 6, f, f + 3);
+}
+
+__device__ __forceinline__ float impedance(const float* si, float pos, float margin) {
+  float dmin = clampf(si[0], kMinImp, kMaxImp), dmax = clampf(si[1], kMinImp, kMaxImp);
+  float width = si[2], mid = si[3], power = si[4];
+  if (dmin == dmax || width <= kMinVal) return 0.5f * (dmin + dmax);
+  float x = fabsf((pos - margin) / width);
+  if (x >= 1.f) return dmax;
+  if (x <= 0.f) return dmin;
+  float y;
+  if (power == 1.f) y = x;
+  else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
+  else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
+  return dmin + y * (dmax - dmin);
+}
+
+// ---------------------------------------------------------------------------
+// line search point (MJX-style, see oracle)
+
+struct LsPt { float alpha, cost, d0, d1; };
+
+__device__ __forceinline__ void ls_rows(const Smem& s, int lane, float alpha, float& q0, float& q1, float& q2) {
+  q0 = q1 = q2 = 0.f;
+  for (int r = lane; r < s.nefc; r += WAVE) {
+    float jar = s.efc_jar[r], jv = s.efc_jv[r];
+    float x = jar + alpha * jv;
+    if (((s.efc_src[r] >> 24) == 1) || x < 0.f) {
+      float D = s.efc_D[r];
+      q0 += 0.5f * D * jar * jar;
+      q1 += D * jv * jar;
+      q2 += 0.5f * D * jv * jv;
+    }
+  }
+}
+
+__device__ __forceinline__ LsPt ls_make(float alpha, float q0, float q1, float q2) {
+  LsPt p;
+  p.alpha = alpha;
+  p.cost = alpha * alpha * q2 + alpha * q1 + q0;
+  p.d0 = 2.f * alpha * q2 + q1;
+  p.d1 = 2.f * q2 + (q2 == 0.f ? kMinVal : 0.f);
+  return p;
+}
+
+__device__ __forceinline__ LsPt ls_eval(const Smem& s, int lane, const float qg[3], float alpha) {
+  float q0, q1, q2;
+  ls_rows(s, lane, alpha, q0, q1, q2);
+  q0 = wsum(q0) + qg[0];
+  q1 = wsum(q1) + qg[1];
+  q2 = wsum(q2) + qg[2];
+  return ls_make(alpha, q0, q1, q2);
+}
+
+// ---------------------------------------------------------------------------
+// the kernel
+
+__global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
+  __shared__ Smem s;
+  const DevModel* __restrict__ m = args.m;
+  const int lane = threadIdx.x;
+  const int b = blockIdx.x;
+  if (b >= args.n) return;
+  const int H = args.H;
+  const int nv = m->nv, nb = m->nbody, nc = m->nctrl;
+
+  // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
+  for (int i = lane; i < DX_NQ; i += WAVE) s.qpos[i] = i < m->nq ? m->qpos_init[i] : 0.f;
+  if (lane < DX_NV) {
+    s.qvel[lane] = lane < nv ? m->qvel_init[lane] : 0.f;
+    s.qws[lane] = 0.f;
+    s.qacc[lane] = 0.f;
+  }
+  sync();
+  if (lane < nc) s.qpos[m->ctrl_qposadr[lane]] = args.q0[lane];
+  if (args.layout == 0) {
+    const int nx = nc * args.nbasis;
+    for (int i = lane; i < nx; i += WAVE) s.xi[i] = args.input[(size_t)b * nx + i];
+  }
+  sync();
+
+  float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
+  int status = 0;
+
+  for (int t = 0; t < H; t++) {
+    // ---- qvel[:nctrl] = thetadot_t (basis evaluated on the fly) -------------
+    if (lane < nc) {
+      float v;
+      if (args.layout == 0) {
+        v = 0.f;
+        const float* pd = args.pdot + (size_t)t * args.nbasis;
+        for (int k = 0; k < args.nbasis; k++) v = fmaf(pd[k], s.xi[lane * args.nbasis + k], v);
+      } else {
+        v = args.input[(size_t)b * nc * H + lane * H + t];
+      }
+      s.qvel[m->ctrl_dofadr[lane]] = v;
+      if (args.thetadot) args.thetadot[(size_t)b * nc * H + lane * H + t] = v;
+    }
+    sync();
+
+    // ---- kinematics: local pose per body, then pointer jumping ----------------
+    {
+      float q[4] = {1.f, 0.f, 0.f, 0.f}, p[3] = {0.f, 0.f, 0.f};
+      int anc = -1;
+      if (lane < nb) {
+        const int kind = m->body_kind[lane];
+        const int j = m->body_jnt[lane];
+        q[0] = m->body_bquat[lane][0]; q[1] = m->body_bquat[lane][1];
+        q[2] = m->body_bquat[lane][2]; q[3] = m->body_bquat[lane][3];
+        p[0] = m->body_bpos[lane][0]; p[1] = m->body_bpos[lane][1]; p[2] = m->body_bpos[lane][2];
+        anc = m->body_anc[lane];
+        if (kind == BK_FREE) {
+          const int a = m->jnt_qposadr[j];
+          p[0] = s.qpos[a]; p[1] = s.qpos[a + 1]; p[2] = s.qpos[a + 2];
+          q[0] = s.qpos[a + 3]; q[1] = s.qpos[a + 4]; q[2] = s.qpos[a + 5]; q[3] = s.qpos[a + 6];
+          float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+          if (n < kMinVal) { q[0] = 1.f; q[1] = q[2] = q[3] = 0.f; }
+          else { q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n; }
+          anc = -1;
+        } else if (kind == BK_HINGE || kind == BK_SLIDE) {
+          const float qa = s.qpos[m->jnt_qposadr[j]] - m->jnt_qpos0[j];
+          const float* ax = m->jnt_axis[j];
+          float R[9];
+          q2m(R, q);
+          if (kind == BK_SLIDE) {
+            float w[3];
+            mv(w, R, ax);
+            p[0] += w[0] * qa; p[1] += w[1] * qa; p[2] += w[2] * qa;
+          } else {
+            float sn, cs;
+            __sincosf(0.5f * qa, &sn, &cs);
+            float qj[4] = {cs, ax[0] * sn, ax[1] * sn, ax[2] * sn}, Rj[9], c[3], rc[3], d[3], w[3];
+            c[0] = m->jnt_pos[j][0]; c[1] = m->jnt_pos[j][1]; c[2] = m->jnt_pos[j][2];
+            q2m(Rj, qj);
+            mv(rc, Rj, c);
+            d[0] = c[0] - rc[0]; d[1] = c[1] - rc[1]; d[2] = c[2] - rc[2];
+            mv(w, R, d);
+            p[0] += w[0]; p[1] += w[1]; p[2] += w[2];
+            qmul(q, q, qj);
+          }
+        }
+      }
+      for (int r = 0; r < m->jump_rounds; r++) {
+        const int src = anc >= 0 ? anc : lane;
+        float aq[4], ap[3];
+        aq[0] = __shfl(q[0], src); aq[1] = __shfl(q[1], src); aq[2] = __shfl(q[2], src); aq[3] = __shfl(q[3], src);
+        ap[0] = __shfl(p[0], src); ap[1] = __shfl(p[1], src); ap[2] = __shfl(p[2], src);
+        const int aanc = __shfl(anc, src);
+        if (anc >= 0) {
+          float R[9], w[3];
+          q2m(R, aq);
+          mv(w, R, p);
+          p[0] = ap[0] + w[0]; p[1] = ap[1] + w[1]; p[2] = ap[2] + w[2];
+          qmul(q, aq, q);
+          anc = aanc;
+        }
+      }
+      if (lane < nb) {
+        float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
+        float R[9], w[3];
+        q2m(R, q);
+        s.xpos[lane][0] = p[0]; s.xpos[lane][1] = p[1]; s.xpos[lane][2] = p[2];
+        s.xquat[lane][0] = q[0]; s.xquat[lane][1] = q[1]; s.xquat[lane][2] = q[2]; s.xquat[lane][3] = q[3];
+#pragma unroll
+        for (int k = 0; k < 9; k++) s.xmat[lane][k] = R[k];
+        mv(w, R, m->body_ipos[lane]);
+        s.xipos[lane][0] = p[0] + w[0]; s.xipos[lane][1] = p[1] + w[1]; s.xipos[lane][2] = p[2] + w[2];
+      }
+    }
+    sync();
+
+    // ---- geom poses, tree COMs ------------------------------------------------
+    if (lane < m->ngeom) {
+      const int gb = m->geom_body[lane];
+      float gq[4] = {m->geom_quat[lane][0], m->geom_quat[lane][1], m->geom_quat[lane][2], m->geom_quat[lane][3]};
+      float Rg[9];
+      q2m(Rg, gq);
+      if (gb < 0) {
+        s.gxpos[lane][0] = m->geom_pos[lane][0]; s.gxpos[lane][1] = m->geom_pos[lane][1];
+        s.gxpos[lane][2] = m->geom_pos[lane][2];
+#pragma unroll
+        for (int k = 0; k < 9; k++) s.gxmat[lane][k] = Rg[k];
+      } else {
+        float w[3], R[9], Rr[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) R[k] = s.xmat[gb][k];
+        mv(w, R, m->geom_pos[lane]);
+        s.gxpos[lane][0] = s.xpos[gb][0] + w[0]; s.gxpos[lane][1] = s.xpos[gb][1] + w[1];
+        s.gxpos[lane][2] = s.xpos[gb][2] + w[2];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int k = 0; k < 3; k++)
+            Rr[3 * i + k] = R[3 * i] * Rg[k] + R[3 * i + 1] * Rg[3 + k] + R[3 * i + 2] * Rg[6 + k];
+#pragma unroll
+        for (int k = 0; k < 9; k++) s.gxmat[lane][k] = Rr[k];
+      }
+    }
+    for (int tr = 0; tr < m->ntree; tr++) {
+      float mm = (lane < nb && m->body_tree[lane] == tr) ? m->body_mass[lane] : 0.f;
+      float cx = wsum(mm * (lane < nb ? s.xipos[lane][0] : 0.f));
+      float cy = wsum(mm * (lane < nb ? s.xipos[lane][1] : 0.f));
+      float cz = wsum(mm * (lane < nb ? s.xipos[lane][2] : 0.f));
+      if (lane == 0) {
+        float tm = m->tree_mass[tr];
+        s.com[tr][0] = cx / tm; s.com[tr][1] = cy / tm; s.com[tr][2] = cz / tm;
+      }
+    }
+    sync();
+
+    // ---- eef outputs (pre-integration) + pose cost -------------------------
+    if (lane == 0) {
+      float ep[3] = {0.f, 0.f, 0.f}, eq[4] = {1.f, 0.f, 0.f, 0.f};
+      if (m->tcp_body >= 0) {
+        float w[3], R[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) R[k] = s.xmat[m->tcp_body][k];
+        mv(w, R, m->tcp_pos);
+        ep[0] = s.xpos[m->tcp_body][0] + w[0]; ep[1] = s.xpos[m->tcp_body][1] + w[1];
+        ep[2] = s.xpos[m->tcp_body][2] + w[2];
+      }
+      if (m->hande_body >= 0) {
+        eq[0] = s.xquat[m->hande_body][0]; eq[1] = s.xquat[m->hande_body][1];
+        eq[2] = s.xquat[m->hande_body][2]; eq[3] = s.xquat[m->hande_body][3];
+      }
+      float dx = ep[0] - args.ptgt[0], dy = ep[1] - args.ptgt[1], dz = ep[2] - args.ptgt[2];
+      cost_g += sqrtf(dx * dx + dy * dy + dz * dz);
+      float qn = sqrtf(eq[0] * eq[0] + eq[1] * eq[1] + eq[2] * eq[2] + eq[3] * eq[3]);
+      float dq = fabsf((eq[0] * args.qtgt[0] + eq[1] * args.qtgt[1] + eq[2] * args.qtgt[2] + eq[3] * args.qtgt[3]) / qn);
+      cost_r += 2.f * acosf(clampf(dq, -1.f, 1.f));
+      if (args.trace_eef) {
+        float* e = args.trace_eef + ((size_t)b * H + t) * 7;
+        e[0] = ep[0]; e[1] = ep[1]; e[2] = ep[2]; e[3] = eq[0]; e[4] = eq[1]; e[5] = eq[2]; e[6] = eq[3];
+      }
+    }
+
+    // ---- cinert, cdof ---------------------------------------------------------
+    if (lane < nb) {
+      const int tr = m->body_tree[lane];
+      float R[9], I[6];
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = s.xmat[lane][k];
+      const float* Il = m->body_Iloc[lane];
+      // I_w = R Il R^T
+      float A[9] = {Il[0], Il[3], Il[4], Il[3], Il[1], Il[5], Il[4], Il[5], Il[2]}, RA[9];
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) RA[3 * i + k] = R[3 * i] * A[k] + R[3 * i + 1] * A[3 + k] + R[3 * i + 2] * A[6 + k];
+      I[0] = RA[0] * R[0] + RA[1] * R[1] + RA[2] * R[2];
+      I[1] = RA[3] * R[3] + RA[4] * R[4] + RA[5] * R[5];
+      I[2] = RA[6] * R[6] + RA[7] * R[7] + RA[8] * R[8];
+      I[3] = RA[0] * R[3] + RA[1] * R[4] + RA[2] * R[5];
+      I[4] = RA[0] * R[6] + RA[1] * R[7] + RA[2] * R[8];
+      I[5] = RA[3] * R[6] + RA[4] * R[7] + RA[5] * R[8];
+      const float mass = m->body_mass[lane];
+      float d[3] = {s.xipos[lane][0] - s.com[tr][0], s.xipos[lane][1] - s.com[tr][1],
+                    s.xipos[lane][2] - s.com[tr][2]};
+      const float dd = dot3(d, d);
+      float* c = s.cinert[lane];
+      c[0] = I[0] + mass * (dd - d[0] * d[0]);
+      c[1] = I[1] + mass * (dd - d[1] * d[1]);
+      c[2] = I[2] + mass * (dd - d[2] * d[2]);
+      c[3] = I[3] - mass * d[0] * d[1];
+      c[4] = I[4] - mass * d[0] * d[2];
+      c[5] = I[5] - mass * d[1] * d[2];
+      c[6] = mass * d[0]; c[7] = mass * d[1]; c[8] = mass * d[2];
+      c[9] = mass;
+    }
+    if (lane < nv) {
+      const int bd = m->dof_body[lane], kind = m->dof_kind[lane];
+      const int tr = m->body_tree[bd];
+      float* c = s.cdof[lane];
+      float R[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = s.xmat[bd][k];
+      if (kind == 2) {  // free translation
+        c[0] = c[1] = c[2] = 0.f;
+        const int k = m->dof_sub[lane];
+        c[3] = k == 0 ? 1.f : 0.f;
+        c[4] = k == 1 ? 1.f : 0.f;
+        c[5] = k == 2 ? 1.f : 0.f;
+      } else {
+        float ax[3], anchor[3];
+        if (kind == 3) {
+          const int k = m->dof_sub[lane];
+          ax[0] = R[k]; ax[1] = R[3 + k]; ax[2] = R[6 + k];
+          anchor[0] = s.xpos[bd][0]; anchor[1] = s.xpos[bd][1]; anchor[2] = s.xpos[bd][2];
+        } else {
+          const int j = m->dof_jnt[lane];
+          float w[3];
+          mv(ax, R, m->jnt_axis[j]);
+          mv(w, R, m->jnt_pos[j]);
+          anchor[0] = s.xpos[bd][0] + w[0]; anchor[1] = s.xpos[bd][1] + w[1]; anchor[2] = s.xpos[bd][2] + w[2];
+        }
+        if (kind == 1) {
+          c[0] = c[1] = c[2] = 0.f;
+          c[3] = ax[0]; c[4] = ax[1]; c[5] = ax[2];
+        } else {
+          float off[3] = {s.com[tr][0] - anchor[0], s.com[tr][1] - anchor[1], s.com[tr][2] - anchor[2]}, cr[3];
+          cross(cr, ax, off);
+          c[0] = ax[0]; c[1] = ax[1]; c[2] = ax[2];
+          c[3] = cr[0]; c[4] = cr[1]; c[5] = cr[2];
+        }
+      }
+    }
+    sync();
+
+    // ---- CRB, velocity, RNE + gravcomp (subtree sums by bitmask) -----------
+    for (int idx = lane; idx < nb * 10; idx += WAVE) {
+      const int bb = idx / 10, k = idx - bb * 10;
+      uint32_t sm = m->body_submask[bb];
+      float acc = 0.f;
+      while (sm) {
+        const int c = __builtin_ctz(sm);
+        sm &= sm - 1;
+        acc += s.cinert[c][k];
+      }
+      s.crb[bb][k] = acc;
+    }
+    if (lane < nb) {  // cvel = sum over the chain of cdof * qvel
+      uint32_t dm = m->body_dofmask[lane];
+      float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      while (dm) {
+        const int d = __builtin_ctz(dm);
+        dm &= dm - 1;
+        const float qd = s.qvel[d];
+#pragma unroll
+        for (int k = 0; k < 6; k++) v[k] = fmaf(s.cdof[d][k], qd, v[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 6; k++) s.cvel[lane][k] = v[k];
+    }
+    if (lane < nv) {  // cdof_dot = cvel_before x cdof (0 for free translation)
+      uint32_t dm = m->dof_velmask[lane];
+      float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, r[6];
+      while (dm) {
+        const int d = __builtin_ctz(dm);
+        dm &= dm - 1;
+        const float qd = s.qvel[d];
+#pragma unroll
+        for (int k = 0; k < 6; k++) v[k] = fmaf(s.cdof[d][k], qd, v[k]);
+      }
+      cross_motion(r, v, s.cdof[lane]);
+      const bool zero = m->dof_kind[lane] == 2;
+#pragma unroll
+      for (int k = 0; k < 6; k++) s.cdofdot[lane][k] = zero ? 0.f : r[k];
+    }
+    sync();
+    if (lane < nv) {  // f_i = crb[body(i)] * cdof_i
+      float f[6];
+      mul_inert_vec(f, s.crb[m->dof_body[lane]], s.cdof[lane]);
+#pragma unroll
+      for (int k = 0; k < 6; k++) s.fvec[lane][k] = f[k];
+    }
+    if (lane < nb) {  // cfrc_body = I*cacc + v x* (I v) - gravcomp wrench
+      uint32_t dm = m->body_dofmask[lane];
+      float a[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
+      while (dm) {
+        const int d = __builtin_ctz(dm);
+        dm &= dm - 1;
+        const float qd = s.qvel[d];
+#pragma unroll
+        for (int k = 0; k < 6; k++) a[k] = fmaf(s.cdofdot[d][k], qd, a[k]);
+      }
+      float f[6], iv[6], vf[6], cv[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) cv[k] = s.cvel[lane][k];
+      mul_inert_vec(f, s.cinert[lane], a);
+      mul_inert_vec(iv, s.cinert[lane], cv);
+      cross_force(vf, cv, iv);
+      const float gc = m->body_gravcomp[lane] * m->body_mass[lane];
+      const int tr = m->body_tree[lane];
+      float F[3] = {-m->gravity[0] * gc, -m->gravity[1] * gc, -m->gravity[2] * gc};
+      float rr[3] = {s.xipos[lane][0] - s.com[tr][0], s.xipos[lane][1] - s.com[tr][1],
+                     s.xipos[lane][2] - s.com[tr][2]}, tq[3];
+      cross(tq, rr, F);
+      s.cfrc[lane][0] = f[0] + vf[0] - tq[0];
+      s.cfrc[lane][1] = f[1] + vf[1] - tq[1];
+      s.cfrc[lane][2] = f[2] + vf[2] - tq[2];
+      s.cfrc[lane][3] = f[3] + vf[3] - F[0];
+      s.cfrc[lane][4] = f[4] + vf[4] - F[1];
+      s.cfrc[lane][5] = f[5] + vf[5] - F[2];
+    }
+    sync();
+    // mass matrix entries (chain-masked) + bias forces
+    for (int idx = lane; idx < DX_NV * DX_NV; idx += WAVE) {
+      const int i = idx >> 4, j = idx & 15;
+      float v = 0.f;
+      if (i < nv && j < nv) {
+        if ((m->dof_chainmask[i] >> j) & 1u) {
+#pragma unroll
+          for (int k = 0; k < 6; k++) v = fmaf(s.cdof[j][k], s.fvec[i][k], v);
+        } else if ((m->dof_chainmask[j] >> i) & 1u) {
+#pragma unroll
+          for (int k = 0; k < 6; k++) v = fmaf(s.cdof[i][k], s.fvec[j][k], v);
+        }
+        if (i == j) v += m->dof_armature[i];
+      } else if (i == j) {
+        v = 1.f;
+      }
+      s.M[i][j] = v;
+    }
+    if (lane < nv) {
+      uint32_t sm = m->body_submask[m->dof_body[lane]];
+      float f[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      while (sm) {
+        const int c = __builtin_ctz(sm);
+        sm &= sm - 1;
+#pragma unroll
+        for (int k = 0; k < 6; k++) f[k] += s.cfrc[c][k];
+      }
+      float bias = 0.f;
+#pragma unroll
+      for (int k = 0; k < 6; k++) bias = fmaf(s.cdof[lane][k], f[k], bias);
+      s.qfs[lane] = -bias - m->dof_damping[lane] * s.qvel[lane];
+    } else if (lane < DX_NV) {
+      s.qfs[lane] = 0.f;
+    }
+    sync();
+
+    // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
+    float Lm[DX_NV];
+    {
+#pragma unroll
+      for (int j = 0; j < DX_NV; j++) Lm[j] = lane < DX_NV ? s.M[lane][j] : (lane == j ? 1.f : 0.f);
+      chol_rows(Lm, lane);
+      float rhs = lane < DX_NV ? s.qfs[lane] : 0.f;
+      float x = chol_solve(Lm, rhs, lane, s.Lsh);
+      if (lane < DX_NV) s.qas[lane] = lane < nv ? x : 0.f;
+    }
+    sync();
+
+    // ---- collision: lanes over pairs; cost_c on masked slots; compaction ----
+    if (lane == 0) { s.ncon = 0; s.trunc = 0; }
+    sync();
+    for (int k = 0; k * WAVE < m->npair; k++) {
+      const int p = lane + k * WAVE;
+      float dist[4], pos[4][3], nrm[4][3];
+      int nslot = 0, act = 0;
+      if (p < m->npair) {
+        const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
+        bool run = true;
+        if (m->pair_slotadr[p] < 0 && m->geom_type[g1] != 0) {
+          float dx = s.gxpos[g2][0] - s.gxpos[g1][0], dy = s.gxpos[g2][1] - s.gxpos[g1][1],
+                dz = s.gxpos[g2][2] - s.gxpos[g1][2];
+          run = sqrtf(dx * dx + dy * dy + dz * dz) <= m->geom_rbound[g1] + m->geom_rbound[g2] + m->pair_margin[p];
+        }
+        if (run) nslot = narrow_phase(m, s, p, dist, pos, nrm);
+        else {
+#pragma unroll
+          for (int c = 0; c < 4; c++) dist[c] = 1e30f;
+        }
+        const int sa = m->pair_slotadr[p];
+        if (sa >= 0) {
+          const int ns = m->pair_ncon[p];
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            if (c < ns) {
+              const float d = dist[c];
+              if (d < 0.f) cost_c += 1.f;
+              if (t > 0) cost_c += fmaxf(s.cprev[sa + c] * (1.f - 0.005f) - d, 0.f);
+              s.cprev[sa + c] = d;
+              if (args.trace_slots) args.trace_slots[((size_t)b * H + t) * m->nslot + sa + c] = d;
+            }
+          }
+        }
+        if (!(m->disableflags & 16)) {
+#pragma unroll
+          for (int c = 0; c < 4; c++)
+            if (c < nslot && dist[c] < m->pair_margin[p]) act++;
+        }
+      }
+      // append active contacts
+      const int incl = wscan_incl(act, lane);
+      const int base = s.ncon;
+      const int total = __shfl(incl, WAVE - 1);
+      int o = base + incl - act;
+      if (act) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          if (c < nslot && dist[c] < m->pair_margin[p]) {
+            if (o < DX_MAXACT) {
+              float f[9];
+              make_frame(f, nrm[c]);
+              s.con_pos[o][0] = pos[c][0]; s.con_pos[o][1] = pos[c][1]; s.con_pos[o][2] = pos[c][2];
+#pragma unroll
+              for (int e = 0; e < 9; e++) s.con_frame[o][e] = f[e];
+              s.con_dist[o] = dist[c];
+              s.con_pair[o] = p;
+            }
+            o++;
+          }
+        }
+      }
+      sync();
+      if (lane == 0) {
+        s.ncon = base + total;
+      }
+      sync();
+    }
+    if (lane == 0 && s.ncon > DX_MAXACT) { s.trunc = 1; s.ncon = DX_MAXACT; }
+    sync();
+
+    // ---- constraint rows: equality, limits, contacts ------------------------
+    {
+      const int neq = (m->disableflags & 64) ? 0 : m->neq;
+      int nlim_l = 0, lsides = 0;
+      if (lane < m->njnt && !(m->disableflags & 32) && m->jnt_limited[lane] &&
+          (m->jnt_type[lane] == 2 || m->jnt_type[lane] == 3)) {
+        const float q = s.qpos[m->jnt_qposadr[lane]];
+        if (q - m->jnt_range[lane][0] < m->jnt_margin[lane]) { nlim_l++; lsides |= 1; }
+        if (m->jnt_range[lane][1] - q < m->jnt_margin[lane]) { nlim_l++; lsides |= 2; }
+      }
+      const int lim_incl = wscan_incl(nlim_l, lane);
+      const int nlim = __shfl(lim_incl, WAVE - 1);
+      int ncr = 0;
+      if (lane < s.ncon) ncr = m->pair_condim[s.con_pair[lane]] == 1 ? 1 : 4;
+      const int con_incl = wscan_incl(ncr, lane);
+      const int ncrow = __shfl(con_incl, WAVE - 1);
+      int nefc = neq + nlim + ncrow;
+      // capacity: drop trailing contacts that do not fit
+      int keep_con = s.ncon;
+      if (nefc > DX_MAXEFC) {
+        // largest prefix of contacts whose rows fit
+        const int room = DX_MAXEFC - neq - nlim;
+        const bool fits = con_incl <= room;
+        const unsigned long long bal = __ballot(lane < s.ncon && fits);
+        keep_con = __popcll(bal);
+        const int rows_kept = keep_con > 0 ? __shfl(con_incl, keep_con - 1) : 0;
+        nefc = neq + nlim + rows_kept;
+        if (lane == 0) s.trunc = 1;
+      }
+      // row sources
+      if (lane < neq) s.efc_src[lane] = (1 << 24) | (lane << 4);
+      if (nlim_l) {
+        int o = neq + lim_incl - nlim_l;
+        if (lsides & 1) s.efc_src[o++] = (2 << 24) | (lane << 4) | 0;
+        if (lsides & 2) s.efc_src[o++] = (2 << 24) | (lane << 4) | 1;
+      }
+      if (lane < keep_con) {
+        int o = neq + nlim + con_incl - ncr;
+        for (int r = 0; r < ncr; r++) s.efc_src[o + r] = (3 << 24) | (lane << 4) | r;
+      }
+      if (lane == 0) s.nefc = nefc;
+      sync();
+      // Jacobian entries: (row, dof) for equality/limit rows
+      const int nsimple = neq + nlim;
+      for (int idx = lane; idx < nsimple * DX_NV; idx += WAVE) {
+        const int r = idx >> 4, i = idx & 15;
+        const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
+        float v = 0.f;
+        if (kind == 1) {
+          const int j1 = m->eq_j1[id], j2 = m->eq_j2[id];
+          if (i == m->jnt_dofadr[j1]) v += 1.f;
+          if (j2 >= 0 && i == m->jnt_dofadr[j2]) {
+            const float* c = m->eq_data[id];
+            const float dif = s.qpos[m->jnt_qposadr[j2]] - m->jnt_qpos0[j2];
+            v -= c[1] + dif * (2.f * c[2] + dif * (3.f * c[3] + dif * 4.f * c[4]));
+          }
+        } else if (i == m->jnt_dofadr[id]) {
+          v = side == 0 ? 1.f : -1.f;
+        }
+        s.J[r][i] = v;
+      }
+      // contact Jacobians: (contact, dof)
+      for (int idx = lane; idx < keep_con * DX_NV; idx += WAVE) {
+        const int c = idx >> 4, i = idx & 15;
+        const int p = s.con_pair[c];
+        const int b1 = m->geom_body[m->pair_g1[p]], b2 = m->geom_body[m->pair_g2[p]];
+        float jd[3] = {0.f, 0.f, 0.f};
+        if (i < nv) {
+          const float* cd = s.cdof[i];
+#pragma unroll
+          for (int side = 0; side < 2; side++) {
+            const int bb = side == 0 ? b1 : b2;
+            if (bb >= 0 && ((m->body_dofmask[bb] >> i) & 1u)) {
+              const int tr = m->body_tree[bb];
+              float r[3] = {s.con_pos[c][0] - s.com[tr][0], s.con_pos[c][1] - s.com[tr][1],
+                            s.con_pos[c][2] - s.com[tr][2]}, cr[3];
+              cross(cr, cd, r);
+              const float sg = side == 0 ? -1.f : 1.f;
+              jd[0] += sg * (cd[3] + cr[0]); jd[1] += sg * (cd[4] + cr[1]); jd[2] += sg * (cd[5] + cr[2]);
+            }
+          }
+        }
+        const float* f = s.con_frame[c];
+        const float jn = f[0] * jd[0] + f[1] * jd[1] + f[2] * jd[2];
+        // locate this contact's first row
+        const int cond = m->pair_condim[p];
+        // row offset = neq + nlim + (rows of contacts before c)
+        int off = neq + nlim;
+        for (int cc = 0; cc < c; cc++) off += m->pair_condim[s.con_pair[cc]] == 1 ? 1 : 4;
+        if (cond == 1) {
+          s.J[off][i] = jn;
+        } else {
+          const float mu = m->pair_friction[p];
+          const float jt1 = f[3] * jd[0] + f[4] * jd[1] + f[5] * jd[2];
+          const float jt2 = f[6] * jd[0] + f[7] * jd[1] + f[8] * jd[2];
+          s.J[off + 0][i] = jn + mu * jt1;
+          s.J[off + 1][i] = jn - mu * jt1;
+          s.J[off + 2][i] = jn + mu * jt2;
+          s.J[off + 3][i] = jn - mu * jt2;
+        }
+      }
+      sync();
+      // row parameters: vel, imp, D, aref
+      for (int r = lane; r < nefc; r += WAVE) {
+        const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
+        float pos, margin, diag;
+        const float* sref;
+        const float* simp;
+        if (kind == 1) {
+          const int j1 = m->eq_j1[id], j2 = m->eq_j2[id];
+          const float* c = m->eq_data[id];
+          const float q1 = s.qpos[m->jnt_qposadr[j1]] - m->jnt_qpos0[j1];
+          if (j2 >= 0) {
+            const float dif = s.qpos[m->jnt_qposadr[j2]] - m->jnt_qpos0[j2];
+            pos = q1 - (c[0] + dif * (c[1] + dif * (c[2] + dif * (c[3] + dif * c[4]))));
+          } else {
+            pos = q1 - c[0];
+          }
+          margin = 0.f;
+          diag = m->eq_diag[id];
+          sref = m->eq_solref[id];
+          simp = m->eq_solimp[id];
+        } else if (kind == 2) {
+          const float q = s.qpos[m->jnt_qposadr[id]];
+          pos = side == 0 ? q - m->jnt_range[id][0] : m->jnt_range[id][1] - q;
+          margin = m->jnt_margin[id];
+          diag = m->dof_invweight0[m->jnt_dofadr[id]];
+          sref = m->jnt_solref[id];
+          simp = m->jnt_solimp[id];
+        } else {
+          const int p = s.con_pair[id];
+          pos = s.con_dist[id];
+          margin = m->pair_margin[p];
+          const float mu = m->pair_friction[p];
+          diag = m->pair_condim[p] == 1 ? m->pair_diag[p] : m->pair_diag[p] * (1.f + mu * mu);
+          sref = m->pair_solref[p];
+          simp = m->pair_solimp[p];
+        }
+        float vel = 0.f;
+#pragma unroll
+        for (int i = 0; i < DX_NV; i++) vel = fmaf(s.J[r][i], s.qvel[i], vel);
+        const float imp = impedance(simp, pos, margin);
+        const float R = fmaxf((1.f - imp) / imp * diag, kMinVal);
+        float tc = sref[0], dr = sref[1];
+        const float dmax = clampf(simp[1], kMinImp, kMaxImp);
+        float K, B;
+        if (tc > 0.f) {
+          if (!(m->disableflags & 2)) tc = fmaxf(tc, 2.f * m->timestep);
+          K = 1.f / (dmax * dmax * tc * tc * dr * dr);
+          B = 2.f / (dmax * tc);
+        } else {
+          K = -tc / (dmax * dmax);
+          B = -dr / dmax;
+        }
+        s.efc_D[r] = 1.f / R;
+        s.efc_aref[r] = -B * vel - K * imp * (pos - margin);
+        s.efc_pos[r] = pos;
+      }
+      sync();
+    }
+    if (s.trunc) status |= 1;
+
+    // ---- Newton solver (primal), MJX-style line search ------------------------
+    {
+      const int nefc = s.nefc;
+      float qacc_l = lane < DX_NV ? s.qas[lane] : 0.f;  // this lane's dof value
+      if (nefc > 0) {
+        // warm start: better of qacc_warmstart and qacc_smooth
+        float cw = 0.f, cs = 0.f;
+        if (!(m->disableflags & 4)) {
+#pragma unroll
+          for (int pass = 0; pass < 2; pass++) {
+            const float* x = pass == 0 ? s.qws : s.qas;
+            float ma = 0.f;
+            if (lane < nv) {
+#pragma unroll
+              for (int j = 0; j < DX_NV; j++) ma = fmaf(s.M[lane][j], x[j], ma);
+            }
+            float g = lane < nv ? (ma - s.qfs[lane]) * (x[lane] - s.qas[lane]) : 0.f;
+            float c = 0.f;
+            for (int r = lane; r < nefc; r += WAVE) {
+              float jar = -s.efc_aref[r];
+#pragma unroll
+              for (int i = 0; i < DX_NV; i++) jar = fmaf(s.J[r][i], x[i], jar);
+              if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) c += s.efc_D[r] * jar * jar;
+            }
+            const float tot = 0.5f * wsum(g) + 0.5f * wsum(c);
+            if (pass == 0) cw = tot; else cs = tot;
+          }
+          if (cw < cs && lane < DX_NV) qacc_l = s.qws[lane];
+        }
+        if (lane < DX_NV) s.qacc[lane] = qacc_l;
+        sync();
+        const float scale = 1.f / (m->meaninertia * (float)(nv > 1 ? nv : 1));
+        float prev_cost = 3.4e38f;
+        for (int it = 0;; it++) {
+          // Ma, jar, cost, grad
+          float ma = 0.f;
+          if (lane < nv) {
+#pragma unroll
+            for (int j = 0; j < DX_NV; j++) ma = fmaf(s.M[lane][j], s.qacc[j], ma);
+          }
+          float cc = 0.f;
+          for (int r = lane; r < nefc; r += WAVE) {
+            float jar = -s.efc_aref[r];
+#pragma unroll
+            for (int i = 0; i < DX_NV; i++) jar = fmaf(s.J[r][i], s.qacc[i], jar);
+            s.efc_jar[r] = jar;
+            if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) cc += s.efc_D[r] * jar * jar;
+          }
+          const float gauss = wsum(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
+          const float cost = 0.5f * gauss + 0.5f * wsum(cc);
+          sync();
+          float grad = 0.f;
+          if (lane < nv) {
+            float qc = 0.f;
+            for (int r = 0; r < nefc; r++) {
+              const float jar = s.efc_jar[r];
+              if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) qc = fmaf(s.J[r][lane], -s.efc_D[r] * jar, qc);
+            }
+            grad = ma - s.qfs[lane] - qc;
+          }
+          const float gn = sqrtf(wsum(grad * grad));
+          if (it >= m->iterations || scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance) break;
+          // Hessian rows: H = M + J^T D_active J
+          float h[DX_NV];
+#pragma unroll
+          for (int j = 0; j < DX_NV; j++) h[j] = lane < DX_NV ? s.M[lane][j] : (lane == j ? 1.f : 0.f);
+          if (lane < nv) {
+            for (int r = 0; r < nefc; r++) {
+              const float jar = s.efc_jar[r];
+              if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) {
+                const float c = s.efc_D[r] * s.J[r][lane];
+#pragma unroll
+                for (int j = 0; j < DX_NV; j++) h[j] = fmaf(c, s.J[r][j], h[j]);
+              }
+            }
+          }
+          chol_rows(h, lane);
+          const float mg = chol_solve(h, lane < nv ? grad : 0.f, lane, s.Lsh);
+          const float search = lane < nv ? -mg : 0.f;
+          if (lane < DX_NV) s.vec1[lane] = search;
+          sync();
+          // Mv, jv, quadratic coefficients
+          float mvv = 0.f;
+          if (lane < nv) {
+#pragma unroll
+            for (int j = 0; j < DX_NV; j++) mvv = fmaf(s.M[lane][j], s.vec1[j], mvv);
+          }
+          for (int r = lane; r < nefc; r += WAVE) {
+            float jv = 0.f;
+#pragma unroll
+            for (int i = 0; i < DX_NV; i++) jv = fmaf(s.J[r][i], s.vec1[i], jv);
+            s.efc_jv[r] = jv;
+          }
+          const float sn = sqrtf(wsum(search * search));
+          const float gtol = m->tolerance * m->ls_tolerance * sn * m->meaninertia * (float)(nv > 1 ? nv : 1);
+          float qg[3];
+          qg[0] = 0.5f * gauss;
+          qg[1] = wsum(lane < nv ? search * (ma - s.qfs[lane]) : 0.f);
+          qg[2] = 0.5f * wsum(search * mvv);
+          sync();
+          LsPt p0 = ls_eval(s, lane, qg, 0.f);
+          LsPt lo = ls_eval(s, lane, qg, p0.alpha - p0.d0 / p0.d1);
+          LsPt hi;
+          if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
+          bool swap = true;
+          for (int ls = 0; ls < m->ls_iterations; ls++) {
+            if (!swap) break;
+            if (lo.d0 < 0.f && lo.d0 > -gtol) break;
+            if (hi.d0 > 0.f && hi.d0 < gtol) break;
+            LsPt lo_next = ls_eval(s, lane, qg, lo.alpha - lo.d0 / lo.d1);
+            LsPt hi_next = ls_eval(s, lane, qg, hi.alpha - hi.d0 / hi.d1);
+            LsPt mid = ls_eval(s, lane, qg, 0.5f * (lo.alpha + hi.alpha));
+            const bool s1 = lo.d0 > 0.f || lo.d0 < lo_next.d0;
+            if (s1) lo = lo_next;
+            const bool s2 = mid.d0 < 0.f && lo.d0 < mid.d0;
+            if (s2) lo = mid;
+            const bool s3 = hi.d0 < 0.f || hi.d0 > hi_next.d0;
+            if (s3) hi = hi_next;
+            const bool s4 = mid.d0 > 0.f && hi.d0 > mid.d0;
+            if (s4) hi = mid;
+            swap = s1 || s2 || s3 || s4;
+          }
+          const bool improved = lo.cost < p0.cost || hi.cost < p0.cost;
+          const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+          if (improved && lane < DX_NV) s.qacc[lane] = s.qacc[lane] + alpha * s.vec1[lane];
+          prev_cost = cost;
+          sync();
+        }
+      } else {
+        if (lane < DX_NV) s.qacc[lane] = qacc_l;
+        sync();
+      }
+    }
+
+    // ---- Euler: qvel += dt qacc; integrate qpos; warm start -----------------
+    {
+      const float dt = m->timestep;
+      if (lane < nv) {
+        s.qvel[lane] = s.qvel[lane] + dt * s.qacc[lane];
+        s.qws[lane] = s.qacc[lane];
+      }
+      sync();
+      if (lane < m->njnt) {
+        const int a = m->jnt_qposadr[lane], v = m->jnt_dofadr[lane], type = m->jnt_type[lane];
+        if (type == 0) {
+          s.qpos[a] += dt * s.qvel[v];
+          s.qpos[a + 1] += dt * s.qvel[v + 1];
+          s.qpos[a + 2] += dt * s.qvel[v + 2];
+          float w[3] = {s.qvel[v + 3], s.qvel[v + 4], s.qvel[v + 5]};
+          float q[4] = {s.qpos[a + 3], s.qpos[a + 4], s.qpos[a + 5], s.qpos[a + 6]};
+          const float wn = sqrtf(dot3(w, w));
+          const float ang = wn * dt;
+          if (ang > kMinVal) {
+            float sn, cs;
+            __sincosf(0.5f * ang, &sn, &cs);
+            float dq[4] = {cs, w[0] / wn * sn, w[1] / wn * sn, w[2] / wn * sn};
+            qmul(q, q, dq);
+          }
+          float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+          s.qpos[a + 3] = q[0] / n; s.qpos[a + 4] = q[1] / n; s.qpos[a + 5] = q[2] / n; s.qpos[a + 6] = q[3] / n;
+        } else if (type == 2 || type == 3) {
+          s.qpos[a] += dt * s.qvel[v];
+        }
+      }
+      sync();
+      if (lane < nc && args.theta) args.theta[(size_t)b * nc * H + lane * H + t] = s.qpos[m->ctrl_qposadr[lane]];
+    }
+  }
+
+  // ---- final reductions, outputs ----------------------------------------------
+  cost_c = wsum(cost_c);
+  bool finite = true;
+  if (lane < m->nq) finite = isfinite(s.qpos[lane]);
+  finite = __all(finite);
+  if (!finite) status |= 2;
+  if (lane == 0) {
+    const float cost = args.w[0] * cost_g + args.w[1] * cost_r + args.w[2] * cost_c;
+    args.cost4[4 * (size_t)b + 0] = cost;
+    args.cost4[4 * (size_t)b + 1] = cost_g;
+    args.cost4[4 * (size_t)b + 2] = cost_r;
+    args.cost4[4 * (size_t)b + 3] = cost_c;
+    if (args.status) args.status[b] = status;
+    if (args.best_key) {
+      const uint32_t u = __float_as_uint(cost);
+      uint32_t key = isnan(cost) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
+      const unsigned long long k64 = ((unsigned long long)key << 32) | (uint32_t)(args.index_base + b);
+      atomicMin(args.best_key, k64);
+    }
+  }
+}
+
+// argmin with NaN-first / first-index semantics over cost[i*stride]
+__global__ void __launch_bounds__(256) argmin_kernel(const float* __restrict__ cost, int stride, int n, int base,
+                                                     unsigned long long* key) {
+  unsigned long long best = ~0ull;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float c = cost[(size_t)i * stride];
+    const uint32_t u = __float_as_uint(c);
+    const uint32_t k = isnan(c) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
+    const unsigned long long k64 = ((unsigned long long)k << 32) | (uint32_t)(base + i);
+    best = k64 < best ? k64 : best;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long other = __shfl_xor(best, o);
+    best = other < best ? other : best;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMin(key, best);
+}
+
+__global__ void fill_u64(unsigned long long* p, unsigned long long v) { *p = v; }
+
+}  // namespace mpcr

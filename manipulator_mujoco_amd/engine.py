@@ -1,0 +1,137 @@
+"""Python handle on a libmpcr engine (one compiled model on one GPU).
+
+``Engine.rollout_cost`` is the fused hot path: Bernstein basis -> H physics
+steps -> cost, one wavefront per candidate.
+Accepts either torch device tensors (zero-copy, launched on the current
+torch stream) or host numpy arrays (staged through the engine's buffers).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import MPCR_F_DEVICE_PTRS, MPCR_F_RESET_BEST, MPCR_LAYOUT_THETADOT, MPCR_LAYOUT_XI, check
+
+
+def _f32p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+class Model:
+    """Host model handle (``mpcr_model``) built from a compiled model."""
+
+    def __init__(self, compiled):
+        lib = _lib.load()
+        self.compiled = compiled
+        blob = compiled.to_blob()
+        self._blob = ctypes.create_string_buffer(blob, len(blob))
+        h = ctypes.c_void_p()
+        check(lib.mpcr_model_from_blob(self._blob, len(blob), ctypes.byref(h)))
+        self.handle = h
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            _lib.load().mpcr_model_free(self.handle)
+            self.handle = None
+
+
+class Engine:
+    def __init__(self, compiled_model, num_steps: int, max_n: int, pdot: np.ndarray, device: int = 0):
+        lib = _lib.load()
+        self.model = Model(compiled_model)
+        self.H = int(num_steps)
+        self.max_n = int(max_n)
+        self.nctrl = int(compiled_model.nctrl)
+        self.nslot = int(compiled_model.nslot)
+        pdot = np.ascontiguousarray(pdot, dtype=np.float32)
+        if pdot.shape[0] != self.H:
+            raise ValueError(f"pdot has {pdot.shape[0]} rows, expected num_steps={self.H}")
+        self.nbasis = pdot.shape[1]
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        check(lib.mpcr_engine_create(self.model.handle, self.device, self.max_n, self.H, pdot.ctypes.data,
+                                     self.nbasis, ctypes.byref(h)))
+        self.handle = h
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            _lib.load().mpcr_engine_free(self.handle)
+            self.handle = None
+
+    @staticmethod
+    def _vec(x, n, dtype):
+        a = np.zeros(n, dtype=dtype)
+        x = np.asarray(x, dtype=dtype).reshape(-1)
+        a[: x.size] = x
+        return a
+
+    def rollout_cost(self, inp, layout: int, q0, w, ptgt, qtgt, cost4=None, theta=None, thetadot=None,
+                     best_key=None, index_base: int = 0, status=None, reset_best: bool = True, stream=None):
+        """Run the fused rollout.
+
+        torch path: ``inp``/outputs are CUDA tensors (float32, contiguous);
+        ``best_key`` an int64 tensor of one element.  numpy path: host arrays.
+        Returns cost4 (and fills the optional outputs in place).
+        """
+        lib = _lib.load()
+        q0 = self._vec(q0, 8, np.float64)
+        w = self._vec(w, 3, np.float32)
+        pt = self._vec(ptgt, 3, np.float32)
+        qt = self._vec(qtgt, 4, np.float32)
+        dp = ctypes.POINTER(ctypes.c_double)
+        try:
+            import torch
+            is_torch = isinstance(inp, torch.Tensor)
+        except ImportError:  # pragma: no cover
+            is_torch = False
+        n = int(inp.shape[0])
+        if is_torch:
+            import torch
+            if not inp.is_cuda or inp.dtype != torch.float32 or not inp.is_contiguous():
+                raise ValueError("input must be a contiguous float32 CUDA tensor")
+            if cost4 is None:
+                cost4 = torch.empty((n, 4), dtype=torch.float32, device=inp.device)
+            ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+            st = stream if stream is not None else torch.cuda.current_stream(inp.device).cuda_stream
+            flags = MPCR_F_DEVICE_PTRS | (MPCR_F_RESET_BEST if reset_best else 0)
+            check(lib.mpcr_rollout_cost(self.handle, ptr(inp), layout, n, q0.ctypes.data_as(dp), _f32p(w),
+                                        _f32p(pt), _f32p(qt), ptr(cost4), ptr(theta), ptr(thetadot),
+                                        ptr(best_key), int(index_base), ptr(status), flags, ctypes.c_void_p(st)))
+            return cost4
+        inp = np.ascontiguousarray(inp, dtype=np.float32)
+        if cost4 is None:
+            cost4 = np.zeros((n, 4), dtype=np.float32)
+        key = np.zeros(1, dtype=np.uint64) if best_key is not None else None
+        hp = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None  # noqa: E731
+        check(lib.mpcr_rollout_cost(self.handle, hp(inp), layout, n, q0.ctypes.data_as(dp), _f32p(w), _f32p(pt),
+                                    _f32p(qt), hp(cost4), hp(theta), hp(thetadot), hp(key), int(index_base),
+                                    hp(status), 0, None))
+        if best_key is not None:
+            best_key[...] = key
+        return cost4
+
+    def trace(self, inp, layout: int, q0, w, ptgt, qtgt):
+        """Debug/parity run (host arrays): cost4, theta, per-step eef pose, masked slot distances."""
+        lib = _lib.load()
+        inp = np.ascontiguousarray(inp, dtype=np.float32)
+        n = inp.shape[0]
+        q0 = self._vec(q0, 8, np.float64)
+        w = self._vec(w, 3, np.float32)
+        pt = self._vec(ptgt, 3, np.float32)
+        qt = self._vec(qtgt, 4, np.float32)
+        cost4 = np.zeros((n, 4), dtype=np.float32)
+        theta = np.zeros((n, self.nctrl * self.H), dtype=np.float32)
+        eef = np.zeros((n, self.H, 7), dtype=np.float32)
+        slots = np.zeros((n, self.H, max(self.nslot, 1)), dtype=np.float32)
+        check(lib.mpcr_rollout_trace(self.handle, inp.ctypes.data_as(ctypes.c_void_p), layout, n,
+                                     q0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), _f32p(w), _f32p(pt),
+                                     _f32p(qt), cost4.ctypes.data_as(ctypes.c_void_p),
+                                     theta.ctypes.data_as(ctypes.c_void_p), eef.ctypes.data_as(ctypes.c_void_p),
+                                     slots.ctypes.data_as(ctypes.c_void_p)))
+        return dict(cost4=cost4, theta=theta, eef=eef, slots=slots[:, :, : self.nslot])
+
+
+__all__ = ["Engine", "Model", "MPCR_LAYOUT_XI", "MPCR_LAYOUT_THETADOT"]

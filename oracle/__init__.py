@@ -1,0 +1,99 @@
+"""CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this package.  The product path
+(``manipulator_mujoco_amd``) never imports, links or executes anything here.
+
+* ``liboracle.so`` (built from ``mpcr_oracle.c`` by ``make``): fp64 scalar C
+  restatement of the rollout + MuJoCo step + cost (see the header of
+  ``mpcr_oracle.c`` for what is pinned and what is "parity unpinned");
+* ``cem_np``: numpy transliterations of the reference's pure-algebra planner
+  pieces (basis, projection, cost, elite, mean/cov update).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def build(force: bool = False) -> str:
+    path = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "mpcr_oracle.c")
+    if force or not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE], stdout=subprocess.DEVNULL)
+    return path
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = ctypes.CDLL(build())
+        dp = ctypes.POINTER(ctypes.c_double)
+        _LIB.oracle_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, dp,
+                                        dp, dp, dp]
+        _LIB.oracle_rollout.restype = ctypes.c_int
+        _LIB.oracle_step.argtypes = [ctypes.c_void_p, dp, dp, dp, dp, dp, dp, dp, dp, dp,
+                                     ctypes.POINTER(ctypes.c_int)]
+        _LIB.oracle_step.restype = ctypes.c_int
+        _LIB.oracle_model_size.restype = ctypes.c_int
+    return _LIB
+
+
+def _p(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def rollout(model, thetadot, q0, w, ptgt, qtgt, want_theta=True, want_slots=False, want_eef=False):
+    """fp64 oracle rollout; thetadot is (n, nctrl*H) joint-major."""
+    s = model.to_struct()
+    td = np.ascontiguousarray(thetadot, dtype=np.float64)
+    n = td.shape[0]
+    nc = model.nctrl
+    H = td.shape[1] // nc
+    cost4 = np.zeros((n, 4))
+    theta = np.zeros((n, nc * H)) if want_theta else None
+    slots = np.zeros((n, H, max(model.nslot, 1))) if want_slots else None
+    eef = np.zeros((n, H, 7)) if want_eef else None
+    q0 = np.ascontiguousarray(q0, dtype=np.float64)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    pt = np.ascontiguousarray(ptgt, dtype=np.float64)
+    qt = np.ascontiguousarray(qtgt, dtype=np.float64)
+    st = lib().oracle_rollout(ctypes.byref(s), n, H, _p(td), _p(q0), _p(w), _p(pt), _p(qt), _p(cost4),
+                              _p(theta), _p(slots), _p(eef))
+    if st < 0:
+        raise RuntimeError(f"oracle_rollout failed ({st})")
+    out = dict(cost4=cost4, theta=theta, status=st)
+    if want_slots:
+        out["slots"] = slots[:, :, :model.nslot]
+    if want_eef:
+        out["eef"] = eef
+    return out
+
+
+def step(model, qpos, qvel, qacc_ws):
+    """One mj_step restatement; returns a dict of the intermediate quantities."""
+    s = model.to_struct()
+    nv = model.nv
+    qpos = np.array(qpos, dtype=np.float64)
+    qvel = np.array(qvel, dtype=np.float64)
+    qws = np.array(qacc_ws, dtype=np.float64)
+    M = np.zeros((nv, nv))
+    bias = np.zeros(nv)
+    pas = np.zeros(nv)
+    qacc = np.zeros(nv)
+    eef = np.zeros(7)
+    dist = np.zeros(max(model.ncon, 1))
+    nefc = ctypes.c_int(0)
+    st = lib().oracle_step(ctypes.byref(s), _p(qpos), _p(qvel), _p(qws), _p(M), _p(bias), _p(pas), _p(qacc),
+                           _p(eef), _p(dist), ctypes.byref(nefc))
+    return dict(qpos=qpos, qvel=qvel, qacc_warmstart=qws, M=M, qfrc_bias=bias, qfrc_passive=pas, qacc=qacc,
+                eef=eef, dist=dist[:model.ncon], nefc=nefc.value, status=st)

@@ -1,0 +1,1251 @@
+/*
+ * mpcr_oracle.c — CPU restatement (fp64, scalar C) of the reference's hot
+ * path, used ONLY as the parity checker (tests/, __graft_entry__.smoke(),
+ * bench.py's cpu_baseline leg).  Never linked into libmpcr.
+ *
+ * What it restates:
+ *   - the rollout / output timing of compute_rollout_single + mjx_step
+ *     (SBP/mjx_planner.py:251-274): qvel[:6] <- thetadot_t, step, emit
+ *     qpos[:6] post-integration and xquat[hande], site_xpos[tcp],
+ *     contact.dist[mask] pre-integration (from forward);
+ *   - compute_cost_single (SBP/mjx_planner.py:276-303);
+ *   - mjx.step (third-party mujoco-mjx 3.3.1, called at :108,256; not in
+ *     /root/reference): kinematics, COM quantities, CRB mass matrix with
+ *     armature, RNE bias forces, passive damping + gravcomp, narrow-phase
+ *     contacts, pyramidal contact / limit / joint-equality constraints with
+ *     solref/solimp impedance, Newton solver (iterations=1, ls_iterations=5,
+ *     warm start = better of qacc_warmstart and qacc_smooth), semi-implicit
+ *     Euler (eulerdamp disabled).
+ *
+ * PARITY STATUS: MuJoCo/MJX are not importable or buildable here
+ * (SURVEY.md §0.2, §8c), so the physics restatement is pinned only by the
+ * reference's own logged CPU-MuJoCo run (SBP/data/theta.csv + thetadot.csv,
+ * tests/test_oracle_replay.py) and by analytic invariants; contact slot
+ * layout and solver details are "parity unpinned" (DESIGN.md §Oracle).
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/mpcr_model.h"
+
+#define NB MPCR_MAX_BODY
+#define NV MPCR_MAX_DOF
+#define MAXCON (4 * MPCR_MAX_PAIR)
+#define MAXEFC 512
+#define MINVAL 1e-15
+#define MINIMP 0.0001
+#define MAXIMP 0.9999
+
+typedef struct {
+  double dist, pos[3], frame[9];
+  int pair, active;
+} ocontact;
+
+typedef struct {
+  /* state */
+  double qpos[MPCR_MAX_NQ], qvel[NV], qacc[NV], qacc_warmstart[NV];
+  /* position-dependent */
+  double xpos[NB][3], xquat[NB][4], xmat[NB][9], xipos[NB][3], ximat[NB][9];
+  double xanchor[MPCR_MAX_JNT][3], xaxis[MPCR_MAX_JNT][3];
+  double subtree_com[NB][3], cinert[NB][10], crb[NB][10], cdof[NV][6];
+  double geom_xpos[MPCR_MAX_GEOM][3], geom_xmat[MPCR_MAX_GEOM][9];
+  double site_xpos[MPCR_MAX_SITE][3];
+  double M[NV][NV], L[NV][NV];
+  /* velocity-dependent */
+  double cvel[NB][6], cdof_dot[NV][6];
+  double qfrc_bias[NV], qfrc_passive[NV], qfrc_smooth[NV], qacc_smooth[NV];
+  /* contacts (all slots) */
+  int ncon;
+  ocontact con[MAXCON];
+  /* constraints */
+  int nefc, efc_eq[MAXEFC];
+  double efc_J[MAXEFC][NV], efc_pos[MAXEFC], efc_margin[MAXEFC], efc_D[MAXEFC];
+  double efc_aref[MAXEFC], efc_diag[MAXEFC], efc_vel[MAXEFC];
+  double efc_solref[MAXEFC][2], efc_solimp[MAXEFC][5];
+  int efc_trunc; /* constraint rows dropped for capacity (should stay 0) */
+} odata;
+
+/* ------------------------------------------------------------------------ */
+/* small math                                                                */
+
+static void q2m(const double q[4], double m[9]) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
+}
+static void qmul(double r[4], const double a[4], const double b[4]) {
+  double t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+                 a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+                 a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+                 a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  memcpy(r, t, sizeof(t));
+}
+static void qnorm(double q[4]) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  for (int i = 0; i < 4; i++) q[i] /= n;
+}
+static void mulmv(double r[3], const double m[9], const double v[3]) {
+  double t[3] = {m[0] * v[0] + m[1] * v[1] + m[2] * v[2], m[3] * v[0] + m[4] * v[1] + m[5] * v[2],
+                 m[6] * v[0] + m[7] * v[1] + m[8] * v[2]};
+  memcpy(r, t, sizeof(t));
+}
+static void mulmtv(double r[3], const double m[9], const double v[3]) {
+  double t[3] = {m[0] * v[0] + m[3] * v[1] + m[6] * v[2], m[1] * v[0] + m[4] * v[1] + m[7] * v[2],
+                 m[2] * v[0] + m[5] * v[1] + m[8] * v[2]};
+  memcpy(r, t, sizeof(t));
+}
+static void mulmm(double r[9], const double a[9], const double b[9]) {
+  double t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+  memcpy(r, t, sizeof(t));
+}
+static void cross3(double r[3], const double a[3], const double b[3]) {
+  double t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+  memcpy(r, t, sizeof(t));
+}
+static double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static double norm3(const double a[3]) { return sqrt(dot3(a, a)); }
+static void axisangle(double q[4], const double ax[3], double ang) {
+  double s = sin(0.5 * ang);
+  q[0] = cos(0.5 * ang); q[1] = ax[0] * s; q[2] = ax[1] * s; q[3] = ax[2] * s;
+}
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+/* spatial algebra, MuJoCo layout: motion/force = [angular(3); linear(3)] and
+   10-vector inertia {Ixx,Iyy,Izz,Ixy,Ixz,Iyz, m*cx,m*cy,m*cz, m} about the
+   tree's subtree_com (mju_mulInertVec / mju_crossMotion / mju_crossForce). */
+static void mul_inert_vec(double r[6], const double i[10], const double v[6]) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+static void cross_motion(double r[6], const double v[6], const double u[6]) {
+  double a[3], b[3], c[3];
+  cross3(a, v, u);
+  cross3(b, v, u + 3);
+  cross3(c, v + 3, u);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+static void cross_force(double r[6], const double v[6], const double f[6]) {
+  double a[3], b[3], c[3];
+  cross3(a, v, f);
+  cross3(b, v + 3, f + 3);
+  cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+
+/* dense Cholesky (lower) of the leading n x n block; returns 0 on success */
+static int chol(double L[NV][NV], const double A[NV][NV], int n) {
+  for (int j = 0; j < n; j++) {
+    double s = A[j][j];
+    for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
+    if (s <= MINVAL) s = MINVAL;
+    L[j][j] = sqrt(s);
+    for (int i = j + 1; i < n; i++) {
+      double t = A[i][j];
+      for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
+      L[i][j] = t / L[j][j];
+    }
+    for (int i = 0; i < j; i++) L[i][j] = 0;
+  }
+  return 0;
+}
+static void chol_solve(double x[NV], const double L[NV][NV], const double b[NV], int n) {
+  double y[NV];
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = y[i];
+    for (int k = i + 1; k < n; k++) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* kinematics + COM quantities + CRB (mj_kinematics, mj_comPos, mj_crb)      */
+
+static void kinematics(const mpcr_model_t* m, odata* d) {
+  d->xpos[0][0] = d->xpos[0][1] = d->xpos[0][2] = 0;
+  d->xquat[0][0] = 1; d->xquat[0][1] = d->xquat[0][2] = d->xquat[0][3] = 0;
+  q2m(d->xquat[0], d->xmat[0]);
+  memcpy(d->xipos[0], d->xpos[0], sizeof(d->xpos[0]));
+  memcpy(d->ximat[0], d->xmat[0], sizeof(d->xmat[0]));
+  for (int b = 1; b < m->nbody; b++) {
+    int p = m->body_parentid[b];
+    double pos[3], quat[4], tmp[3];
+    int j0 = m->body_jntadr[b], nj = m->body_jntnum[b];
+    if (nj > 0 && m->jnt_type[j0] == MPCR_JNT_FREE) {
+      int a = m->jnt_qposadr[j0];
+      memcpy(pos, d->qpos + a, 3 * sizeof(double));
+      memcpy(quat, d->qpos + a + 3, 4 * sizeof(double));
+      qnorm(quat);
+      memcpy(d->xanchor[j0], pos, sizeof(pos));
+      d->xaxis[j0][0] = 0; d->xaxis[j0][1] = 0; d->xaxis[j0][2] = 1;
+    } else {
+      mulmv(tmp, d->xmat[p], m->body_pos[b]);
+      for (int k = 0; k < 3; k++) pos[k] = d->xpos[p][k] + tmp[k];
+      qmul(quat, d->xquat[p], m->body_quat[b]);
+      for (int j = j0; j < j0 + nj; j++) {
+        double R[9], qa = d->qpos[m->jnt_qposadr[j]] - m->qpos0[m->jnt_qposadr[j]];
+        q2m(quat, R);
+        mulmv(d->xaxis[j], R, m->jnt_axis[j]);
+        mulmv(tmp, R, m->jnt_pos[j]);
+        for (int k = 0; k < 3; k++) d->xanchor[j][k] = tmp[k] + pos[k];
+        if (m->jnt_type[j] == MPCR_JNT_SLIDE) {
+          for (int k = 0; k < 3; k++) pos[k] += d->xaxis[j][k] * qa;
+        } else if (m->jnt_type[j] == MPCR_JNT_HINGE) {
+          double ql[4];
+          axisangle(ql, m->jnt_axis[j], qa);
+          qmul(quat, quat, ql);
+          q2m(quat, R);
+          mulmv(tmp, R, m->jnt_pos[j]);
+          for (int k = 0; k < 3; k++) pos[k] = d->xanchor[j][k] - tmp[k];
+        }
+      }
+      qnorm(quat);
+    }
+    memcpy(d->xpos[b], pos, sizeof(pos));
+    memcpy(d->xquat[b], quat, sizeof(quat));
+    q2m(quat, d->xmat[b]);
+    mulmv(tmp, d->xmat[b], m->body_ipos[b]);
+    for (int k = 0; k < 3; k++) d->xipos[b][k] = d->xpos[b][k] + tmp[k];
+    double Ri[9];
+    q2m(m->body_iquat[b], Ri);
+    mulmm(d->ximat[b], d->xmat[b], Ri);
+  }
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = m->geom_bodyid[g];
+    double tmp[3], R[9];
+    mulmv(tmp, d->xmat[b], m->geom_pos[g]);
+    for (int k = 0; k < 3; k++) d->geom_xpos[g][k] = d->xpos[b][k] + tmp[k];
+    q2m(m->geom_quat[g], R);
+    mulmm(d->geom_xmat[g], d->xmat[b], R);
+  }
+  for (int s = 0; s < m->nsite; s++) {
+    int b = m->site_bodyid[s];
+    double tmp[3];
+    mulmv(tmp, d->xmat[b], m->site_pos[s]);
+    for (int k = 0; k < 3; k++) d->site_xpos[s][k] = d->xpos[b][k] + tmp[k];
+  }
+}
+
+static void com_pos(const mpcr_model_t* m, odata* d) {
+  double sm[NB], smc[NB][3];
+  for (int b = 0; b < m->nbody; b++) {
+    sm[b] = m->body_mass[b];
+    for (int k = 0; k < 3; k++) smc[b][k] = m->body_mass[b] * d->xipos[b][k];
+  }
+  for (int b = m->nbody - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    sm[p] += sm[b];
+    for (int k = 0; k < 3; k++) smc[p][k] += smc[b][k];
+  }
+  for (int b = 0; b < m->nbody; b++)
+    for (int k = 0; k < 3; k++) d->subtree_com[b][k] = sm[b] > MINVAL ? smc[b][k] / sm[b] : d->xipos[b][k];
+  /* cinert: inertia about subtree_com[root], world orientation (mju_inertCom) */
+  memset(d->cinert[0], 0, sizeof(d->cinert[0]));
+  for (int b = 1; b < m->nbody; b++) {
+    const double* R = d->ximat[b];
+    const double* I = m->body_inertia[b];
+    double mass = m->body_mass[b], dif[3], full[9];
+    for (int k = 0; k < 3; k++) dif[k] = d->xipos[b][k] - d->subtree_com[m->body_rootid[b]][k];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        full[3 * i + j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
+    double dd = dot3(dif, dif);
+    double* c = d->cinert[b];
+    c[0] = full[0] + mass * (dd - dif[0] * dif[0]);
+    c[1] = full[4] + mass * (dd - dif[1] * dif[1]);
+    c[2] = full[8] + mass * (dd - dif[2] * dif[2]);
+    c[3] = full[1] - mass * dif[0] * dif[1];
+    c[4] = full[2] - mass * dif[0] * dif[2];
+    c[5] = full[5] - mass * dif[1] * dif[2];
+    c[6] = mass * dif[0]; c[7] = mass * dif[1]; c[8] = mass * dif[2];
+    c[9] = mass;
+  }
+  /* cdof (mju_dofCom) */
+  for (int j = 0; j < m->njnt; j++) {
+    int b = m->jnt_bodyid[j], d0 = m->jnt_dofadr[j];
+    const double* com = d->subtree_com[m->body_rootid[b]];
+    double off[3];
+    for (int k = 0; k < 3; k++) off[k] = com[k] - d->xanchor[j][k];
+    switch (m->jnt_type[j]) {
+      case MPCR_JNT_FREE:
+        for (int i = 0; i < 3; i++) {
+          double* c = d->cdof[d0 + i];
+          memset(c, 0, 6 * sizeof(double));
+          c[3 + i] = 1;
+        }
+        d0 += 3; /* fall through to the rotational part */
+      case MPCR_JNT_BALL:
+        for (int i = 0; i < 3; i++) {
+          double ax[3] = {d->xmat[b][i], d->xmat[b][3 + i], d->xmat[b][6 + i]};
+          double* c = d->cdof[d0 + i];
+          memcpy(c, ax, sizeof(ax));
+          cross3(c + 3, ax, off);
+        }
+        break;
+      case MPCR_JNT_SLIDE: {
+        double* c = d->cdof[d0];
+        c[0] = c[1] = c[2] = 0;
+        memcpy(c + 3, d->xaxis[j], 3 * sizeof(double));
+        break;
+      }
+      default: {
+        double* c = d->cdof[d0];
+        memcpy(c, d->xaxis[j], 3 * sizeof(double));
+        cross3(c + 3, d->xaxis[j], off);
+      }
+    }
+  }
+}
+
+static void crb(const mpcr_model_t* m, odata* d) {
+  memcpy(d->crb, d->cinert, sizeof(double) * 10 * m->nbody);
+  for (int b = m->nbody - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    if (p > 0)
+      for (int k = 0; k < 10; k++) d->crb[p][k] += d->crb[b][k];
+  }
+  int nv = m->nv;
+  for (int i = 0; i < nv; i++)
+    for (int j = 0; j < nv; j++) d->M[i][j] = 0;
+  for (int i = 0; i < nv; i++) {
+    double f[6];
+    mul_inert_vec(f, d->crb[m->dof_bodyid[i]], d->cdof[i]);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      double v = 0;
+      for (int k = 0; k < 6; k++) v += d->cdof[j][k] * f[k];
+      d->M[i][j] = v;
+      d->M[j][i] = v;
+    }
+    d->M[i][i] += m->dof_armature[i];
+  }
+  chol(d->L, d->M, nv);
+}
+
+/* translational Jacobian row-block of a world point attached to body b:
+   jac[k][dof] (mj_jac) */
+static void jac_point(const mpcr_model_t* m, const odata* d, int b, const double p[3], double jac[3][NV]) {
+  const double* com = d->subtree_com[m->body_rootid[b]];
+  double r[3] = {p[0] - com[0], p[1] - com[1], p[2] - com[2]};
+  for (int i = 0; i < m->nv; i++) {
+    if (b > 0 && (m->body_dofmask[b] >> i & 1u)) {
+      double c[3];
+      cross3(c, d->cdof[i], r);
+      for (int k = 0; k < 3; k++) jac[k][i] = d->cdof[i][3 + k] + c[k];
+    } else {
+      jac[0][i] = jac[1][i] = jac[2][i] = 0;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* velocity: mj_comVel, mj_passive, mj_rne                                   */
+
+static void com_vel(const mpcr_model_t* m, odata* d) {
+  memset(d->cvel[0], 0, sizeof(d->cvel[0]));
+  for (int b = 1; b < m->nbody; b++) {
+    double cv[6];
+    memcpy(cv, d->cvel[m->body_parentid[b]], sizeof(cv));
+    int j0 = m->body_jntadr[b];
+    for (int j = j0; j < j0 + m->body_jntnum[b]; j++) {
+      int d0 = m->jnt_dofadr[j];
+      if (m->jnt_type[j] == MPCR_JNT_FREE) {
+        for (int i = 0; i < 3; i++) memset(d->cdof_dot[d0 + i], 0, 6 * sizeof(double));
+        for (int i = 0; i < 3; i++)
+          for (int k = 0; k < 6; k++) cv[k] += d->cdof[d0 + i][k] * d->qvel[d0 + i];
+        d0 += 3;
+        for (int i = 0; i < 3; i++) cross_motion(d->cdof_dot[d0 + i], cv, d->cdof[d0 + i]);
+        for (int i = 0; i < 3; i++)
+          for (int k = 0; k < 6; k++) cv[k] += d->cdof[d0 + i][k] * d->qvel[d0 + i];
+      } else if (m->jnt_type[j] == MPCR_JNT_BALL) {
+        for (int i = 0; i < 3; i++) cross_motion(d->cdof_dot[d0 + i], cv, d->cdof[d0 + i]);
+        for (int i = 0; i < 3; i++)
+          for (int k = 0; k < 6; k++) cv[k] += d->cdof[d0 + i][k] * d->qvel[d0 + i];
+      } else {
+        cross_motion(d->cdof_dot[d0], cv, d->cdof[d0]);
+        for (int k = 0; k < 6; k++) cv[k] += d->cdof[d0][k] * d->qvel[d0];
+      }
+    }
+    memcpy(d->cvel[b], cv, sizeof(cv));
+  }
+}
+
+static void passive(const mpcr_model_t* m, odata* d) {
+  for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] = 0;
+  if (m->disableflags & MPCR_DSBL_PASSIVE) return;
+  for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] = -m->dof_damping[i] * d->qvel[i];
+  /* gravity compensation: -gravity*mass*gravcomp applied at xipos */
+  for (int b = 1; b < m->nbody; b++) {
+    double gc = m->body_gravcomp[b];
+    if (gc == 0 || m->body_mass[b] == 0) continue;
+    double f[3], jac[3][NV];
+    for (int k = 0; k < 3; k++) f[k] = -m->gravity[k] * m->body_mass[b] * gc;
+    jac_point(m, d, b, d->xipos[b], jac);
+    for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] += jac[0][i] * f[0] + jac[1][i] * f[1] + jac[2][i] * f[2];
+  }
+}
+
+static void rne(const mpcr_model_t* m, odata* d) {
+  double cacc[NB][6], cfrc[NB][6];
+  memset(cacc[0], 0, sizeof(cacc[0]));
+  if (!(m->disableflags & MPCR_DSBL_GRAVITY))
+    for (int k = 0; k < 3; k++) cacc[0][3 + k] = -m->gravity[k];
+  for (int b = 1; b < m->nbody; b++) {
+    memcpy(cacc[b], cacc[m->body_parentid[b]], sizeof(cacc[b]));
+    for (int i = m->body_dofadr[b]; i < m->body_dofadr[b] + m->body_dofnum[b]; i++)
+      for (int k = 0; k < 6; k++) cacc[b][k] += d->cdof_dot[i][k] * d->qvel[i];
+    double t1[6], t2[6];
+    mul_inert_vec(cfrc[b], d->cinert[b], cacc[b]);
+    mul_inert_vec(t1, d->cinert[b], d->cvel[b]);
+    cross_force(t2, d->cvel[b], t1);
+    for (int k = 0; k < 6; k++) cfrc[b][k] += t2[k];
+  }
+  for (int b = m->nbody - 1; b > 0; b--) {
+    int p = m->body_parentid[b];
+    if (p > 0)
+      for (int k = 0; k < 6; k++) cfrc[p][k] += cfrc[b][k];
+  }
+  for (int i = 0; i < m->nv; i++) {
+    double v = 0;
+    for (int k = 0; k < 6; k++) v += d->cdof[i][k] * cfrc[m->dof_bodyid[i]][k];
+    d->qfrc_bias[i] = v;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* narrow phase (contact definitions shared with the HIP kernel: DESIGN.md   */
+/* "Contact slot layout").  normal points from geom1 to geom2.              */
+
+static void make_frame(double f[9], const double n[3]) {
+  /* mju_makeFrame: x = normal, y from (0,1,0) or (0,0,1), z = x cross y */
+  memcpy(f, n, 3 * sizeof(double));
+  double y[3] = {0, 1, 0};
+  if (fabs(n[1]) >= 0.5) { y[0] = 0; y[1] = 0; y[2] = 1; }
+  double dd = dot3(n, y);
+  for (int k = 0; k < 3; k++) y[k] -= dd * n[k];
+  double ny = norm3(y);
+  for (int k = 0; k < 3; k++) f[3 + k] = y[k] / ny;
+  cross3(f + 6, f, f + 3);
+}
+
+static void set_contact(ocontact* c, double dist, const double pos[3], const double n[3]) {
+  c->dist = dist;
+  memcpy(c->pos, pos, 3 * sizeof(double));
+  make_frame(c->frame, n);
+}
+
+static void col_plane_capsule(const odata* d, int gp, int gc, const double* sz, ocontact* out) {
+  const double* R = d->geom_xmat[gp];
+  double n[3] = {R[2], R[5], R[8]};
+  const double* Rc = d->geom_xmat[gc];
+  double ax[3] = {Rc[2], Rc[5], Rc[8]};
+  double r = sz[0], hl = sz[1];
+  for (int s = 0; s < 2; s++) {
+    double sg = s == 0 ? 1.0 : -1.0, e[3], dif[3], pos[3];
+    for (int k = 0; k < 3; k++) e[k] = d->geom_xpos[gc][k] + sg * hl * ax[k];
+    for (int k = 0; k < 3; k++) dif[k] = e[k] - d->geom_xpos[gp][k];
+    double dist = dot3(n, dif) - r;
+    for (int k = 0; k < 3; k++) pos[k] = e[k] - n[k] * (r + 0.5 * dist);
+    set_contact(&out[s], dist, pos, n);
+  }
+}
+
+static void col_plane_box(const odata* d, int gp, int gb, const double* h, ocontact* out) {
+  const double* R = d->geom_xmat[gp];
+  double n[3] = {R[2], R[5], R[8]};
+  const double* Rb = d->geom_xmat[gb];
+  double dist[8], corner[8][3];
+  for (int c = 0; c < 8; c++) {
+    double l[3] = {(c & 1) ? h[0] : -h[0], (c & 2) ? h[1] : -h[1], (c & 4) ? h[2] : -h[2]}, w[3], dif[3];
+    mulmv(w, Rb, l);
+    for (int k = 0; k < 3; k++) corner[c][k] = d->geom_xpos[gb][k] + w[k];
+    for (int k = 0; k < 3; k++) dif[k] = corner[c][k] - d->geom_xpos[gp][k];
+    dist[c] = dot3(n, dif);
+  }
+  /* the 4 deepest corners, ascending depth order, ties by corner index */
+  int used = 0;
+  for (int s = 0; s < 4; s++) {
+    int best = -1;
+    for (int c = 0; c < 8; c++)
+      if (!(used >> c & 1) && (best < 0 || dist[c] < dist[best])) best = c;
+    used |= 1 << best;
+    double pos[3];
+    for (int k = 0; k < 3; k++) pos[k] = corner[best][k] - n[k] * 0.5 * dist[best];
+    set_contact(&out[s], dist[best], pos, n);
+  }
+}
+
+/* closest points between segments p1+s*d1 (s in [0,1]) and p2+t*d2 */
+static void seg_seg(const double p1[3], const double d1[3], const double p2[3], const double d2[3],
+                    double* sc, double* tc) {
+  double r[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+  double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  double s, t;
+  if (a <= MINVAL && e <= MINVAL) { *sc = 0; *tc = 0; return; }
+  if (a <= MINVAL) {
+    s = 0; t = clampd(f / e, 0, 1);
+  } else {
+    double c = dot3(d1, r);
+    if (e <= MINVAL) {
+      t = 0; s = clampd(-c / a, 0, 1);
+    } else {
+      double b = dot3(d1, d2), den = a * e - b * b;
+      s = den > 1e-12 * a * e ? clampd((b * f - c * e) / den, 0, 1) : 0;
+      t = (b * s + f) / e;
+      if (t < 0) { t = 0; s = clampd(-c / a, 0, 1); }
+      else if (t > 1) { t = 1; s = clampd((b - c) / a, 0, 1); }
+    }
+  }
+  *sc = s; *tc = t;
+}
+
+static void any_normal(double n[3], const double a[3]) {
+  /* a unit vector perpendicular to a (fallback for coincident points) */
+  double t[3] = {1, 0, 0};
+  if (fabs(a[0]) > 0.9) { t[0] = 0; t[1] = 1; }
+  cross3(n, a, t);
+  double l = norm3(n);
+  for (int k = 0; k < 3; k++) n[k] /= l;
+}
+
+static void col_capsule_capsule(const odata* d, int g1, int g2, const double* s1, const double* s2,
+                                ocontact* out) {
+  const double *R1 = d->geom_xmat[g1], *R2 = d->geom_xmat[g2];
+  double a1[3] = {R1[2], R1[5], R1[8]}, a2[3] = {R2[2], R2[5], R2[8]};
+  double p1[3], p2[3], d1[3], d2[3];
+  for (int k = 0; k < 3; k++) {
+    p1[k] = d->geom_xpos[g1][k] - s1[1] * a1[k]; d1[k] = 2 * s1[1] * a1[k];
+    p2[k] = d->geom_xpos[g2][k] - s2[1] * a2[k]; d2[k] = 2 * s2[1] * a2[k];
+  }
+  double s, t, c1[3], c2[3], n[3];
+  seg_seg(p1, d1, p2, d2, &s, &t);
+  for (int k = 0; k < 3; k++) { c1[k] = p1[k] + s * d1[k]; c2[k] = p2[k] + t * d2[k]; n[k] = c2[k] - c1[k]; }
+  double len = norm3(n);
+  if (len < 1e-12) any_normal(n, a1);
+  else for (int k = 0; k < 3; k++) n[k] /= len;
+  double dist = len - s1[0] - s2[0], pos[3];
+  for (int k = 0; k < 3; k++) pos[k] = c1[k] + n[k] * (s1[0] + 0.5 * dist);
+  set_contact(&out[0], dist, pos, n);
+}
+
+/* signed distance of a box-local point to a box (half sizes h); returns the
+   local normal pointing from the point towards the box surface region the
+   point must move along to reach the box (from geom1 = point's owner to
+   geom2 = box) and the closest/deepest box surface point. */
+static double point_box(const double p[3], const double h[3], double nl[3], double q[3]) {
+  double o[3], out2 = 0;
+  for (int k = 0; k < 3; k++) {
+    q[k] = clampd(p[k], -h[k], h[k]);
+    o[k] = q[k] - p[k];
+    out2 += o[k] * o[k];
+  }
+  if (out2 > 0) {
+    double l = sqrt(out2);
+    for (int k = 0; k < 3; k++) nl[k] = o[k] / l;
+    return l;
+  }
+  /* inside: deepest face is the one with max(|p_k| - h_k) */
+  int best = 0;
+  double g = fabs(p[0]) - h[0];
+  for (int k = 1; k < 3; k++)
+    if (fabs(p[k]) - h[k] > g) { g = fabs(p[k]) - h[k]; best = k; }
+  double sg = p[best] >= 0 ? 1.0 : -1.0;
+  nl[0] = nl[1] = nl[2] = 0;
+  nl[best] = -sg;
+  memcpy(q, p, 3 * sizeof(double));
+  q[best] = sg * h[best];
+  return g;
+}
+
+static void col_capsule_box(const odata* d, int gc, int gb, const double* sc, const double* h,
+                            ocontact* out) {
+  const double* Rc = d->geom_xmat[gc];
+  const double* Rb = d->geom_xmat[gb];
+  double ax[3] = {Rc[2], Rc[5], Rc[8]}, r = sc[0], hl = sc[1];
+  double A[3], B[3], a[3], dd[3], tmp[3];
+  for (int k = 0; k < 3; k++) {
+    A[k] = d->geom_xpos[gc][k] - hl * ax[k] - d->geom_xpos[gb][k];
+    B[k] = 2 * hl * ax[k];
+  }
+  mulmtv(a, Rb, A);
+  mulmtv(dd, Rb, B);
+  /* f(t) = sum_k max(|a_k + t dd_k| - h_k, 0)^2 is convex, C1, piecewise
+     quadratic; f'(t) is monotone and piecewise linear between the knots
+     t in {0, 1, (+-h_k - a_k)/dd_k}. */
+  double knots[8];
+  int nk = 0;
+  knots[nk++] = 0;
+  knots[nk++] = 1;
+  for (int k = 0; k < 3; k++) {
+    if (fabs(dd[k]) > MINVAL) {
+      for (int sgn = -1; sgn <= 1; sgn += 2) {
+        double t = (sgn * h[k] - a[k]) / dd[k];
+        if (t > 0 && t < 1) knots[nk++] = t;
+      }
+    }
+  }
+  double tlo = -1, thi = 2, flo = 0, fhi = 0;
+  for (int i = 0; i < nk; i++) {
+    double t = knots[i], fp = 0;
+    for (int k = 0; k < 3; k++) {
+      double x = a[k] + t * dd[k], e = fabs(x) - h[k];
+      if (e > 0) fp += 2 * dd[k] * (x > 0 ? e : -e);
+    }
+    if (fp < 0) { if (t > tlo) { tlo = t; flo = fp; } }
+    else { if (t < thi) { thi = t; fhi = fp; } }
+  }
+  double ts;
+  if (tlo < 0) ts = 0;
+  else if (thi > 1) ts = 1;
+  else ts = fhi - flo > 0 ? tlo - flo * (thi - tlo) / (fhi - flo) : tlo;
+  double p[3], q[3], nl[3];
+  for (int k = 0; k < 3; k++) p[k] = a[k] + ts * dd[k];
+  double g = point_box(p, h, nl, q);
+  if (g <= 0) {
+    /* segment reaches the box: deepest point of the convex, piecewise linear
+       g(t) = max_k(|x_k(t)| - h_k) over its kinks */
+    double cand[17];
+    int nc = 0;
+    cand[nc++] = 0;
+    cand[nc++] = 1;
+    for (int k = 0; k < 3; k++)
+      if (fabs(dd[k]) > MINVAL) { double t = -a[k] / dd[k]; if (t > 0 && t < 1) cand[nc++] = t; }
+    for (int i = 0; i < 3; i++)
+      for (int j = i + 1; j < 3; j++)
+        for (int si = -1; si <= 1; si += 2)
+          for (int sj = -1; sj <= 1; sj += 2) {
+            double den = si * dd[i] - sj * dd[j];
+            if (fabs(den) > MINVAL) {
+              double t = (h[i] - h[j] - si * a[i] + sj * a[j]) / den;
+              if (t > 0 && t < 1) cand[nc++] = t;
+            }
+          }
+    double gbest = 1e300, tbest = 0;
+    for (int c = 0; c < nc; c++) {
+      double gm = -1e300;
+      for (int k = 0; k < 3; k++) {
+        double e = fabs(a[k] + cand[c] * dd[k]) - h[k];
+        if (e > gm) gm = e;
+      }
+      if (gm < gbest) { gbest = gm; tbest = cand[c]; }
+    }
+    ts = tbest;
+    for (int k = 0; k < 3; k++) p[k] = a[k] + ts * dd[k];
+    g = point_box(p, h, nl, q);
+  }
+  for (int s = 0; s < 2; s++) {
+    double t = s == 0 ? ts : (ts < 0.5 ? 1.0 : 0.0);
+    if (s == 1) {
+      for (int k = 0; k < 3; k++) p[k] = a[k] + t * dd[k];
+      g = point_box(p, h, nl, q);
+    }
+    double n[3], pl[3], pos[3];
+    mulmv(n, Rb, nl);
+    for (int k = 0; k < 3; k++) pl[k] = 0.5 * (p[k] + r * nl[k] + q[k]);
+    mulmv(tmp, Rb, pl);
+    for (int k = 0; k < 3; k++) pos[k] = tmp[k] + d->geom_xpos[gb][k];
+    set_contact(&out[s], g - r, pos, n);
+  }
+}
+
+static void col_box_box(const odata* d, int ga, int gb, const double* ha, const double* hb,
+                        double margin, ocontact* out) {
+  const double *Ra = d->geom_xmat[ga], *Rb = d->geom_xmat[gb];
+  double axA[3][3], axB[3][3], t[3];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) { axA[i][k] = Ra[3 * k + i]; axB[i][k] = Rb[3 * k + i]; }
+  for (int k = 0; k < 3; k++) t[k] = d->geom_xpos[gb][k] - d->geom_xpos[ga][k];
+  for (int s = 0; s < 4; s++) out[s].dist = 1e30;
+  /* separating-axis test: 3 + 3 face axes, 9 edge axes */
+  double best_face = -1e300, best_edge = -1e300, Lf[3] = {0, 0, 1}, Le[3] = {0, 0, 1};
+  int face_id = -1, edge_i = -1, edge_j = -1;
+  for (int ax = 0; ax < 6; ax++) {
+    const double* L = ax < 3 ? axA[ax] : axB[ax - 3];
+    double ra = 0, rb = 0;
+    for (int k = 0; k < 3; k++) { ra += ha[k] * fabs(dot3(axA[k], L)); rb += hb[k] * fabs(dot3(axB[k], L)); }
+    double sep = fabs(dot3(t, L)) - ra - rb;
+    if (sep > best_face) { best_face = sep; face_id = ax; memcpy(Lf, L, sizeof(Lf)); }
+  }
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      double L[3];
+      cross3(L, axA[i], axB[j]);
+      double l = norm3(L);
+      if (l < 1e-6) continue;
+      for (int k = 0; k < 3; k++) L[k] /= l;
+      double ra = 0, rb = 0;
+      for (int k = 0; k < 3; k++) { ra += ha[k] * fabs(dot3(axA[k], L)); rb += hb[k] * fabs(dot3(axB[k], L)); }
+      double sep = fabs(dot3(t, L)) - ra - rb;
+      if (sep > best_edge) { best_edge = sep; edge_i = i; edge_j = j; memcpy(Le, L, sizeof(Le)); }
+    }
+  double best = best_face > best_edge ? best_face : best_edge;
+  out[0].dist = best; /* separation (used only if a masked slot asks for it) */
+  if (best >= margin) return;
+  int use_edge = edge_i >= 0 && best_edge > 0.95 * best_face + 1e-5;
+  double n[3];
+  const double* L = use_edge ? Le : Lf;
+  double sg = dot3(t, L) >= 0 ? 1.0 : -1.0;
+  for (int k = 0; k < 3; k++) n[k] = sg * L[k]; /* from A towards B */
+  if (use_edge) {
+    double pa[3], pb[3], da[3], db[3];
+    for (int k = 0; k < 3; k++) { pa[k] = d->geom_xpos[ga][k]; pb[k] = d->geom_xpos[gb][k]; }
+    for (int k = 0; k < 3; k++) {
+      if (k != edge_i) {
+        double s = dot3(n, axA[k]) >= 0 ? 1.0 : -1.0;
+        for (int c = 0; c < 3; c++) pa[c] += s * ha[k] * axA[k][c];
+      }
+      if (k != edge_j) {
+        double s = dot3(n, axB[k]) >= 0 ? -1.0 : 1.0;
+        for (int c = 0; c < 3; c++) pb[c] += s * hb[k] * axB[k][c];
+      }
+    }
+    for (int c = 0; c < 3; c++) {
+      pa[c] -= ha[edge_i] * axA[edge_i][c]; da[c] = 2 * ha[edge_i] * axA[edge_i][c];
+      pb[c] -= hb[edge_j] * axB[edge_j][c]; db[c] = 2 * hb[edge_j] * axB[edge_j][c];
+    }
+    double s, u, pos[3];
+    seg_seg(pa, da, pb, db, &s, &u);
+    for (int c = 0; c < 3; c++) pos[c] = 0.5 * (pa[c] + s * da[c] + pb[c] + u * db[c]);
+    set_contact(&out[0], best_edge, pos, n);
+    return;
+  }
+  /* face contact: reference box owns the face axis */
+  int refA = face_id < 3, fi = refA ? face_id : face_id - 3;
+  const double *cr = refA ? d->geom_xpos[ga] : d->geom_xpos[gb], *ci = refA ? d->geom_xpos[gb] : d->geom_xpos[ga];
+  double (*axR)[3] = refA ? axA : axB, (*axI)[3] = refA ? axB : axA;
+  const double *hr = refA ? ha : hb, *hi = refA ? hb : ha;
+  double nf[3];
+  for (int k = 0; k < 3; k++) nf[k] = refA ? n[k] : -n[k]; /* ref face normal towards incident box */
+  int ki = 0;
+  double bestdot = -1;
+  for (int k = 0; k < 3; k++) {
+    double v = fabs(dot3(axI[k], nf));
+    if (v > bestdot) { bestdot = v; ki = k; }
+  }
+  double si = dot3(axI[ki], nf) > 0 ? -1.0 : 1.0;
+  int u = (ki + 1) % 3, v = (ki + 2) % 3;
+  double poly[8][3], tmpp[8][3];
+  int np = 4;
+  const double su[4] = {1, -1, -1, 1}, sv[4] = {1, 1, -1, -1};
+  for (int c = 0; c < 4; c++)
+    for (int k = 0; k < 3; k++)
+      poly[c][k] = ci[k] + si * hi[ki] * axI[ki][k] + su[c] * hi[u] * axI[u][k] + sv[c] * hi[v] * axI[v][k];
+  /* clip against the 4 side planes of the reference face */
+  for (int pl = 0; pl < 4 && np > 0; pl++) {
+    int ax = (fi + 1 + (pl >> 1)) % 3;
+    double s = (pl & 1) ? -1.0 : 1.0;
+    int nn = 0;
+    for (int c = 0; c < np; c++) {
+      const double *P = poly[c], *Q = poly[(c + 1) % np];
+      double dp = s * (dot3(P, axR[ax]) - dot3(cr, axR[ax])) - hr[ax];
+      double dq = s * (dot3(Q, axR[ax]) - dot3(cr, axR[ax])) - hr[ax];
+      if (dp <= 0) { memcpy(tmpp[nn++], P, 3 * sizeof(double)); }
+      if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
+        double w = dp / (dp - dq);
+        for (int k = 0; k < 3; k++) tmpp[nn][k] = P[k] + w * (Q[k] - P[k]);
+        nn++;
+      }
+    }
+    np = nn;
+    memcpy(poly, tmpp, sizeof(double) * 3 * np);
+  }
+  double depth[8];
+  int keep[8], nkeep = 0;
+  for (int c = 0; c < np; c++) {
+    double rel[3];
+    for (int k = 0; k < 3; k++) rel[k] = poly[c][k] - cr[k];
+    depth[c] = hr[fi] - dot3(rel, nf);
+    if (-depth[c] < margin) keep[nkeep++] = c;
+  }
+  if (nkeep == 0) return;
+  int pick[4], npick;
+  if (nkeep <= 4) {
+    for (int c = 0; c < nkeep; c++) pick[c] = keep[c];
+    npick = nkeep;
+  } else {
+    int d0 = 0;
+    for (int c = 1; c < nkeep; c++)
+      if (depth[keep[c]] > depth[keep[d0]]) d0 = c;
+    for (int s = 0; s < 4; s++) pick[s] = keep[(d0 + s * nkeep / 4) % nkeep];
+    npick = 4;
+  }
+  for (int s = 0; s < npick; s++) {
+    int c = pick[s];
+    double pos[3];
+    for (int k = 0; k < 3; k++) pos[k] = poly[c][k] + nf[k] * 0.5 * depth[c];
+    set_contact(&out[s], -depth[c], pos, n);
+  }
+}
+
+static void collision(const mpcr_model_t* m, odata* d) {
+  d->ncon = m->ncon;
+  for (int p = 0; p < m->npair; p++) {
+    int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
+    ocontact* out = &d->con[m->pair_conadr[p]];
+    for (int s = 0; s < m->pair_ncon[p]; s++) {
+      out[s].dist = 1e30;
+      out[s].pair = p;
+      out[s].active = 0;
+    }
+    /* unmasked pairs only feed the solver: cull by bounding spheres */
+    if (m->pair_slotadr[p] < 0 && m->geom_type[g1] != MPCR_GEOM_PLANE) {
+      double dif[3];
+      for (int k = 0; k < 3; k++) dif[k] = d->geom_xpos[g2][k] - d->geom_xpos[g1][k];
+      if (norm3(dif) > m->geom_rbound[g1] + m->geom_rbound[g2] + m->pair_margin[p]) continue;
+    }
+    const double *s1 = m->geom_size[g1], *s2 = m->geom_size[g2];
+    switch (m->pair_func[p]) {
+      case MPCR_COL_PLANE_CAPSULE: col_plane_capsule(d, g1, g2, s2, out); break;
+      case MPCR_COL_PLANE_BOX: col_plane_box(d, g1, g2, s2, out); break;
+      case MPCR_COL_CAPSULE_CAPSULE: col_capsule_capsule(d, g1, g2, s1, s2, out); break;
+      case MPCR_COL_CAPSULE_BOX: col_capsule_box(d, g1, g2, s1, s2, out); break;
+      case MPCR_COL_BOX_BOX: col_box_box(d, g1, g2, s1, s2, m->pair_margin[p] - m->pair_gap[p], out); break;
+      default: break;
+    }
+    for (int s = 0; s < m->pair_ncon[p]; s++) {
+      out[s].pair = p;
+      out[s].active = !(m->disableflags & MPCR_DSBL_CONTACT) && out[s].dist < m->pair_margin[p] - m->pair_gap[p];
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* constraints: equality, limits, pyramidal contacts + impedance             */
+
+static void impedance(const double solimp[5], double pos, double margin, double* imp) {
+  double dmin = clampd(solimp[0], MINIMP, MAXIMP), dmax = clampd(solimp[1], MINIMP, MAXIMP);
+  double width = solimp[2], mid = solimp[3], power = solimp[4];
+  if (dmin == dmax || width <= MINVAL) { *imp = 0.5 * (dmin + dmax); return; }
+  double x = fabs((pos - margin) / width);
+  if (x >= 1) { *imp = dmax; return; }
+  if (x <= 0) { *imp = dmin; return; }
+  double y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = pow(x, power) / pow(mid, power - 1);
+  else y = 1 - pow(1 - x, power) / pow(1 - mid, power - 1);
+  *imp = dmin + y * (dmax - dmin);
+}
+
+static int add_row(const mpcr_model_t* m, odata* d, int eq, double pos, double margin, double diag,
+                   const double solref[2], const double solimp[5]) {
+  if (d->nefc >= MAXEFC) { d->efc_trunc++; return -1; }
+  int r = d->nefc++;
+  d->efc_eq[r] = eq;
+  d->efc_pos[r] = pos;
+  d->efc_margin[r] = margin;
+  d->efc_diag[r] = diag;
+  memcpy(d->efc_solref[r], solref, 2 * sizeof(double));
+  memcpy(d->efc_solimp[r], solimp, 5 * sizeof(double));
+  for (int i = 0; i < m->nv; i++) d->efc_J[r][i] = 0;
+  return r;
+}
+
+static void make_constraint(const mpcr_model_t* m, odata* d) {
+  int nv = m->nv;
+  d->nefc = 0;
+  d->efc_trunc = 0;
+  /* joint equality: q1 - qpos0_1 = poly(q2 - qpos0_2) */
+  if (!(m->disableflags & MPCR_DSBL_EQUALITY))
+    for (int e = 0; e < m->neq; e++) {
+      if (m->eq_type[e] != MPCR_EQ_JOINT) continue;
+      int j1 = m->eq_obj1[e], j2 = m->eq_obj2[e];
+      const double* c = m->eq_data[e];
+      int a1 = m->jnt_qposadr[j1], d1 = m->jnt_dofadr[j1];
+      double pos, deriv = 0, diag = m->dof_invweight0[d1];
+      if (j2 >= 0) {
+        int a2 = m->jnt_qposadr[j2];
+        double dif = d->qpos[a2] - m->qpos0[a2];
+        pos = d->qpos[a1] - m->qpos0[a1] - (c[0] + dif * (c[1] + dif * (c[2] + dif * (c[3] + dif * c[4]))));
+        deriv = c[1] + dif * (2 * c[2] + dif * (3 * c[3] + dif * 4 * c[4]));
+        diag += m->dof_invweight0[m->jnt_dofadr[j2]];
+      } else {
+        pos = d->qpos[a1] - m->qpos0[a1] - c[0];
+      }
+      int r = add_row(m, d, 1, pos, 0, diag, m->eq_solref[e], m->eq_solimp[e]);
+      if (r < 0) continue;
+      d->efc_J[r][d1] = 1;
+      if (j2 >= 0) d->efc_J[r][m->jnt_dofadr[j2]] -= deriv;
+    }
+  /* joint limits (hinge / slide) */
+  if (!(m->disableflags & MPCR_DSBL_LIMIT))
+    for (int j = 0; j < m->njnt; j++) {
+      if (!m->jnt_limited[j] || (m->jnt_type[j] != MPCR_JNT_HINGE && m->jnt_type[j] != MPCR_JNT_SLIDE)) continue;
+      double q = d->qpos[m->jnt_qposadr[j]];
+      int dof = m->jnt_dofadr[j];
+      for (int side = 0; side < 2; side++) {
+        double dist = side == 0 ? q - m->jnt_range[j][0] : m->jnt_range[j][1] - q;
+        if (dist < m->jnt_margin[j]) {
+          int r = add_row(m, d, 0, dist, m->jnt_margin[j], m->dof_invweight0[dof], m->jnt_solref[j], m->jnt_solimp[j]);
+          if (r >= 0) d->efc_J[r][dof] = side == 0 ? 1 : -1;
+        }
+      }
+    }
+  /* contacts: pyramidal, condim 3 -> 4 rows J_n +- mu J_t{1,2}; condim 1 -> J_n */
+  for (int c = 0; c < d->ncon; c++) {
+    ocontact* con = &d->con[c];
+    if (!con->active) continue;
+    int p = con->pair;
+    int b1 = m->geom_bodyid[m->pair_geom1[p]], b2 = m->geom_bodyid[m->pair_geom2[p]];
+    double j1[3][NV], j2[3][NV], jd[3][NV];
+    jac_point(m, d, b1, con->pos, j1);
+    jac_point(m, d, b2, con->pos, j2);
+    for (int k = 0; k < 3; k++)
+      for (int i = 0; i < nv; i++) jd[k][i] = j2[k][i] - j1[k][i];
+    double jf[3][NV];
+    for (int a = 0; a < 3; a++)
+      for (int i = 0; i < nv; i++)
+        jf[a][i] = con->frame[3 * a] * jd[0][i] + con->frame[3 * a + 1] * jd[1][i] + con->frame[3 * a + 2] * jd[2][i];
+    double tran = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+    double mu = m->pair_friction[p], margin = m->pair_margin[p] - m->pair_gap[p];
+    if (m->pair_condim[p] == 1) {
+      int r = add_row(m, d, 0, con->dist, margin, tran, m->pair_solref[p], m->pair_solimp[p]);
+      if (r >= 0)
+        for (int i = 0; i < nv; i++) d->efc_J[r][i] = jf[0][i];
+      continue;
+    }
+    for (int k = 1; k < 3; k++)
+      for (int sgn = 1; sgn >= -1; sgn -= 2) {
+        int r = add_row(m, d, 0, con->dist, margin, tran * (1 + mu * mu), m->pair_solref[p], m->pair_solimp[p]);
+        if (r >= 0)
+          for (int i = 0; i < nv; i++) d->efc_J[r][i] = jf[0][i] + sgn * mu * jf[k][i];
+      }
+  }
+  /* impedance, regularisation and reference acceleration (mj_makeImpedance) */
+  for (int r = 0; r < d->nefc; r++) {
+    double v = 0;
+    for (int i = 0; i < nv; i++) v += d->efc_J[r][i] * d->qvel[i];
+    d->efc_vel[r] = v;
+    double imp;
+    impedance(d->efc_solimp[r], d->efc_pos[r], d->efc_margin[r], &imp);
+    double R = (1 - imp) / imp * d->efc_diag[r];
+    if (R < MINVAL) R = MINVAL;
+    d->efc_D[r] = 1 / R;
+    double K, B, tc = d->efc_solref[r][0], dr = d->efc_solref[r][1];
+    double dmax = clampd(d->efc_solimp[r][1], MINIMP, MAXIMP);
+    if (tc > 0) {
+      if (!(m->disableflags & MPCR_DSBL_REFSAFE) && tc < 2 * m->timestep) tc = 2 * m->timestep;
+      K = 1 / (dmax * dmax * tc * tc * dr * dr);
+      B = 2 / (dmax * tc);
+    } else {
+      K = -tc / (dmax * dmax);
+      B = -dr / dmax;
+    }
+    d->efc_aref[r] = -B * v - K * imp * (d->efc_pos[r] - d->efc_margin[r]);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Newton solver (primal), one iteration + exact-quadratic line search       */
+
+typedef struct { double alpha, cost, d0, d1; } lspt;
+
+static void mulM(const mpcr_model_t* m, const odata* d, const double* x, double* y) {
+  for (int i = 0; i < m->nv; i++) {
+    double s = 0;
+    for (int j = 0; j < m->nv; j++) s += d->M[i][j] * x[j];
+    y[i] = s;
+  }
+}
+
+static double solver_cost(const mpcr_model_t* m, const odata* d, const double* qacc, const double* Ma,
+                          const double* jar) {
+  double gauss = 0, c = 0;
+  for (int i = 0; i < m->nv; i++) gauss += (Ma[i] - d->qfrc_smooth[i]) * (qacc[i] - d->qacc_smooth[i]);
+  for (int r = 0; r < d->nefc; r++)
+    if (d->efc_eq[r] || jar[r] < 0) c += d->efc_D[r] * jar[r] * jar[r];
+  return 0.5 * gauss + 0.5 * c;
+}
+
+static void eval_jar(const mpcr_model_t* m, const odata* d, const double* x, double* jar) {
+  for (int r = 0; r < d->nefc; r++) {
+    double s = 0;
+    for (int i = 0; i < m->nv; i++) s += d->efc_J[r][i] * x[i];
+    jar[r] = s - d->efc_aref[r];
+  }
+}
+
+static lspt ls_eval(const odata* d, const double qg[3], const double* jar, const double* jv, double alpha) {
+  double q0 = qg[0], q1 = qg[1], q2 = qg[2];
+  for (int r = 0; r < d->nefc; r++) {
+    double x = jar[r] + alpha * jv[r];
+    if (d->efc_eq[r] || x < 0) {
+      double D = d->efc_D[r];
+      q0 += 0.5 * D * jar[r] * jar[r];
+      q1 += D * jv[r] * jar[r];
+      q2 += 0.5 * D * jv[r] * jv[r];
+    }
+  }
+  lspt p;
+  p.alpha = alpha;
+  p.cost = alpha * alpha * q2 + alpha * q1 + q0;
+  p.d0 = 2 * alpha * q2 + q1;
+  p.d1 = 2 * q2 + (q2 == 0 ? MINVAL : 0);
+  return p;
+}
+
+static void solve(const mpcr_model_t* m, odata* d) {
+  int nv = m->nv, nefc = d->nefc;
+  if (nefc == 0) { memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv); return; }
+  double Ma[NV], jar[MAXEFC], qacc[NV];
+  /* warm start: the better of qacc_warmstart and qacc_smooth */
+  if (!(m->disableflags & MPCR_DSBL_WARMSTART)) {
+    double Mw[NV], jw[MAXEFC], Ms[NV], js[MAXEFC];
+    mulM(m, d, d->qacc_warmstart, Mw);
+    eval_jar(m, d, d->qacc_warmstart, jw);
+    mulM(m, d, d->qacc_smooth, Ms);
+    eval_jar(m, d, d->qacc_smooth, js);
+    double cw = solver_cost(m, d, d->qacc_warmstart, Mw, jw), cs = solver_cost(m, d, d->qacc_smooth, Ms, js);
+    memcpy(qacc, cw < cs ? d->qacc_warmstart : d->qacc_smooth, sizeof(double) * nv);
+  } else {
+    memcpy(qacc, d->qacc_smooth, sizeof(double) * nv);
+  }
+  mulM(m, d, qacc, Ma);
+  eval_jar(m, d, qacc, jar);
+  double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  double cost = solver_cost(m, d, qacc, Ma, jar), prev_cost = 1e300;
+  for (int it = 0;; it++) {
+    /* gradient and Newton direction with the Hessian of the active set */
+    double grad[NV], H[NV][NV], Lh[NV][NV], Mgrad[NV], search[NV];
+    for (int i = 0; i < nv; i++) {
+      double qc = 0;
+      for (int r = 0; r < nefc; r++)
+        if (d->efc_eq[r] || jar[r] < 0) qc += d->efc_J[r][i] * (-d->efc_D[r] * jar[r]);
+      grad[i] = Ma[i] - d->qfrc_smooth[i] - qc;
+    }
+    double gn = 0;
+    for (int i = 0; i < nv; i++) gn += grad[i] * grad[i];
+    gn = sqrt(gn);
+    if (it >= m->iterations || scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance) break;
+    for (int i = 0; i < nv; i++)
+      for (int j = 0; j < nv; j++) {
+        double h = d->M[i][j];
+        for (int r = 0; r < nefc; r++)
+          if (d->efc_eq[r] || jar[r] < 0) h += d->efc_J[r][i] * d->efc_D[r] * d->efc_J[r][j];
+        H[i][j] = h;
+      }
+    chol(Lh, H, nv);
+    chol_solve(Mgrad, Lh, grad, nv);
+    for (int i = 0; i < nv; i++) search[i] = -Mgrad[i];
+    /* line search (MJX-style bracketing on the piecewise quadratic) */
+    double Mv[NV], jv[MAXEFC], sn = 0;
+    mulM(m, d, search, Mv);
+    for (int r = 0; r < nefc; r++) {
+      double s = 0;
+      for (int i = 0; i < nv; i++) s += d->efc_J[r][i] * search[i];
+      jv[r] = s;
+    }
+    for (int i = 0; i < nv; i++) sn += search[i] * search[i];
+    double gtol = m->tolerance * m->ls_tolerance * sqrt(sn) * m->meaninertia * (nv > 1 ? nv : 1);
+    double gauss = 0, q1 = 0, q2 = 0;
+    for (int i = 0; i < nv; i++) {
+      gauss += (Ma[i] - d->qfrc_smooth[i]) * (qacc[i] - d->qacc_smooth[i]);
+      q1 += search[i] * (Ma[i] - d->qfrc_smooth[i]);
+      q2 += search[i] * Mv[i];
+    }
+    double qg[3] = {0.5 * gauss, q1, 0.5 * q2};
+    lspt p0 = ls_eval(d, qg, jar, jv, 0.0);
+    lspt lo = ls_eval(d, qg, jar, jv, p0.alpha - p0.d0 / p0.d1);
+    lspt hi;
+    if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
+    int swap = 1;
+    for (int ls = 0; ls < m->ls_iterations; ls++) {
+      if (!swap) break;
+      if (lo.d0 < 0 && lo.d0 > -gtol) break;
+      if (hi.d0 > 0 && hi.d0 < gtol) break;
+      lspt lo_next = ls_eval(d, qg, jar, jv, lo.alpha - lo.d0 / lo.d1);
+      lspt hi_next = ls_eval(d, qg, jar, jv, hi.alpha - hi.d0 / hi.d1);
+      lspt mid = ls_eval(d, qg, jar, jv, 0.5 * (lo.alpha + hi.alpha));
+      int s1 = lo.d0 > 0 || lo.d0 < lo_next.d0;
+      if (s1) lo = lo_next;
+      int s2 = mid.d0 < 0 && lo.d0 < mid.d0;
+      if (s2) lo = mid;
+      int s3 = hi.d0 < 0 || hi.d0 > hi_next.d0;
+      if (s3) hi = hi_next;
+      int s4 = mid.d0 > 0 && hi.d0 > mid.d0;
+      if (s4) hi = mid;
+      swap = s1 || s2 || s3 || s4;
+    }
+    int improved = lo.cost < p0.cost || hi.cost < p0.cost;
+    double alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+    if (improved) {
+      for (int i = 0; i < nv; i++) { qacc[i] += alpha * search[i]; Ma[i] += alpha * Mv[i]; }
+      for (int r = 0; r < nefc; r++) jar[r] += alpha * jv[r];
+    }
+    prev_cost = cost;
+    cost = solver_cost(m, d, qacc, Ma, jar);
+  }
+  memcpy(d->qacc, qacc, sizeof(double) * nv);
+}
+
+/* ------------------------------------------------------------------------ */
+/* step = forward + Euler (mj_step with eulerdamp disabled)                   */
+
+static void forward(const mpcr_model_t* m, odata* d) {
+  kinematics(m, d);
+  com_pos(m, d);
+  crb(m, d);
+  collision(m, d);
+  com_vel(m, d);
+  passive(m, d);
+  rne(m, d);
+  make_constraint(m, d);
+  for (int i = 0; i < m->nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i];
+  chol_solve(d->qacc_smooth, d->L, d->qfrc_smooth, m->nv);
+  solve(m, d);
+}
+
+static void euler(const mpcr_model_t* m, odata* d) {
+  double dt = m->timestep;
+  for (int i = 0; i < m->nv; i++) d->qvel[i] += dt * d->qacc[i];
+  for (int j = 0; j < m->njnt; j++) {
+    int a = m->jnt_qposadr[j], v = m->jnt_dofadr[j];
+    if (m->jnt_type[j] == MPCR_JNT_FREE) {
+      for (int k = 0; k < 3; k++) d->qpos[a + k] += dt * d->qvel[v + k];
+      a += 3; v += 3;
+    }
+    if (m->jnt_type[j] == MPCR_JNT_FREE || m->jnt_type[j] == MPCR_JNT_BALL) {
+      /* mju_quatIntegrate: q <- q * exp(omega_local * dt) */
+      double w[3] = {d->qvel[v], d->qvel[v + 1], d->qvel[v + 2]};
+      double ang = norm3(w) * dt;
+      double* q = d->qpos + a;
+      if (ang > MINVAL) {
+        double ax[3] = {w[0] * dt / ang, w[1] * dt / ang, w[2] * dt / ang}, dq[4];
+        axisangle(dq, ax, ang);
+        qmul(q, q, dq);
+      }
+      qnorm(q);
+    } else {
+      d->qpos[a] += dt * d->qvel[v];
+    }
+  }
+  memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * m->nv);
+}
+
+/* ------------------------------------------------------------------------ */
+/* exported API (ctypes)                                                      */
+
+int oracle_model_size(void) { return (int)sizeof(mpcr_model_t); }
+int oracle_data_size(void) { return (int)sizeof(odata); }
+
+/* One mj_step from (qpos, qvel, qacc_warmstart), all updated in place.
+   Optional outputs (NULL to skip): M (nv x nv), qfrc_bias, qfrc_passive,
+   qacc (the solved acceleration), eef (7: tcp xpos, hande xquat, pre-step),
+   dist (ncon slot distances, pre-step), nefc. */
+int oracle_step(const mpcr_model_t* m, double* qpos, double* qvel, double* qacc_ws, double* M_out,
+                double* bias_out, double* passive_out, double* qacc_out, double* eef_out, double* dist_out,
+                int* nefc_out) {
+  odata* d = (odata*)calloc(1, sizeof(odata));
+  if (!d) return -1;
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  memcpy(d->qvel, qvel, sizeof(double) * m->nv);
+  memcpy(d->qacc_warmstart, qacc_ws, sizeof(double) * m->nv);
+  forward(m, d);
+  if (M_out)
+    for (int i = 0; i < m->nv; i++)
+      for (int j = 0; j < m->nv; j++) M_out[i * m->nv + j] = d->M[i][j];
+  if (bias_out) memcpy(bias_out, d->qfrc_bias, sizeof(double) * m->nv);
+  if (passive_out) memcpy(passive_out, d->qfrc_passive, sizeof(double) * m->nv);
+  if (qacc_out) memcpy(qacc_out, d->qacc, sizeof(double) * m->nv);
+  if (eef_out) {
+    if (m->tcp_site >= 0) memcpy(eef_out, d->site_xpos[m->tcp_site], 3 * sizeof(double));
+    if (m->hande_body >= 0) memcpy(eef_out + 3, d->xquat[m->hande_body], 4 * sizeof(double));
+  }
+  if (dist_out)
+    for (int c = 0; c < m->ncon; c++) dist_out[c] = d->con[c].dist;
+  if (nefc_out) *nefc_out = d->nefc;
+  euler(m, d);
+  memcpy(qpos, d->qpos, sizeof(double) * m->nq);
+  memcpy(qvel, d->qvel, sizeof(double) * m->nv);
+  memcpy(qacc_ws, d->qacc_warmstart, sizeof(double) * m->nv);
+  int trunc = d->efc_trunc;
+  free(d);
+  return trunc ? 1 : 0;
+}
+
+/* Rollout + cost for n candidates (compute_rollout_single +
+   compute_cost_single, SBP/mjx_planner.py:265-303).
+     thetadot : n x (nctrl*H), joint-major (A_thetadot @ xi, :348)
+     q0       : nctrl initial joint positions
+     w        : (w_pos, w_rot, w_col);  ptgt (3), qtgt (4, wxyz)
+   outputs:
+     cost4    : n x 4 (cost, cost_g, cost_r, cost_c)
+     theta    : n x (nctrl*H) joint-major post-step qpos (nullable)
+     slots    : n x H x nslot masked contact distances (nullable)
+     eef      : n x H x 7 (tcp pos, hande quat) (nullable)              */
+int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, const double* q0,
+                   const double* w, const double* ptgt, const double* qtgt, double* cost4, double* theta,
+                   double* slots, double* eef) {
+  if (m->magic != MPCR_MODEL_MAGIC || m->nbytes != sizeof(mpcr_model_t)) return -2;
+  odata* d = (odata*)calloc(1, sizeof(odata));
+  double* cprev = (double*)calloc(m->nslot > 0 ? m->nslot : 1, sizeof(double));
+  if (!d || !cprev) { free(d); free(cprev); return -1; }
+  int nc = m->nctrl, status = 0;
+  double qt[4];
+  memcpy(qt, qtgt, sizeof(qt));
+  double qtn = sqrt(qt[0] * qt[0] + qt[1] * qt[1] + qt[2] * qt[2] + qt[3] * qt[3]);
+  for (int k = 0; k < 4; k++) qt[k] /= qtn;
+  for (int b = 0; b < n; b++) {
+    memset(d, 0, sizeof(odata));
+    memcpy(d->qpos, m->qpos_init, sizeof(double) * m->nq);
+    memcpy(d->qvel, m->qvel_init, sizeof(double) * m->nv);
+    for (int j = 0; j < nc; j++) d->qpos[m->ctrl_qposadr[j]] = q0[j];
+    double cg = 0, cr = 0, cc = 0;
+    const double* td = thetadot + (size_t)b * nc * H;
+    for (int t = 0; t < H; t++) {
+      for (int j = 0; j < nc; j++) d->qvel[m->ctrl_dofadr[j]] = td[j * H + t];
+      forward(m, d);
+      if (d->efc_trunc) status = 1;
+      /* eef pose and collision distances: pre-integration (from forward) */
+      const double* p = m->tcp_site >= 0 ? d->site_xpos[m->tcp_site] : d->xpos[0];
+      const double* q = m->hande_body >= 0 ? d->xquat[m->hande_body] : d->xquat[0];
+      double dp[3] = {p[0] - ptgt[0], p[1] - ptgt[1], p[2] - ptgt[2]};
+      cg += norm3(dp);
+      double qn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+      double dotq = fabs((q[0] * qt[0] + q[1] * qt[1] + q[2] * qt[2] + q[3] * qt[3]) / qn);
+      cr += 2 * acos(clampd(dotq, -1, 1));
+      if (eef) {
+        double* e = eef + ((size_t)b * H + t) * 7;
+        memcpy(e, p, 3 * sizeof(double));
+        memcpy(e + 3, q, 4 * sizeof(double));
+      }
+      for (int pi = 0; pi < m->npair; pi++) {
+        int sa = m->pair_slotadr[pi];
+        if (sa < 0) continue;
+        for (int s = 0; s < m->pair_ncon[pi]; s++) {
+          double c = d->con[m->pair_conadr[pi] + s].dist;
+          if (slots) slots[((size_t)b * H + t) * m->nslot + sa + s] = c;
+          if (c < 0) cc += 1;
+          if (t > 0) {
+            double g = cprev[sa + s] * (1 - 0.005) - c; /* y = 0.005, :287-291 */
+            if (g > 0) cc += g;
+          }
+          cprev[sa + s] = c;
+        }
+      }
+      euler(m, d);
+      if (theta)
+        for (int j = 0; j < nc; j++) theta[(size_t)b * nc * H + j * H + t] = d->qpos[m->ctrl_qposadr[j]];
+    }
+    cost4[4 * b + 0] = w[0] * cg + w[1] * cr + w[2] * cc;
+    cost4[4 * b + 1] = cg;
+    cost4[4 * b + 2] = cr;
+    cost4[4 * b + 3] = cc;
+  }
+  free(cprev);
+  free(d);
+  return status;
+}
