@@ -1,0 +1,44 @@
+"""Build libmpcr.so in-tree for gfx950 (hipcc, no JIT caches).
+
+    python -m manipulator_mujoco_amd.build
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = [os.path.join(HERE, "csrc", "engine.hip")]
+DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("rollout.hip", "mpcr_device.h")] + [
+    os.path.join(os.path.dirname(HERE), "include", f) for f in ("mpcr.h", "mpcr_model.h")]
+OUT = os.path.join(HERE, "libmpcr.so")
+ARCH = os.environ.get("MPCR_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and os.path.exists(OUT):
+        mt = os.path.getmtime(OUT)
+        if all(os.path.getmtime(d) <= mt for d in DEPS):
+            return OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-Wno-pass-failed", "-o", OUT + ".tmp"] + SRC
+    if verbose:
+        cmd.append("-Rpass-analysis=kernel-resource-usage")
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))

@@ -698,7 +698,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
   sync();
 
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
-  int status = 0;
+  int status = 0, nefc_sum = 0;
 
   for (int t = 0; t < H; t++) {
     // ---- qvel[:nctrl] = thetadot_t (basis evaluated on the fly) -------------
@@ -1282,6 +1282,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
       sync();
     }
     if (s.trunc) status |= 1;
+    nefc_sum += s.nefc;
 
     // ---- Newton solver (primal), MJX-style line search ------------------------
     {
@@ -1464,7 +1465,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     args.cost4[4 * (size_t)b + 1] = cost_g;
     args.cost4[4 * (size_t)b + 2] = cost_r;
     args.cost4[4 * (size_t)b + 3] = cost_c;
-    if (args.status) args.status[b] = status;
+    if (args.status) args.status[b] = status | (nefc_sum << 8);
     if (args.best_key) {
       const uint32_t u = __float_as_uint(cost);
       uint32_t key = isnan(cost) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));

@@ -1,0 +1,191 @@
+"""GPU parity gates: the HIP path through the C ABI vs the fp64 CPU oracle on
+identical inputs (cost within 1e-4 relative, the north-star tolerance), plus
+size-independent properties at the full BASELINE sizes."""
+import numpy as np
+import pytest
+
+import oracle
+from manipulator_mujoco_amd import basis, models
+from manipulator_mujoco_amd.engine import MPCR_LAYOUT_THETADOT, MPCR_LAYOUT_XI, Engine
+
+pytestmark = pytest.mark.gpu
+
+Q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
+W = np.array([20.0, 3.0, 80.0])
+PT = np.array([-0.3, -0.3, 0.5])
+QT = np.array([0.0, 1.0, 0.0, 0.0])
+TOL = 1e-4  # north star: costs within 1e-4 relative fp32
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch
+
+
+def projected_xi(n, H, seed, device):
+    """BASELINE.md synthetic inputs: xi ~ N(0, 10.003 I) projected with 10 ADMM iterations."""
+    import torch
+
+    from manipulator_mujoco_amd.projection import ProjectionFilter
+    _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
+    f = ProjectionFilter(P, Pd, Pdd, 6, device)
+    rng = np.random.default_rng(seed)
+    xi = torch.tensor(rng.normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32), device=device)
+    return f(xi, f.boundary(Q0, np.zeros(6), np.zeros(6), n), 10)
+
+
+def compare(m, g, o, H):
+    gc, oc = g["cost4"].astype(np.float64), o["cost4"]
+    rel = np.abs(gc[:, 0] - oc[:, 0]) / np.maximum(np.abs(oc[:, 0]), 1e-6)
+    # candidates grazing a contact (|dist| < 1e-5 somewhere) can flip the
+    # integer #{c < 0} term between fp32 and fp64: reported separately
+    if m.nslot:
+        graze = (np.abs(o["slots"]) < 1e-5).any(axis=(1, 2))
+    else:
+        graze = np.zeros(len(rel), bool)
+    return rel, graze
+
+
+@pytest.mark.parametrize("name", list(models.BUNDLES))
+@pytest.mark.parametrize("layout", [MPCR_LAYOUT_XI, MPCR_LAYOUT_THETADOT])
+def test_parity_small(torch_cuda, name, layout):
+    n, H = 64, 20
+    m = models.load(name, 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    rng = np.random.default_rng(11)
+    if layout == MPCR_LAYOUT_XI:
+        inp = rng.normal(0, 0.05, (n, 66)).astype(np.float32)
+        td = np.einsum("tk,njk->njt", Pd, inp.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
+    else:
+        t = np.arange(H) * 0.05
+        inp = (rng.uniform(-0.7, 0.7, (n, 6, 1)) * np.sin(rng.uniform(0.2, 2, (n, 6, 1)) * t)).reshape(n, 6 * H)
+        inp = inp.astype(np.float32)
+        td = inp.astype(np.float64)
+    e = Engine(m, H, n, Pd)
+    g = e.trace(inp, layout, Q0, W, PT, QT)
+    o = oracle.rollout(m, td, Q0, W, PT, QT, want_slots=True, want_eef=True)
+    rel, graze = compare(m, g, o, H)
+    assert rel[~graze].max() < TOL, rel.max()
+    assert graze.mean() < 0.1
+    assert np.abs(g["theta"] - o["theta"]).max() < 1e-4
+    assert np.abs(g["eef"][..., :3] - o["eef"][..., :3]).max() < 1e-4
+    if m.nslot:
+        assert np.abs(g["slots"] - o["slots"]).max() < 1e-4
+
+
+@pytest.mark.parametrize("name", ["planner_scene", "scene_mjx", "ur5e_hande_mjx"])
+def test_parity_projected_h50(torch_cuda, name):
+    """Realistic samples (projected to |thetadot| <= 0.8): arm/table/box contacts occur."""
+    torch = torch_cuda
+    n, H = 256, 50
+    m = models.load(name, 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 3, torch.device("cuda:0"))
+    xi_h = xi.cpu().numpy()
+    e = Engine(m, H, n, Pd)
+    g = e.trace(xi_h, MPCR_LAYOUT_XI, Q0, W, PT, QT)
+    td = np.einsum("tk,njk->njt", Pd, xi_h.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
+    o = oracle.rollout(m, td, Q0, W, PT, QT, want_slots=True, want_eef=True)
+    rel, graze = compare(m, g, o, H)
+    ok = rel[~graze] < TOL
+    assert ok.mean() >= 0.98, (ok.mean(), np.sort(rel)[-5:])
+    assert np.median(rel) < 1e-5
+    # the selected candidate agrees
+    assert int(np.argmin(g["cost4"][:, 0])) == int(np.argmin(o["cost4"][:, 0]))
+
+
+def test_thetadot_and_theta_outputs(torch_cuda):
+    torch = torch_cuda
+    n, H = 128, 50
+    m = models.load("scene_mjx", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 5, torch.device("cuda:0"))
+    e = Engine(m, H, n, Pd)
+    td = torch.empty((n, 6 * H), device="cuda:0")
+    th = torch.empty((n, 6 * H), device="cuda:0")
+    key = torch.empty(1, dtype=torch.int64, device="cuda:0")
+    c4 = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, theta=th, thetadot=td, best_key=key)
+    torch.cuda.synchronize()
+    ref = np.einsum("tk,njk->njt", Pd, xi.cpu().numpy().reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
+    np.testing.assert_allclose(td.cpu().numpy(), ref, atol=2e-5)
+    # first post-step theta ~ q0 + dt * thetadot_0
+    th0 = th.cpu().numpy()[:, ::H]
+    assert np.abs(th0 - (Q0 + 0.05 * ref[:, ::H])).max() < 0.05
+    from manipulator_mujoco_amd import _lib
+    idx, val = _lib.decode_key(int(key.item()) & 0xFFFFFFFFFFFFFFFF)
+    c = c4.cpu().numpy()
+    assert idx == int(np.argmin(c[:, 0])) and val == c[idx, 0]
+
+
+def test_argmin_nan_first_and_ties(torch_cuda):
+    import ctypes
+    torch = torch_cuda
+    from manipulator_mujoco_amd import _lib
+    _, P, Pd, _ = basis.planner_basis(20, 0.05)
+    e = Engine(models.load("planner_scene", 0.05), 20, 4096, Pd)
+    lib = _lib.load()
+    c = np.random.default_rng(2).uniform(1, 9, (3000, 4)).astype(np.float32)
+    c[1234, 0] = c[2345, 0] = -5.0
+    idx, val = ctypes.c_int(), ctypes.c_float()
+    assert lib.mpcr_argmin(e.handle, c.ctypes.data, 4, 3000, 0, None, ctypes.byref(idx), ctypes.byref(val), 0,
+                           None) == 0
+    assert idx.value == 1234 and val.value == -5.0
+    c[2999, 0] = np.nan
+    c[2000, 0] = np.nan
+    assert lib.mpcr_argmin(e.handle, c.ctypes.data, 4, 3000, 100, None, ctypes.byref(idx), ctypes.byref(val), 0,
+                           None) == 0
+    assert idx.value == 2100 and np.isnan(val.value)
+
+
+def test_full_size_properties(torch_cuda):
+    """C3 at the BASELINE size (4096 x 50): finite, deterministic, sharding-invariant."""
+    torch = torch_cuda
+    n, H = 4096, 50
+    m = models.load("scene_mjx", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 3, torch.device("cuda:0"))
+    e = Engine(m, H, n, Pd)
+    st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    key = torch.empty(1, dtype=torch.int64, device="cuda:0")
+    a = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, best_key=key, status=st).clone()
+    b = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)  # bitwise deterministic
+    assert torch.isfinite(a).all()
+    assert int((st & 1).sum()) == 0  # no constraint-row truncation
+    half = n // 2
+    k2 = torch.empty(1, dtype=torch.int64, device="cuda:0")
+    c1 = e.rollout_cost(xi[:half].contiguous(), MPCR_LAYOUT_XI, Q0, W, PT, QT).clone()
+    c2 = e.rollout_cost(xi[half:].contiguous(), MPCR_LAYOUT_XI, Q0, W, PT, QT, best_key=k2, index_base=half).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([c1, c2]), a)
+    from manipulator_mujoco_amd import _lib
+    i_full, _ = _lib.decode_key(int(key.item()) & 0xFFFFFFFFFFFFFFFF)
+    i_hi, _ = _lib.decode_key(int(k2.item()) & 0xFFFFFFFFFFFFFFFF)
+    assert i_full == int(torch.argmin(a[:, 0]))
+    assert i_hi == half + int(torch.argmin(a[half:, 0]))
+    # a 64-candidate sample of the full-size batch still matches the oracle
+    sel = np.arange(0, n, n // 64)
+    td = np.einsum("tk,njk->njt", Pd, xi.cpu().numpy()[sel].reshape(-1, 6, 11).astype(np.float64)).reshape(-1, 6 * H)
+    o = oracle.rollout(m, td, Q0, W, PT, QT, want_theta=False)["cost4"]
+    rel = np.abs(a.cpu().numpy()[sel, 0] - o[:, 0]) / np.abs(o[:, 0])
+    assert (rel < TOL).mean() >= 0.95, np.sort(rel)[-4:]
+
+
+def test_compute_cem_dropin(torch_cuda):
+    from manipulator_mujoco_amd.planner import cem_planner
+    p = cem_planner(num_dof=6, num_batch=256, num_steps=16, timestep=0.05, maxiter_cem=3, num_elite=0.05,
+                    w_pos=20.0, w_rot=3.0, w_col=80.0, maxiter_projection=10, verbose=False)
+    out = p.compute_cem(np.zeros(p.nvar), Q0, np.zeros(6), np.zeros(6), PT, QT)
+    cost, cg, cr, cc, best_vels, best_traj, xi_mean, thetadot, theta = out
+    assert cost.shape == (3,) and best_vels.shape == (16, 6) and best_traj.shape == (16, 6)
+    assert xi_mean.shape == (66,) and thetadot.shape == (3, 256, 96) and theta.shape == (3, 256, 96)
+    assert np.isfinite(cost).all() and cost[-1] <= cost[0] * 1.5
+    # best_vels is the argmin row of the last iteration's thetadot
+    k = np.where((thetadot[-1] == best_vels.T.reshape(-1)).all(axis=1))[0]
+    assert k.size >= 1
+    # the same call is deterministic (fixed key, SBP/mjx_planner.py:388)
+    out2 = p.compute_cem(np.zeros(p.nvar), Q0, np.zeros(6), np.zeros(6), PT, QT)
+    np.testing.assert_array_equal(out2[0], cost)
