@@ -525,6 +525,34 @@ extern "C" int mpcr_rollout_trace(mpcr_engine* e, const float* input, int layout
   return rc;
 }
 
+#ifdef MPCR_PROFILE
+// diagnostic build only: per-phase s_memtime cycles summed over all waves
+extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
+                                    const float* w, const float* ptgt, const float* qtgt,
+                                    unsigned long long* phases16) {
+  HIPCHK(hipSetDevice(e->device));
+  const int nc = e->host.nctrl;
+  const size_t cols = layout == MPCR_LAYOUT_XI ? (size_t)nc * e->nbasis : (size_t)nc * e->H;
+  unsigned long long* d_prof = nullptr;
+  HIPCHK(hipMalloc(&d_prof, 16 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(d_prof, 0, 16 * sizeof(unsigned long long)));
+  HIPCHK(hipMemcpy(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice));
+  RolloutArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
+  a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
+  for (int k = 0; k < nc; k++) a.q0[k] = (float)q0[k];
+  for (int k = 0; k < 3; k++) { a.w[k] = w[k]; a.ptgt[k] = ptgt[k]; }
+  float qn = std::sqrt(qtgt[0] * qtgt[0] + qtgt[1] * qtgt[1] + qtgt[2] * qtgt[2] + qtgt[3] * qtgt[3]);
+  for (int k = 0; k < 4; k++) a.qtgt[k] = qtgt[k] / qn;
+  hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, nullptr, a);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(phases16, d_prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  (void)hipFree(d_prof);
+  return MPCR_OK;
+}
+#endif
+
 extern "C" void mpcr_best_key_decode(uint64_t key, int* idx, float* cost) {
   uint32_t hi = (uint32_t)(key >> 32);
   if (idx) *idx = (int)(uint32_t)(key & 0xffffffffu);

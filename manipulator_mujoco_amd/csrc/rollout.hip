@@ -34,6 +34,7 @@ struct RolloutArgs {
   int* status;
   float* trace_eef;    // n x H x 7 (debug)
   float* trace_slots;  // n x H x nslot (debug)
+  unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
   int layout, n, H, nbasis, index_base, pad_;
   float q0[DX_NCTRL];
   float w[4];
@@ -81,6 +82,25 @@ struct __align__(16) Smem {
   int efc_src[DX_MAXEFC];  // (kind << 24) | (index << 4) | side
   int ncon, nefc, trunc, pad_;
 };
+
+// ---------------------------------------------------------------------------
+// diagnostic phase stamps (separate -DMPCR_PROFILE build; never in the timed one)
+#ifdef MPCR_PROFILE
+#define PROF_DECL unsigned long long prof_acc[16] = {0}; unsigned long long prof_last = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                              \
+  do {                                                        \
+    unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
+    prof_acc[i] += now_ - prof_last;                          \
+    prof_last = now_;                                         \
+  } while (0)
+#define PROF_FLUSH                                                          \
+  if (lane == 0 && args.prof)                                               \
+    for (int i_ = 0; i_ < 16; i_++) atomicAdd(&args.prof[i_], prof_acc[i_]);
+#else
+#define PROF_DECL
+#define STAMP(i)
+#define PROF_FLUSH
+#endif
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -699,6 +719,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
 
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
   int status = 0, nefc_sum = 0;
+  PROF_DECL
 
   for (int t = 0; t < H; t++) {
     // ---- qvel[:nctrl] = thetadot_t (basis evaluated on the fly) -------------
@@ -716,6 +737,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
     sync();
 
+    STAMP(0);
     // ---- kinematics: local pose per body, then pointer jumping ----------------
     {
       float q[4] = {1.f, 0.f, 0.f, 0.f}, p[3] = {0.f, 0.f, 0.f};
@@ -788,6 +810,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
     sync();
 
+    STAMP(1);
     // ---- geom poses, tree COMs ------------------------------------------------
     if (lane < m->ngeom) {
       const int gb = m->geom_body[lane];
@@ -853,6 +876,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
       }
     }
 
+    STAMP(2);
     // ---- cinert, cdof ---------------------------------------------------------
     if (lane < nb) {
       const int tr = m->body_tree[lane];
@@ -925,6 +949,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
     sync();
 
+    STAMP(3);
     // ---- CRB, velocity, RNE + gravcomp (subtree sums by bitmask) -----------
     for (int idx = lane; idx < nb * 10; idx += WAVE) {
       const int bb = idx / 10, k = idx - bb * 10;
@@ -1002,6 +1027,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
       s.cfrc[lane][5] = f[5] + vf[5] - F[2];
     }
     sync();
+    STAMP(4);
     // mass matrix entries (chain-masked) + bias forces
     for (int idx = lane; idx < DX_NV * DX_NV; idx += WAVE) {
       const int i = idx >> 4, j = idx & 15;
@@ -1038,6 +1064,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
     sync();
 
+    STAMP(5);
     // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
     float Lm[DX_NV];
     {
@@ -1050,6 +1077,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
     sync();
 
+    STAMP(6);
     // ---- collision: lanes over pairs; cost_c on masked slots; compaction ----
     if (lane == 0) { s.ncon = 0; s.trunc = 0; }
     sync();
@@ -1121,6 +1149,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     if (lane == 0 && s.ncon > DX_MAXACT) { s.trunc = 1; s.ncon = DX_MAXACT; }
     sync();
 
+    STAMP(7);
     // ---- constraint rows: equality, limits, contacts ------------------------
     {
       const int neq = (m->disableflags & 64) ? 0 : m->neq;
@@ -1284,6 +1313,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     if (s.trunc) status |= 1;
     nefc_sum += s.nefc;
 
+    STAMP(8);
     // ---- Newton solver (primal), MJX-style line search ------------------------
     {
       const int nefc = s.nefc;
@@ -1418,6 +1448,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
       }
     }
 
+    STAMP(9);
     // ---- Euler: qvel += dt qacc; integrate qpos; warm start -----------------
     {
       const float dt = m->timestep;
@@ -1453,6 +1484,8 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
   }
 
+  STAMP(10);
+  PROF_FLUSH
   // ---- final reductions, outputs ----------------------------------------------
   cost_c = wsum(cost_c);
   bool finite = true;

@@ -1,0 +1,54 @@
+"""Diagnostic: per-phase cycle shares of the rollout kernel (s_memtime stamps).
+Builds a separate -DMPCR_PROFILE library; never used for timing claims."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from manipulator_mujoco_amd import _lib, basis, build, models  # noqa: E402
+
+PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rne", "M/bias", "M solve",
+          "collision", "constraint rows", "newton", "euler"]
+
+
+def main():
+    so = os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr_prof.so")
+    subprocess.run([build.hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMPCR_PROFILE",
+                    "-Wno-pass-failed", "-o", so] + build.SRC, check=True)
+    _lib.LIB_PATH = so
+    lib = _lib.load()
+    lib.mpcr_rollout_profile.restype = ctypes.c_int
+    vp, P_ = ctypes.c_void_p, ctypes.POINTER
+    lib.mpcr_rollout_profile.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, P_(ctypes.c_double),
+                                         P_(ctypes.c_float), P_(ctypes.c_float), P_(ctypes.c_float), vp]
+    import torch
+    from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine
+    from manipulator_mujoco_amd.projection import ProjectionFilter
+    name = sys.argv[1] if len(sys.argv) > 1 else "scene_mjx"
+    n, H = int(os.environ.get("N", 4096)), 50
+    m = models.load(name, 0.05)
+    _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
+    proj = ProjectionFilter(P, Pd, Pdd, 6, torch.device("cpu"))
+    q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
+    xi = proj(torch.tensor(np.random.default_rng(20250632).normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32)),
+              proj.boundary(q0, np.zeros(6), np.zeros(6), n), 10).numpy()
+    e = Engine(m, H, n, Pd)
+    ph = (ctypes.c_ulonglong * 16)()
+    f = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
+    w, pt, qt = np.array([20, 3, 80.]), np.array([-0.3, -0.3, 0.5]), np.array([0, 1, 0, 0.])
+    for _ in range(2):
+        ph = (ctypes.c_ulonglong * 16)()
+        _lib.check(lib.mpcr_rollout_profile(e.handle, xi.ctypes.data, MPCR_LAYOUT_XI, n,
+                                            q0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), f(w), f(pt), f(qt), ph))
+    tot = sum(ph[:11])
+    print(f"{name}: n={n} H={H} cycles/wave-step {tot / n / H:.0f}")
+    for i, p in enumerate(PHASES):
+        print(f"  {p:16s} {ph[i] / n / H:10.0f} cyc  {100 * ph[i] / tot:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
