@@ -339,6 +339,8 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.pair_g1[p] = gmap[g1];
     d.pair_g2[p] = gmap[g2];
     d.pair_func[p] = m.pair_func[p];
+    if (m.pair_func[p] == MPCR_COL_BOX_BOX && m.pair_slotadr[p] >= 0)
+      return fail(MPCR_EMODEL, "robot-masked box-box pairs are not supported by the kernel");
     d.pair_ncon[p] = m.pair_ncon[p];
     d.pair_slotadr[p] = m.pair_slotadr[p];
     d.pair_condim[p] = m.pair_condim[p];

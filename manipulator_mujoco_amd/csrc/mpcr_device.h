@@ -9,18 +9,18 @@
 namespace mpcr {
 
 constexpr int WAVE = 64;
-constexpr int DX_NB = 32;    // bodies
+constexpr int DX_NB = 16;    // moving bodies
 constexpr int DX_NV = 16;    // dofs (padded register width of the dense solves)
 constexpr int DX_NQ = 24;
 constexpr int DX_NJ = 16;
-constexpr int DX_NG = 32;    // collision geoms (remapped)
+constexpr int DX_NG = 24;    // collision geoms (remapped)
 constexpr int DX_NP = 256;   // pairs
 constexpr int DX_NEQ = 4;
 constexpr int DX_NCTRL = 8;
 constexpr int DX_NTREE = 4;
-constexpr int DX_MAXACT = 24;  // active contacts kept per step
-constexpr int DX_MAXEFC = 112; // constraint rows kept per step
-constexpr int DX_NSLOT = 256;  // robot-masked contact slots
+constexpr int DX_MAXACT = 20;  // active contacts kept per step
+constexpr int DX_MAXEFC = 96;  // constraint rows kept per step
+constexpr int DX_NSLOT = 192;  // robot-masked contact slots
 
 // body kinds for the kinematics pass
 enum { BK_STATIC = 0, BK_FREE = 1, BK_HINGE = 2, BK_SLIDE = 3, BK_WELD = 4 };

@@ -42,45 +42,56 @@ struct RolloutArgs {
   float qtgt[4];  // normalised
 };
 
+constexpr int LDM = DX_NV + 1;  // padded row strides: row-parallel access
+constexpr int LDJ = DX_NV + 1;  // is bank-conflict free
+
 struct __align__(16) Smem {
+  // ---- persistent across the step ----
   float xi[DX_NCTRL * 16];
   float qpos[DX_NQ];
   float qvel[DX_NV];
   float qacc[DX_NV];
   float qws[DX_NV];
-  float qfs[DX_NV];  // qfrc_smooth
-  float qas[DX_NV];  // qacc_smooth
-  float vec0[DX_NV];
-  float vec1[DX_NV];
-  float xpos[DX_NB][4];
-  float xquat[DX_NB][4];
-  float xmat[DX_NB][12];
-  float xipos[DX_NB][4];
+  float qfs[DX_NV];   // qfrc_smooth
+  float qas[DX_NV];   // qacc_smooth
+  float srch[DX_NV];  // Newton search direction
   float com[DX_NTREE][4];
-  float cinert[DX_NB][12];
-  float crb[DX_NB][12];
-  float cvel[DX_NB][8];
-  float cfrc[DX_NB][8];
   float cdof[DX_NV][8];
-  float cdofdot[DX_NV][8];
-  float fvec[DX_NV][8];
-  float M[DX_NV][DX_NV];
-  float Lsh[DX_NV][DX_NV];  // transpose scratch of the register Cholesky
+  float M[DX_NV][LDM];
   float gxpos[DX_NG][4];
   float gxmat[DX_NG][12];
-  float con_pos[DX_MAXACT][4];
-  float con_frame[DX_MAXACT][12];
-  float con_dist[DX_MAXACT];
-  int con_pair[DX_MAXACT];
-  float J[DX_MAXEFC][DX_NV];
-  float efc_pos[DX_MAXEFC];
-  float efc_D[DX_MAXEFC];
-  float efc_aref[DX_MAXEFC];
-  float efc_jar[DX_MAXEFC];
-  float efc_jv[DX_MAXEFC];
-  float cprev[DX_NSLOT];   // previous-step masked slot distances (cost_c)
-  int efc_src[DX_MAXEFC];  // (kind << 24) | (index << 4) | side
-  int ncon, nefc, trunc, pad_;
+  float cprev[DX_NSLOT];  // previous-step masked slot distances (cost_c)
+  int ncon, nefc, pad_[2];
+  // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the
+  //      contact / constraint arrays (collision .. Newton) ----
+  union {
+    struct {
+      float xpos[DX_NB][4];
+      float xquat[DX_NB][4];
+      float xmat[DX_NB][12];
+      float xipos[DX_NB][4];
+      float cinert[DX_NB][12];
+      float crb[DX_NB][12];
+      float cvel[DX_NB][8];
+      float cfrc[DX_NB][8];
+      float cdofdot[DX_NV][8];
+      float fvec[DX_NV][8];
+    };
+    struct {
+      float con_pos[DX_MAXACT][4];
+      float con_frame[DX_MAXACT][12];
+      float con_dist[DX_MAXACT];
+      int con_pair[DX_MAXACT];
+      int con_row[DX_MAXACT];
+      float poly[2][8][4];  // box-box clipping polygon (double buffered)
+      float J[DX_MAXEFC][LDJ];
+      float efc_D[DX_MAXEFC];
+      float efc_aref[DX_MAXEFC];
+      float efc_jar[DX_MAXEFC];
+      float efc_jv[DX_MAXEFC];
+      int efc_src[DX_MAXEFC];  // (kind << 24) | (index << 4) | side
+    };
+  };
 };
 
 // ---------------------------------------------------------------------------
@@ -105,21 +116,37 @@ struct __align__(16) Smem {
 // ---------------------------------------------------------------------------
 // wave helpers
 
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ int wscan_incl(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < WAVE; o <<= 1) {
-    int t = __shfl_up(v, o);
-    if (lane >= o) v += t;
-  }
-  return v;
-}
 __device__ __forceinline__ float rdlane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// full-wave sum, result uniform: DPP inside each 16-lane row (quad_perm
+// [1,0,3,2], [2,3,0,1], row_ror:4, row_ror:8) + 4 readlanes.  No LDS
+// traffic (a __shfl_xor butterfly is 6 dependent ds_bpermute round trips).
+__device__ __forceinline__ float wsum(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x124>(v);
+  v += dppf<0x128>(v);
+  return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
+}
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+// exclusive prefix sum of small per-lane counts (0..7) by bit-plane ballots
+__device__ __forceinline__ int wscan_excl(int v, int& total) {
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int bit = 0; bit < 3; bit++) {
+    const unsigned long long mk = __ballot((v >> bit) & 1);
+    pre += lanes_below(mk) << bit;
+    tot += __popcll(mk) << bit;
+  }
+  total = tot;
+  return pre;
 }
 __device__ __forceinline__ void sync() { __syncthreads(); }
 
@@ -207,37 +234,28 @@ __device__ __forceinline__ void chol_rows(float (&a)[DX_NV], int lane) {
   }
 }
 
-// forward/back substitution; L rows in registers, one rhs value per lane.
-// Uses vtmp (LDS, DX_NV floats) to transpose for the back substitution.
-__device__ __forceinline__ float chol_solve(const float (&l)[DX_NV], float b, int lane,
-                                            float (*Lsh)[DX_NV]) {
-  // forward: y_i = (b_i - sum_{k<i} L_ik y_k) / L_ii
-  float acc = b, y = 0.f;
+// x = L^-T L^-1 b with the factor rows in registers (lane k holds row k) and
+// one rhs value per lane: both substitutions run on uniform values fetched
+// with v_readlane (no LDS transpose, no barrier).  Returns x[lane].
+__device__ __forceinline__ float chol_solve(const float (&l)[DX_NV], float b, int lane) {
+  float y[DX_NV];
 #pragma unroll
   for (int k = 0; k < DX_NV; k++) {
-    float yk_l = acc / l[k];  // valid on lane k
-    float yk = rdlane(yk_l, k);
-    if (lane == k) y = yk;
-    if (lane > k) acc = fmaf(-l[k], yk, acc);
-  }
-  // back: x_i = (y_i - sum_{k>i} L_ki x_k) / L_ii ; need column i of L
-  if (lane < DX_NV) {
+    float acc = rdlane(b, k);
 #pragma unroll
-    for (int j = 0; j < DX_NV; j++) Lsh[lane][j] = l[j];
+    for (int j = 0; j < k; j++) acc = fmaf(-rdlane(l[j], k), y[j], acc);
+    y[k] = acc / rdlane(l[k], k);
   }
-  sync();
-  float x = 0.f;
-  acc = y;
-  float lii = lane < DX_NV ? Lsh[lane][lane] : 1.f;
+  float xl = 0.f;
 #pragma unroll
   for (int k = DX_NV - 1; k >= 0; k--) {
-    float xk_l = acc / lii;
-    float xk = rdlane(xk_l, k);
-    if (lane == k) x = xk;
-    if (lane < k) acc = fmaf(-Lsh[k][lane < DX_NV ? lane : 0], xk, acc);
+    float acc = y[k];
+#pragma unroll
+    for (int j = k + 1; j < DX_NV; j++) acc = fmaf(-rdlane(l[k], j), y[j], acc);
+    y[k] = acc / rdlane(l[k], k);
+    if (lane == k) xl = y[k];
   }
-  sync();
-  return x;
+  return xl;
 }
 
 // ---------------------------------------------------------------------------
@@ -275,25 +293,29 @@ __device__ __forceinline__ float point_box(const float p[3], const float h[3], f
     out2 += o[k] * o[k];
   }
   if (out2 > 0) {
-    float l = sqrtf(out2);
+    const float l = sqrtf(out2);
 #pragma unroll
     for (int k = 0; k < 3; k++) nl[k] = o[k] / l;
     return l;
   }
+  // inside: the deepest face is argmax_k |p_k| - h_k (first maximum)
+  const float g0 = fabsf(p[0]) - h[0], g1 = fabsf(p[1]) - h[1], g2 = fabsf(p[2]) - h[2];
   int best = 0;
-  float g = fabsf(p[0]) - h[0];
-  if (fabsf(p[1]) - h[1] > g) { g = fabsf(p[1]) - h[1]; best = 1; }
-  if (fabsf(p[2]) - h[2] > g) { g = fabsf(p[2]) - h[2]; best = 2; }
-  float sg = p[best] >= 0 ? 1.f : -1.f;
-  nl[0] = nl[1] = nl[2] = 0;
-  nl[best] = -sg;
-  q[0] = p[0]; q[1] = p[1]; q[2] = p[2];
-  q[best] = sg * h[best];
+  float g = g0;
+  if (g1 > g) { g = g1; best = 1; }
+  if (g2 > g) { g = g2; best = 2; }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float sg = p[k] >= 0 ? 1.f : -1.f;
+    nl[k] = k == best ? -sg : 0.f;
+    q[k] = k == best ? sg * h[k] : p[k];
+  }
   return g;
 }
 
-// out: dist[4], pos[4][3], nrm[4][3]; returns number of slots written
-__device__ __noinline__ int narrow_phase(const DevModel* __restrict__ m, const Smem& s, int p, float dist[4],
+// per-lane narrow phase for plane/capsule/box-vs-capsule pairs (box-box is
+// wave-cooperative, below).  out: dist[4], pos[4][3], nrm[4][3]
+__device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const Smem& s, int p, float dist[4],
                             float pos[4][3], float nrm[4][3]) {
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   const int func = m->pair_func[p];
@@ -471,160 +493,6 @@ __device__ __noinline__ int narrow_phase(const DevModel* __restrict__ m, const S
     }
     return 2;
   }
-  if (func == 4) {  // box - box: SAT + reference-face clipping
-    float axA[3][3], axB[3][3], t[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int c = 0; c < 3; c++) { axA[i][c] = R1[3 * c + i]; axB[i][c] = R2[3 * c + i]; }
-#pragma unroll
-    for (int c = 0; c < 3; c++) t[c] = x2[c] - x1[c];
-    const float* ha = s1;
-    const float* hb = s2;
-    float best_face = -1e30f, best_edge = -1e30f, Lf[3] = {0, 0, 1}, Le[3] = {0, 0, 1};
-    int face_id = -1, edge_i = -1, edge_j = -1;
-#pragma unroll
-    for (int ax = 0; ax < 6; ax++) {
-      const float* L = ax < 3 ? axA[ax] : axB[ax - 3];
-      float ra = 0, rb = 0;
-#pragma unroll
-      for (int k = 0; k < 3; k++) { ra += ha[k] * fabsf(dot3(axA[k], L)); rb += hb[k] * fabsf(dot3(axB[k], L)); }
-      float sep = fabsf(dot3(t, L)) - ra - rb;
-      if (sep > best_face) { best_face = sep; face_id = ax; Lf[0] = L[0]; Lf[1] = L[1]; Lf[2] = L[2]; }
-    }
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) {
-        float L[3];
-        cross(L, axA[i], axB[j]);
-        float l = sqrtf(dot3(L, L));
-        if (l >= 1e-6f) {
-          L[0] /= l; L[1] /= l; L[2] /= l;
-          float ra = 0, rb = 0;
-#pragma unroll
-          for (int k = 0; k < 3; k++) { ra += ha[k] * fabsf(dot3(axA[k], L)); rb += hb[k] * fabsf(dot3(axB[k], L)); }
-          float sep = fabsf(dot3(t, L)) - ra - rb;
-          if (sep > best_edge) { best_edge = sep; edge_i = i; edge_j = j; Le[0] = L[0]; Le[1] = L[1]; Le[2] = L[2]; }
-        }
-      }
-    float best = fmaxf(best_face, best_edge);
-    dist[0] = best;
-    const float margin = m->pair_margin[p];
-    if (best >= margin) return 4;
-    bool use_edge = edge_i >= 0 && best_edge > 0.95f * best_face + 1e-5f;
-    const float* L = use_edge ? Le : Lf;
-    float sg = dot3(t, L) >= 0 ? 1.f : -1.f;
-    float n[3] = {sg * L[0], sg * L[1], sg * L[2]};
-    if (use_edge) {
-      float pa[3], pb[3], da[3], db[3];
-#pragma unroll
-      for (int c = 0; c < 3; c++) { pa[c] = x1[c]; pb[c] = x2[c]; }
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        if (k != edge_i) {
-          float s_ = dot3(n, axA[k]) >= 0 ? 1.f : -1.f;
-#pragma unroll
-          for (int c = 0; c < 3; c++) pa[c] += s_ * ha[k] * axA[k][c];
-        }
-        if (k != edge_j) {
-          float s_ = dot3(n, axB[k]) >= 0 ? -1.f : 1.f;
-#pragma unroll
-          for (int c = 0; c < 3; c++) pb[c] += s_ * hb[k] * axB[k][c];
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 3; c++) {
-        pa[c] -= ha[edge_i] * axA[edge_i][c]; da[c] = 2 * ha[edge_i] * axA[edge_i][c];
-        pb[c] -= hb[edge_j] * axB[edge_j][c]; db[c] = 2 * hb[edge_j] * axB[edge_j][c];
-      }
-      float sc, uc;
-      seg_seg(pa, da, pb, db, &sc, &uc);
-      dist[0] = best_edge;
-#pragma unroll
-      for (int c = 0; c < 3; c++) {
-        pos[0][c] = 0.5f * (pa[c] + sc * da[c] + pb[c] + uc * db[c]);
-        nrm[0][c] = n[c];
-      }
-      return 4;
-    }
-    const bool refA = face_id < 3;
-    const int fi = refA ? face_id : face_id - 3;
-    const float* cr = refA ? x1 : x2;
-    const float* ci = refA ? x2 : x1;
-    const float* hr = refA ? ha : hb;
-    const float* hi = refA ? hb : ha;
-    float axR[3][3], axI[3][3];
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int c = 0; c < 3; c++) { axR[i][c] = refA ? axA[i][c] : axB[i][c]; axI[i][c] = refA ? axB[i][c] : axA[i][c]; }
-    float nf[3] = {refA ? n[0] : -n[0], refA ? n[1] : -n[1], refA ? n[2] : -n[2]};
-    int ki = 0;
-    float bestdot = -1;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      float v = fabsf(dot3(axI[k], nf));
-      if (v > bestdot) { bestdot = v; ki = k; }
-    }
-    float si = dot3(axI[ki], nf) > 0 ? -1.f : 1.f;
-    int u = ki == 0 ? 1 : (ki == 1 ? 2 : 0), v = ki == 0 ? 2 : (ki == 1 ? 0 : 1);
-    float poly[8][3], tmpp[8][3];
-    int np = 4;
-    const float su[4] = {1, -1, -1, 1}, sv[4] = {1, 1, -1, -1};
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-#pragma unroll
-      for (int k = 0; k < 3; k++)
-        poly[c][k] = ci[k] + si * hi[ki] * axI[ki][k] + su[c] * hi[u] * axI[u][k] + sv[c] * hi[v] * axI[v][k];
-    for (int pl = 0; pl < 4 && np > 0; pl++) {
-      int ax = (fi + 1 + (pl >> 1)) % 3;
-      float sgn = (pl & 1) ? -1.f : 1.f;
-      float cra = dot3(cr, axR[ax]);
-      int nn = 0;
-      for (int c = 0; c < np; c++) {
-        const int c2 = c + 1 == np ? 0 : c + 1;
-        float dp = sgn * (dot3(poly[c], axR[ax]) - cra) - hr[ax];
-        float dq = sgn * (dot3(poly[c2], axR[ax]) - cra) - hr[ax];
-        if (dp <= 0) { tmpp[nn][0] = poly[c][0]; tmpp[nn][1] = poly[c][1]; tmpp[nn][2] = poly[c][2]; nn++; }
-        if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
-          float wgt = dp / (dp - dq);
-#pragma unroll
-          for (int k = 0; k < 3; k++) tmpp[nn][k] = poly[c][k] + wgt * (poly[c2][k] - poly[c][k]);
-          nn++;
-        }
-      }
-      np = nn;
-      for (int c = 0; c < np; c++) { poly[c][0] = tmpp[c][0]; poly[c][1] = tmpp[c][1]; poly[c][2] = tmpp[c][2]; }
-    }
-    float depth[8];
-    int keep[8], nkeep = 0;
-    for (int c = 0; c < np; c++) {
-      float rel[3] = {poly[c][0] - cr[0], poly[c][1] - cr[1], poly[c][2] - cr[2]};
-      depth[c] = hr[fi] - dot3(rel, nf);
-      if (-depth[c] < margin) keep[nkeep++] = c;
-    }
-    dist[0] = 1e30f;
-    if (nkeep == 0) return 4;
-    int pick[4], npick;
-    if (nkeep <= 4) {
-      for (int c = 0; c < nkeep; c++) pick[c] = keep[c];
-      npick = nkeep;
-    } else {
-      int d0 = 0;
-      for (int c = 1; c < nkeep; c++)
-        if (depth[keep[c]] > depth[keep[d0]]) d0 = c;
-      for (int k = 0; k < 4; k++) pick[k] = keep[(d0 + k * nkeep / 4) % nkeep];
-      npick = 4;
-    }
-    for (int k = 0; k < npick; k++) {
-      int c = pick[k];
-      dist[k] = -depth[c];
-#pragma unroll
-      for (int e = 0; e < 3; e++) { pos[k][e] = poly[c][e] + nf[e] * 0.5f * depth[c]; nrm[k][e] = n[e]; }
-    }
-    return 4;
-  }
   return 0;
 }
 
@@ -651,6 +519,249 @@ __device__ __forceinline__ float impedance(const float* si, float pos, float mar
   else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
   else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
   return dmin + y * (dmax - dmin);
+}
+
+// Box-box, wave-cooperative (one pair, all 64 lanes, uniform control flow):
+// lanes 0..14 evaluate the 15 separating axes, the reference-face clipping
+// (Sutherland-Hodgman against the 4 side planes) runs with one lane per
+// polygon edge and ballot compaction, the >4 selection is done on uniform
+// values.  Same definitions and orders as the oracle's col_box_box.
+// Appends up to 4 contacts to the active list.  Must be called by all lanes.
+__device__ void box_box_wave(const DevModel* __restrict__ m, Smem& s, int p, int lane) {
+  const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
+  const float margin = m->pair_margin[p];
+  float x1[3], x2[3], axA[3][3], axB[3][3], t[3], ha[3], hb[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    x1[c] = s.gxpos[g1][c];
+    x2[c] = s.gxpos[g2][c];
+    t[c] = x2[c] - x1[c];
+    ha[c] = m->geom_size[g1][c];
+    hb[c] = m->geom_size[g2][c];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) { axA[i][c] = s.gxmat[g1][3 * c + i]; axB[i][c] = s.gxmat[g2][3 * c + i]; }
+  // ---- separating axes, one per lane
+  float L[3] = {0.f, 0.f, 1.f}, sep = -3e38f;
+  bool valid = false;
+  if (lane < 6) {
+    const int ia = lane < 3 ? lane : lane - 3;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const float va = ia == 0 ? axA[0][c] : (ia == 1 ? axA[1][c] : axA[2][c]);
+      const float vb = ia == 0 ? axB[0][c] : (ia == 1 ? axB[1][c] : axB[2][c]);
+      L[c] = lane < 3 ? va : vb;
+    }
+    valid = true;
+  } else if (lane < 15) {
+    const int i = (lane - 6) / 3, j = (lane - 6) % 3;
+    float ai[3], bj[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      ai[c] = i == 0 ? axA[0][c] : (i == 1 ? axA[1][c] : axA[2][c]);
+      bj[c] = j == 0 ? axB[0][c] : (j == 1 ? axB[1][c] : axB[2][c]);
+    }
+    cross(L, ai, bj);
+    const float l = sqrtf(dot3(L, L));
+    valid = l >= 1e-6f;
+    if (valid) { L[0] /= l; L[1] /= l; L[2] /= l; }
+  }
+  if (valid) {
+    float ra = 0.f, rb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) { ra += ha[k] * fabsf(dot3(axA[k], L)); rb += hb[k] * fabsf(dot3(axB[k], L)); }
+    sep = fabsf(dot3(t, L)) - ra - rb;
+  }
+  float best_face = -1e30f, best_edge = -1e30f;
+  int face_id = -1, edge_lane = -1;
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+    const float v = rdlane(sep, a);
+    if (v > best_face) { best_face = v; face_id = a; }
+  }
+#pragma unroll
+  for (int a = 6; a < 15; a++) {
+    const float v = rdlane(sep, a);
+    if (v > -1e30f && v > best_edge) { best_edge = v; edge_lane = a; }
+  }
+  const float best = fmaxf(best_face, best_edge);
+  if (!(best < margin)) return;
+  const bool use_edge = edge_lane >= 0 && best_edge > 0.95f * best_face + 1e-5f;
+  const int src = use_edge ? edge_lane : face_id;
+  float n[3] = {rdlane(L[0], src), rdlane(L[1], src), rdlane(L[2], src)};
+  const float sg = dot3(t, n) >= 0.f ? 1.f : -1.f;
+  n[0] *= sg; n[1] *= sg; n[2] *= sg;
+  const int base = s.ncon;
+  sync();
+  if (use_edge) {
+    const int ei = (edge_lane - 6) / 3, ej = (edge_lane - 6) % 3;
+    float pa[3], pb[3], da[3], db[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) { pa[c] = x1[c]; pb[c] = x2[c]; }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (k != ei) {
+        const float s_ = dot3(n, axA[k]) >= 0.f ? 1.f : -1.f;
+#pragma unroll
+        for (int c = 0; c < 3; c++) pa[c] += s_ * ha[k] * axA[k][c];
+      }
+      if (k != ej) {
+        const float s_ = dot3(n, axB[k]) >= 0.f ? -1.f : 1.f;
+#pragma unroll
+        for (int c = 0; c < 3; c++) pb[c] += s_ * hb[k] * axB[k][c];
+      }
+    }
+    const float hae = ei == 0 ? ha[0] : (ei == 1 ? ha[1] : ha[2]);
+    const float hbe = ej == 0 ? hb[0] : (ej == 1 ? hb[1] : hb[2]);
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const float ae = ei == 0 ? axA[0][c] : (ei == 1 ? axA[1][c] : axA[2][c]);
+      const float be = ej == 0 ? axB[0][c] : (ej == 1 ? axB[1][c] : axB[2][c]);
+      pa[c] -= hae * ae; da[c] = 2.f * hae * ae;
+      pb[c] -= hbe * be; db[c] = 2.f * hbe * be;
+    }
+    float sc, uc;
+    seg_seg(pa, da, pb, db, &sc, &uc);
+    if (lane == 0 && base < DX_MAXACT) {
+      float f[9];
+      make_frame(f, n);
+#pragma unroll
+      for (int c = 0; c < 3; c++) s.con_pos[base][c] = 0.5f * (pa[c] + sc * da[c] + pb[c] + uc * db[c]);
+#pragma unroll
+      for (int e = 0; e < 9; e++) s.con_frame[base][e] = f[e];
+      s.con_dist[base] = best_edge;
+      s.con_pair[base] = p;
+    }
+    sync();
+    if (lane == 0) s.ncon = base + 1;
+    sync();
+    return;
+  }
+  // ---- face contact: reference box owns the face axis.  All indices below
+  // are uniform but run-time; select explicitly so nothing lives in scratch.
+  const bool refA = face_id < 3;
+  const int fi = refA ? face_id : face_id - 3;
+  float cr[3], ci[3], nf[3], R0[3], R1[3], R2[3], I0[3], I1[3], I2[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    cr[c] = refA ? x1[c] : x2[c];
+    ci[c] = refA ? x2[c] : x1[c];
+    nf[c] = refA ? n[c] : -n[c];
+    R0[c] = refA ? axA[0][c] : axB[0][c];
+    R1[c] = refA ? axA[1][c] : axB[1][c];
+    R2[c] = refA ? axA[2][c] : axB[2][c];
+    I0[c] = refA ? axB[0][c] : axA[0][c];
+    I1[c] = refA ? axB[1][c] : axA[1][c];
+    I2[c] = refA ? axB[2][c] : axA[2][c];
+  }
+  const float hr0 = refA ? ha[0] : hb[0], hr1 = refA ? ha[1] : hb[1], hr2 = refA ? ha[2] : hb[2];
+  const float hi0 = refA ? hb[0] : ha[0], hi1 = refA ? hb[1] : ha[1], hi2 = refA ? hb[2] : ha[2];
+  const float d0 = fabsf(dot3(I0, nf)), d1 = fabsf(dot3(I1, nf)), d2 = fabsf(dot3(I2, nf));
+  int ki = 0;
+  float bestdot = d0;
+  if (d1 > bestdot) { bestdot = d1; ki = 1; }
+  if (d2 > bestdot) { bestdot = d2; ki = 2; }
+  const int u = ki == 0 ? 1 : (ki == 1 ? 2 : 0), v = ki == 0 ? 2 : (ki == 1 ? 0 : 1);
+  float Ik[3], Iu[3], Iv[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    Ik[c] = ki == 0 ? I0[c] : (ki == 1 ? I1[c] : I2[c]);
+    Iu[c] = u == 0 ? I0[c] : (u == 1 ? I1[c] : I2[c]);
+    Iv[c] = v == 0 ? I0[c] : (v == 1 ? I1[c] : I2[c]);
+  }
+  const float hk = ki == 0 ? hi0 : (ki == 1 ? hi1 : hi2);
+  const float hu = u == 0 ? hi0 : (u == 1 ? hi1 : hi2);
+  const float hv = v == 0 ? hi0 : (v == 1 ? hi1 : hi2);
+  const float si = dot3(Ik, nf) > 0.f ? -1.f : 1.f;
+  if (lane < 4) {
+    const float su = (lane == 0 || lane == 3) ? 1.f : -1.f, sv = lane < 2 ? 1.f : -1.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) s.poly[0][lane][k] = ci[k] + si * hk * Ik[k] + su * hu * Iu[k] + sv * hv * Iv[k];
+  }
+  int np = 4, cur = 0;
+  for (int pl = 0; pl < 4 && np > 0; pl++) {
+    sync();
+    const int ax = (fi + 1 + (pl >> 1)) % 3;
+    const float sgn = (pl & 1) ? -1.f : 1.f;
+    float Ra[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) Ra[c] = ax == 0 ? R0[c] : (ax == 1 ? R1[c] : R2[c]);
+    const float hax = ax == 0 ? hr0 : (ax == 1 ? hr1 : hr2);
+    const float cra = dot3(cr, Ra);
+    float P[3] = {0.f, 0.f, 0.f}, Q[3] = {0.f, 0.f, 0.f}, dp = 0.f, dq = 0.f;
+    int e0 = 0, e1 = 0;
+    if (lane < np) {
+      const int c2 = lane + 1 == np ? 0 : lane + 1;
+#pragma unroll
+      for (int k = 0; k < 3; k++) { P[k] = s.poly[cur][lane][k]; Q[k] = s.poly[cur][c2][k]; }
+      dp = sgn * (dot3(P, Ra) - cra) - hax;
+      dq = sgn * (dot3(Q, Ra) - cra) - hax;
+      e0 = dp <= 0.f;
+      e1 = (dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f);
+    }
+    int tot;
+    const int o = wscan_excl(e0 + e1, tot);
+    if (e0) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) s.poly[cur ^ 1][o][k] = P[k];
+    }
+    if (e1) {
+      const float wgt = dp / (dp - dq);
+#pragma unroll
+      for (int k = 0; k < 3; k++) s.poly[cur ^ 1][o + e0][k] = P[k] + wgt * (Q[k] - P[k]);
+    }
+    np = tot;
+    cur ^= 1;
+  }
+  sync();
+  if (np == 0) return;
+  const float hrf = fi == 0 ? hr0 : (fi == 1 ? hr1 : hr2);
+  float depth = -3e38f;
+  bool keep = false;
+  if (lane < np) {
+    const float rel[3] = {s.poly[cur][lane][0] - cr[0], s.poly[cur][lane][1] - cr[1], s.poly[cur][lane][2] - cr[2]};
+    depth = hrf - dot3(rel, nf);
+    keep = -depth < margin;
+  }
+  const unsigned long long km = __ballot(keep);
+  const int nkeep = __popcll(km);
+  if (nkeep == 0) return;
+  const int rank = lanes_below(km);  // position of this lane among the kept points
+  int slot = keep ? rank : -1;
+  int npick = nkeep;
+  if (nkeep > 4) {
+    // deepest kept point (first maximum), then evenly spaced around the polygon
+    int d0 = 0;
+    float dbest = -3e38f;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const float dc = rdlane(depth, c);
+      const bool kc = (km >> c) & 1ull;
+      const int rc = __popcll(km & ((1ull << c) - 1ull));
+      if (kc && dc > dbest) { dbest = dc; d0 = rc; }
+    }
+    slot = -1;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (keep && rank == (d0 + q * nkeep / 4) % nkeep) slot = q;
+    npick = 4;
+  }
+  if (slot >= 0 && base + slot < DX_MAXACT) {
+    const int o = base + slot;
+    float f[9];
+    make_frame(f, n);
+#pragma unroll
+    for (int k = 0; k < 3; k++) s.con_pos[o][k] = s.poly[cur][lane][k] + nf[k] * 0.5f * depth;
+#pragma unroll
+    for (int e = 0; e < 9; e++) s.con_frame[o][e] = f[e];
+    s.con_dist[o] = -depth;
+    s.con_pair[o] = p;
+  }
+  sync();
+  if (lane == 0) s.ncon = base + npick;
+  sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -690,12 +801,34 @@ __device__ __forceinline__ LsPt ls_eval(const Smem& s, int lane, const float qg[
   return ls_make(alpha, q0, q1, q2);
 }
 
+// three line-search points in one pass over the rows; the 9 reductions are
+// independent so their DPP chains interleave
+__device__ __forceinline__ void ls_eval3(const Smem& s, int lane, const float qg[3], float a0, float a1, float a2,
+                                         LsPt& p0, LsPt& p1, LsPt& p2) {
+  float q[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float al[3] = {a0, a1, a2};
+  for (int r = lane; r < s.nefc; r += WAVE) {
+    const float jar = s.efc_jar[r], jv = s.efc_jv[r], D = s.efc_D[r];
+    const bool eq = (s.efc_src[r] >> 24) == 1;
+    const float c0 = 0.5f * D * jar * jar, c1 = D * jv * jar, c2 = 0.5f * D * jv * jv;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (eq || jar + al[k] * jv < 0.f) { q[3 * k] += c0; q[3 * k + 1] += c1; q[3 * k + 2] += c2; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) q[k] = wsum(q[k]) + qg[k % 3];
+  p0 = ls_make(a0, q[0], q[1], q[2]);
+  p1 = ls_make(a1, q[3], q[4], q[5]);
+  p2 = ls_make(a2, q[6], q[7], q[8]);
+}
+
 // ---------------------------------------------------------------------------
 // the kernel
 
 __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
   __shared__ Smem s;
-  const DevModel* __restrict__ m = args.m;
+  const DevModel* m = args.m;
   const int lane = threadIdx.x;
   const int b = blockIdx.x;
   if (b >= args.n) return;
@@ -722,6 +855,11 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
   PROF_DECL
 
   for (int t = 0; t < H; t++) {
+    // Launder the model pointer every step: otherwise the compiler hoists
+    // every loop-invariant model load out of the horizon loop and keeps them
+    // all live across the whole step (244 VGPRs + SGPR spills).  The loads
+    // stay in their phases and hit L1/L2.
+    asm volatile("" : "+s"(m));
     // ---- qvel[:nctrl] = thetadot_t (basis evaluated on the fly) -------------
     if (lane < nc) {
       float v;
@@ -738,6 +876,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     sync();
 
     STAMP(0);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // ---- kinematics: local pose per body, then pointer jumping ----------------
     {
       float q[4] = {1.f, 0.f, 0.f, 0.f}, p[3] = {0.f, 0.f, 0.f};
@@ -811,6 +950,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     sync();
 
     STAMP(1);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // ---- geom poses, tree COMs ------------------------------------------------
     if (lane < m->ngeom) {
       const int gb = m->geom_body[lane];
@@ -877,6 +1017,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
 
     STAMP(2);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // ---- cinert, cdof ---------------------------------------------------------
     if (lane < nb) {
       const int tr = m->body_tree[lane];
@@ -950,6 +1091,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     sync();
 
     STAMP(3);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // ---- CRB, velocity, RNE + gravcomp (subtree sums by bitmask) -----------
     for (int idx = lane; idx < nb * 10; idx += WAVE) {
       const int bb = idx / 10, k = idx - bb * 10;
@@ -1028,6 +1170,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
     sync();
     STAMP(4);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // mass matrix entries (chain-masked) + bias forces
     for (int idx = lane; idx < DX_NV * DX_NV; idx += WAVE) {
       const int i = idx >> 4, j = idx & 15;
@@ -1065,39 +1208,43 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     sync();
 
     STAMP(5);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
-    float Lm[DX_NV];
     {
+      float Lm[DX_NV];
 #pragma unroll
-      for (int j = 0; j < DX_NV; j++) Lm[j] = lane < DX_NV ? s.M[lane][j] : (lane == j ? 1.f : 0.f);
+      for (int j = 0; j < DX_NV; j++) Lm[j] = lane < DX_NV ? s.M[lane][j] : 0.f;
       chol_rows(Lm, lane);
-      float rhs = lane < DX_NV ? s.qfs[lane] : 0.f;
-      float x = chol_solve(Lm, rhs, lane, s.Lsh);
+      const float x = chol_solve(Lm, lane < DX_NV ? s.qfs[lane] : 0.f, lane);
       if (lane < DX_NV) s.qas[lane] = lane < nv ? x : 0.f;
     }
-    sync();
 
     STAMP(6);
-    // ---- collision: lanes over pairs; cost_c on masked slots; compaction ----
-    if (lane == 0) { s.ncon = 0; s.trunc = 0; }
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    // ---- collision: lanes over pairs (typed segments); cost_c on the masked
+    //      slots; active contacts compacted into the list; box-box pairs
+    //      that pass the bounding-sphere cull are solved wave-cooperatively
+    if (lane == 0) s.ncon = 0;
     sync();
     for (int k = 0; k * WAVE < m->npair; k++) {
       const int p = lane + k * WAVE;
-      float dist[4], pos[4][3], nrm[4][3];
-      int nslot = 0, act = 0;
-      if (p < m->npair) {
+      const bool valid = p < m->npair;
+      const int func = valid ? m->pair_func[p] : -1;
+      bool run = valid;
+      if (valid && m->pair_slotadr[p] < 0) {
         const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
-        bool run = true;
-        if (m->pair_slotadr[p] < 0 && m->geom_type[g1] != 0) {
-          float dx = s.gxpos[g2][0] - s.gxpos[g1][0], dy = s.gxpos[g2][1] - s.gxpos[g1][1],
-                dz = s.gxpos[g2][2] - s.gxpos[g1][2];
+        if (m->geom_type[g1] != 0) {
+          const float dx = s.gxpos[g2][0] - s.gxpos[g1][0], dy = s.gxpos[g2][1] - s.gxpos[g1][1],
+                      dz = s.gxpos[g2][2] - s.gxpos[g1][2];
           run = sqrtf(dx * dx + dy * dy + dz * dz) <= m->geom_rbound[g1] + m->geom_rbound[g2] + m->pair_margin[p];
         }
-        if (run) nslot = narrow_phase(m, s, p, dist, pos, nrm);
-        else {
-#pragma unroll
-          for (int c = 0; c < 4; c++) dist[c] = 1e30f;
-        }
+      }
+      float dist[4] = {1e30f, 1e30f, 1e30f, 1e30f}, pos[4][3], nrm[4][3];
+      int nsl = 0;
+      if (run && func != 4) nsl = narrow_lane(m, s, p, dist, pos, nrm);
+      const unsigned long long bbm = __ballot(run && func == 4);
+      int act = 0;
+      if (valid && func != 4) {
         const int sa = m->pair_slotadr[p];
         if (sa >= 0) {
           const int ns = m->pair_ncon[p];
@@ -1113,20 +1260,20 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
           }
         }
         if (!(m->disableflags & 16)) {
+          const float mg = m->pair_margin[p];
 #pragma unroll
-          for (int c = 0; c < 4; c++)
-            if (c < nslot && dist[c] < m->pair_margin[p]) act++;
+          for (int c = 0; c < 4; c++) act += (c < nsl && dist[c] < mg) ? 1 : 0;
         }
       }
-      // append active contacts
-      const int incl = wscan_incl(act, lane);
+      int tot;
+      const int pre = wscan_excl(act, tot);
       const int base = s.ncon;
-      const int total = __shfl(incl, WAVE - 1);
-      int o = base + incl - act;
       if (act) {
+        const float mg = m->pair_margin[p];
+        int o = base + pre;
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-          if (c < nslot && dist[c] < m->pair_margin[p]) {
+          if (c < nsl && dist[c] < mg) {
             if (o < DX_MAXACT) {
               float f[9];
               make_frame(f, nrm[c]);
@@ -1141,17 +1288,29 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         }
       }
       sync();
-      if (lane == 0) {
-        s.ncon = base + total;
+      if (lane == 0) s.ncon = base + tot;
+      sync();
+      if (bbm && !(m->disableflags & 16)) {
+        unsigned long long mm = bbm;
+        while (mm) {
+          const int q = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          box_box_wave(m, s, k * WAVE + q, lane);
+        }
       }
+    }
+    if (s.ncon > DX_MAXACT) {
+      status |= 1;
+      sync();
+      if (lane == 0) s.ncon = DX_MAXACT;
       sync();
     }
-    if (lane == 0 && s.ncon > DX_MAXACT) { s.trunc = 1; s.ncon = DX_MAXACT; }
-    sync();
 
     STAMP(7);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // ---- constraint rows: equality, limits, contacts ------------------------
     {
+      const int ncon = s.ncon;
       const int neq = (m->disableflags & 64) ? 0 : m->neq;
       int nlim_l = 0, lsides = 0;
       if (lane < m->njnt && !(m->disableflags & 32) && m->jnt_limited[lane] &&
@@ -1160,39 +1319,35 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         if (q - m->jnt_range[lane][0] < m->jnt_margin[lane]) { nlim_l++; lsides |= 1; }
         if (m->jnt_range[lane][1] - q < m->jnt_margin[lane]) { nlim_l++; lsides |= 2; }
       }
-      const int lim_incl = wscan_incl(nlim_l, lane);
-      const int nlim = __shfl(lim_incl, WAVE - 1);
+      int nlim;
+      const int lim_pre = wscan_excl(nlim_l, nlim);
       int ncr = 0;
-      if (lane < s.ncon) ncr = m->pair_condim[s.con_pair[lane]] == 1 ? 1 : 4;
-      const int con_incl = wscan_incl(ncr, lane);
-      const int ncrow = __shfl(con_incl, WAVE - 1);
+      if (lane < ncon) ncr = m->pair_condim[s.con_pair[lane]] == 1 ? 1 : 4;
+      int ncrow;
+      const int con_pre = wscan_excl(ncr, ncrow);
       int nefc = neq + nlim + ncrow;
-      // capacity: drop trailing contacts that do not fit
-      int keep_con = s.ncon;
-      if (nefc > DX_MAXEFC) {
-        // largest prefix of contacts whose rows fit
+      int keep_con = ncon;
+      if (nefc > DX_MAXEFC) {  // keep the longest prefix of contacts that fits
         const int room = DX_MAXEFC - neq - nlim;
-        const bool fits = con_incl <= room;
-        const unsigned long long bal = __ballot(lane < s.ncon && fits);
-        keep_con = __popcll(bal);
-        const int rows_kept = keep_con > 0 ? __shfl(con_incl, keep_con - 1) : 0;
-        nefc = neq + nlim + rows_kept;
-        if (lane == 0) s.trunc = 1;
+        const unsigned long long fit = __ballot(lane < ncon && con_pre + ncr <= room);
+        keep_con = __popcll(fit);
+        nefc = neq + nlim + (keep_con > 0 ? __shfl(con_pre + ncr, keep_con - 1) : 0);
+        status |= 1;
       }
-      // row sources
       if (lane < neq) s.efc_src[lane] = (1 << 24) | (lane << 4);
       if (nlim_l) {
-        int o = neq + lim_incl - nlim_l;
+        int o = neq + lim_pre;
         if (lsides & 1) s.efc_src[o++] = (2 << 24) | (lane << 4) | 0;
         if (lsides & 2) s.efc_src[o++] = (2 << 24) | (lane << 4) | 1;
       }
       if (lane < keep_con) {
-        int o = neq + nlim + con_incl - ncr;
+        const int o = neq + nlim + con_pre;
+        s.con_row[lane] = o;
         for (int r = 0; r < ncr; r++) s.efc_src[o + r] = (3 << 24) | (lane << 4) | r;
       }
       if (lane == 0) s.nefc = nefc;
       sync();
-      // Jacobian entries: (row, dof) for equality/limit rows
+      // Jacobian entries of equality/limit rows: (row, dof)
       const int nsimple = neq + nlim;
       for (int idx = lane; idx < nsimple * DX_NV; idx += WAVE) {
         const int r = idx >> 4, i = idx & 15;
@@ -1211,7 +1366,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         }
         s.J[r][i] = v;
       }
-      // contact Jacobians: (contact, dof)
+      // contact Jacobians: (contact, dof) -> J_n +- mu J_t rows
       for (int idx = lane; idx < keep_con * DX_NV; idx += WAVE) {
         const int c = idx >> 4, i = idx & 15;
         const int p = s.con_pair[c];
@@ -1234,12 +1389,8 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         }
         const float* f = s.con_frame[c];
         const float jn = f[0] * jd[0] + f[1] * jd[1] + f[2] * jd[2];
-        // locate this contact's first row
-        const int cond = m->pair_condim[p];
-        // row offset = neq + nlim + (rows of contacts before c)
-        int off = neq + nlim;
-        for (int cc = 0; cc < c; cc++) off += m->pair_condim[s.con_pair[cc]] == 1 ? 1 : 4;
-        if (cond == 1) {
+        const int off = s.con_row[c];
+        if (m->pair_condim[p] == 1) {
           s.J[off][i] = jn;
         } else {
           const float mu = m->pair_friction[p];
@@ -1252,7 +1403,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         }
       }
       sync();
-      // row parameters: vel, imp, D, aref
+      // row parameters: vel, impedance, D, aref
       for (int r = lane; r < nefc; r += WAVE) {
         const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
         float pos, margin, diag;
@@ -1293,7 +1444,8 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         for (int i = 0; i < DX_NV; i++) vel = fmaf(s.J[r][i], s.qvel[i], vel);
         const float imp = impedance(simp, pos, margin);
         const float R = fmaxf((1.f - imp) / imp * diag, kMinVal);
-        float tc = sref[0], dr = sref[1];
+        float tc = sref[0];
+        const float dr = sref[1];
         const float dmax = clampf(simp[1], kMinImp, kMaxImp);
         float K, B;
         if (tc > 0.f) {
@@ -1306,49 +1458,49 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         }
         s.efc_D[r] = 1.f / R;
         s.efc_aref[r] = -B * vel - K * imp * (pos - margin);
-        s.efc_pos[r] = pos;
       }
       sync();
     }
-    if (s.trunc) status |= 1;
     nefc_sum += s.nefc;
 
     STAMP(8);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // ---- Newton solver (primal), MJX-style line search ------------------------
     {
       const int nefc = s.nefc;
       float qacc_l = lane < DX_NV ? s.qas[lane] : 0.f;  // this lane's dof value
       if (nefc > 0) {
-        // warm start: better of qacc_warmstart and qacc_smooth
-        float cw = 0.f, cs = 0.f;
+        // warm start: the better of qacc_warmstart and qacc_smooth
         if (!(m->disableflags & 4)) {
+          float maw = 0.f, mas = 0.f;
+          if (lane < nv) {
 #pragma unroll
-          for (int pass = 0; pass < 2; pass++) {
-            const float* x = pass == 0 ? s.qws : s.qas;
-            float ma = 0.f;
-            if (lane < nv) {
-#pragma unroll
-              for (int j = 0; j < DX_NV; j++) ma = fmaf(s.M[lane][j], x[j], ma);
+            for (int j = 0; j < DX_NV; j++) {
+              maw = fmaf(s.M[lane][j], s.qws[j], maw);
+              mas = fmaf(s.M[lane][j], s.qas[j], mas);
             }
-            float g = lane < nv ? (ma - s.qfs[lane]) * (x[lane] - s.qas[lane]) : 0.f;
-            float c = 0.f;
-            for (int r = lane; r < nefc; r += WAVE) {
-              float jar = -s.efc_aref[r];
-#pragma unroll
-              for (int i = 0; i < DX_NV; i++) jar = fmaf(s.J[r][i], x[i], jar);
-              if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) c += s.efc_D[r] * jar * jar;
-            }
-            const float tot = 0.5f * wsum(g) + 0.5f * wsum(c);
-            if (pass == 0) cw = tot; else cs = tot;
           }
-          if (cw < cs && lane < DX_NV) qacc_l = s.qws[lane];
+          const float gw = lane < nv ? (maw - s.qfs[lane]) * (s.qws[lane] - s.qas[lane]) : 0.f;
+          const float gs = lane < nv ? (mas - s.qfs[lane]) * (s.qas[lane] - s.qas[lane]) : 0.f;
+          float cw = 0.f, cs = 0.f;
+          for (int r = lane; r < nefc; r += WAVE) {
+            float jw = -s.efc_aref[r], js = -s.efc_aref[r];
+#pragma unroll
+            for (int i = 0; i < DX_NV; i++) { jw = fmaf(s.J[r][i], s.qws[i], jw); js = fmaf(s.J[r][i], s.qas[i], js); }
+            const bool eq = (s.efc_src[r] >> 24) == 1;
+            if (eq || jw < 0.f) cw += s.efc_D[r] * jw * jw;
+            if (eq || js < 0.f) cs += s.efc_D[r] * js * js;
+          }
+          const float costw = 0.5f * wsum(gw) + 0.5f * wsum(cw);
+          const float costs = 0.5f * wsum(gs) + 0.5f * wsum(cs);
+          if (costw < costs && lane < DX_NV) qacc_l = s.qws[lane];
         }
         if (lane < DX_NV) s.qacc[lane] = qacc_l;
         sync();
         const float scale = 1.f / (m->meaninertia * (float)(nv > 1 ? nv : 1));
         float prev_cost = 3.4e38f;
         for (int it = 0;; it++) {
-          // Ma, jar, cost, grad
+          // Ma, jar, cost, grad at the current qacc
           float ma = 0.f;
           if (lane < nv) {
 #pragma unroll
@@ -1379,7 +1531,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
           // Hessian rows: H = M + J^T D_active J
           float h[DX_NV];
 #pragma unroll
-          for (int j = 0; j < DX_NV; j++) h[j] = lane < DX_NV ? s.M[lane][j] : (lane == j ? 1.f : 0.f);
+          for (int j = 0; j < DX_NV; j++) h[j] = lane < DX_NV ? s.M[lane][j] : 0.f;
           if (lane < nv) {
             for (int r = 0; r < nefc; r++) {
               const float jar = s.efc_jar[r];
@@ -1391,20 +1543,20 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
             }
           }
           chol_rows(h, lane);
-          const float mg = chol_solve(h, lane < nv ? grad : 0.f, lane, s.Lsh);
+          const float mg = chol_solve(h, lane < nv ? grad : 0.f, lane);
           const float search = lane < nv ? -mg : 0.f;
-          if (lane < DX_NV) s.vec1[lane] = search;
+          if (lane < DX_NV) s.srch[lane] = search;
           sync();
           // Mv, jv, quadratic coefficients
           float mvv = 0.f;
           if (lane < nv) {
 #pragma unroll
-            for (int j = 0; j < DX_NV; j++) mvv = fmaf(s.M[lane][j], s.vec1[j], mvv);
+            for (int j = 0; j < DX_NV; j++) mvv = fmaf(s.M[lane][j], s.srch[j], mvv);
           }
           for (int r = lane; r < nefc; r += WAVE) {
             float jv = 0.f;
 #pragma unroll
-            for (int i = 0; i < DX_NV; i++) jv = fmaf(s.J[r][i], s.vec1[i], jv);
+            for (int i = 0; i < DX_NV; i++) jv = fmaf(s.J[r][i], s.srch[i], jv);
             s.efc_jv[r] = jv;
           }
           const float sn = sqrtf(wsum(search * search));
@@ -1423,9 +1575,9 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
             if (!swap) break;
             if (lo.d0 < 0.f && lo.d0 > -gtol) break;
             if (hi.d0 > 0.f && hi.d0 < gtol) break;
-            LsPt lo_next = ls_eval(s, lane, qg, lo.alpha - lo.d0 / lo.d1);
-            LsPt hi_next = ls_eval(s, lane, qg, hi.alpha - hi.d0 / hi.d1);
-            LsPt mid = ls_eval(s, lane, qg, 0.5f * (lo.alpha + hi.alpha));
+            LsPt lo_next, hi_next, mid;
+            ls_eval3(s, lane, qg, lo.alpha - lo.d0 / lo.d1, hi.alpha - hi.d0 / hi.d1, 0.5f * (lo.alpha + hi.alpha),
+                     lo_next, hi_next, mid);
             const bool s1 = lo.d0 > 0.f || lo.d0 < lo_next.d0;
             if (s1) lo = lo_next;
             const bool s2 = mid.d0 < 0.f && lo.d0 < mid.d0;
@@ -1438,7 +1590,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
           }
           const bool improved = lo.cost < p0.cost || hi.cost < p0.cost;
           const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
-          if (improved && lane < DX_NV) s.qacc[lane] = s.qacc[lane] + alpha * s.vec1[lane];
+          if (improved && lane < DX_NV) s.qacc[lane] = s.qacc[lane] + alpha * s.srch[lane];
           prev_cost = cost;
           sync();
         }
@@ -1449,6 +1601,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
 
     STAMP(9);
+    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
     // ---- Euler: qvel += dt qacc; integrate qpos; warm start -----------------
     {
       const float dt = m->timestep;

@@ -111,9 +111,10 @@ def test_thetadot_and_theta_outputs(torch_cuda):
     torch.cuda.synchronize()
     ref = np.einsum("tk,njk->njt", Pd, xi.cpu().numpy().reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
     np.testing.assert_allclose(td.cpu().numpy(), ref, atol=2e-5)
-    # first post-step theta ~ q0 + dt * thetadot_0
+    # first post-step theta = q0 + dt*thetadot_0 + dt^2*qacc_0; C3 has no
+    # gravcomp, so gravity sags the arm by up to dt^2 * ~25 rad/s^2
     th0 = th.cpu().numpy()[:, ::H]
-    assert np.abs(th0 - (Q0 + 0.05 * ref[:, ::H])).max() < 0.05
+    assert np.abs(th0 - (Q0 + 0.05 * ref[:, ::H])).max() < 0.1
     from manipulator_mujoco_amd import _lib
     idx, val = _lib.decode_key(int(key.item()) & 0xFFFFFFFFFFFFFFFF)
     c = c4.cpu().numpy()
