@@ -42,31 +42,36 @@ struct RolloutArgs {
   float qtgt[4];  // normalised
 };
 
-constexpr int LDM = DX_NV + 1;  // padded row strides: row-parallel access
-constexpr int LDJ = DX_NV + 1;  // is bank-conflict free
+// Row stride 20 floats (80 B): rows are 16-byte aligned for ds_read_b128 and
+// a 16-lane ds_read_b128 group touching 16 different rows covers all 64
+// banks exactly once (20*r mod 64 are distinct multiples of 4) -> conflict
+// free for row-parallel access, 4x fewer LDS instructions than b32.
+constexpr int LDM = 20;
+constexpr int LDJ = 20;
+constexpr int LDL = 20;
 
 struct __align__(16) Smem {
   // ---- persistent across the step ----
   float xi[DX_NCTRL * 16];
   float qpos[DX_NQ];
-  float qvel[DX_NV];
-  float qacc[DX_NV];
-  float qws[DX_NV];
-  float qfs[DX_NV];   // qfrc_smooth
-  float qas[DX_NV];   // qacc_smooth
-  float srch[DX_NV];  // Newton search direction
+  alignas(16) float qvel[DX_NV];
+  alignas(16) float qacc[DX_NV];
+  alignas(16) float qws[DX_NV];
+  alignas(16) float qfs[DX_NV];   // qfrc_smooth
+  alignas(16) float qas[DX_NV];   // qacc_smooth
+  alignas(16) float srch[DX_NV];  // Newton search direction
   float com[DX_NTREE][4];
   float cdof[DX_NV][8];
-  float M[DX_NV][LDM];
-  float gxpos[DX_NG][4];
-  float gxmat[DX_NG][12];
+  alignas(16) float M[DX_NV][LDM];
+  alignas(16) float gxpos[DX_NG][4];   // gxpos+gxmat (dead during Newton) double as the
+  float gxmat[DX_NG][12];  // Hessian solve's LDS scratch
   float cprev[DX_NSLOT];  // previous-step masked slot distances (cost_c)
   int ncon, nefc, pad_[2];
   // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the
   //      contact / constraint arrays (collision .. Newton) ----
   union {
     struct {
-      float xpos[DX_NB][4];
+      alignas(16) float xpos[DX_NB][4];
       float xquat[DX_NB][4];
       float xmat[DX_NB][12];
       float xipos[DX_NB][4];
@@ -84,7 +89,7 @@ struct __align__(16) Smem {
       int con_pair[DX_MAXACT];
       int con_row[DX_MAXACT];
       float poly[2][8][4];  // box-box clipping polygon (double buffered)
-      float J[DX_MAXEFC][LDJ];
+      alignas(16) float J[DX_MAXEFC][LDJ];
       float efc_D[DX_MAXEFC];
       float efc_aref[DX_MAXEFC];
       float efc_jar[DX_MAXEFC];
@@ -188,6 +193,18 @@ __device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
 }
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+// 16-wide dot product of an LDS row (16-byte aligned) with an LDS vector
+__device__ __forceinline__ float dot16(const float* row, const float* vec) {
+  const float4* r = reinterpret_cast<const float4*>(row);
+  const float4* v = reinterpret_cast<const float4*>(vec);
+  float acc = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const float4 a = r[q], x = v[q];
+    acc = fmaf(a.x, x.x, acc); acc = fmaf(a.y, x.y, acc); acc = fmaf(a.z, x.z, acc); acc = fmaf(a.w, x.w, acc);
+  }
+  return acc;
+}
 
 // spatial algebra (MuJoCo layout, see oracle/mpcr_oracle.c)
 __device__ __forceinline__ void mul_inert_vec(float r[6], const float* i, const float* v) {
@@ -234,28 +251,45 @@ __device__ __forceinline__ void chol_rows(float (&a)[DX_NV], int lane) {
   }
 }
 
-// x = L^-T L^-1 b with the factor rows in registers (lane k holds row k) and
-// one rhs value per lane: both substitutions run on uniform values fetched
-// with v_readlane (no LDS transpose, no barrier).  Returns x[lane].
-__device__ __forceinline__ float chol_solve(const float (&l)[DX_NV], float b, int lane) {
-  float y[DX_NV];
+// x = L^-T L^-1 b with lane i holding row i of L in l[].  Forward pass: lane
+// k finalises y_k, one v_readlane broadcasts it, every lane updates its own
+// accumulator with its own register l[k].  For the backward pass each lane
+// needs its COLUMN of L: the rows are scattered transposed to the LDS scratch
+// Lt[DX_NV][LDL] once, each lane reads its column back with 4 ds_read_b128,
+// and the same broadcast chain runs backwards.  32 readlanes per solve.
+// Returns x[lane].  Must be called by all lanes (one barrier).
+__device__ __forceinline__ float chol_solve(const float (&l)[DX_NV], float b, int lane, float* Lt) {
+  if (lane < DX_NV) {
+#pragma unroll
+    for (int j = 0; j < DX_NV; j++) Lt[j * LDL + lane] = l[j];
+  }
+  float acc = b, y = 0.f;
 #pragma unroll
   for (int k = 0; k < DX_NV; k++) {
-    float acc = rdlane(b, k);
-#pragma unroll
-    for (int j = 0; j < k; j++) acc = fmaf(-rdlane(l[j], k), y[j], acc);
-    y[k] = acc / rdlane(l[k], k);
+    const float yk = rdlane(acc, k) / rdlane(l[k], k);
+    if (lane > k) acc = fmaf(-l[k], yk, acc);
+    if (lane == k) y = yk;
   }
-  float xl = 0.f;
+  sync();
+  float lt[DX_NV];
+  {
+    const float4* col = reinterpret_cast<const float4*>(Lt + (lane < DX_NV ? lane : 0) * LDL);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const float4 v = col[q];
+      lt[4 * q] = v.x; lt[4 * q + 1] = v.y; lt[4 * q + 2] = v.z; lt[4 * q + 3] = v.w;
+    }
+  }
+  float x = 0.f;
+  acc = y;
 #pragma unroll
   for (int k = DX_NV - 1; k >= 0; k--) {
-    float acc = y[k];
-#pragma unroll
-    for (int j = k + 1; j < DX_NV; j++) acc = fmaf(-rdlane(l[k], j), y[j], acc);
-    y[k] = acc / rdlane(l[k], k);
-    if (lane == k) xl = y[k];
+    const float xk = rdlane(acc, k) / rdlane(l[k], k);
+    if (lane < k) acc = fmaf(-lt[k], xk, acc);
+    if (lane == k) x = xk;
   }
-  return xl;
+  sync();
+  return x;
 }
 
 // ---------------------------------------------------------------------------
@@ -1215,7 +1249,8 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
 #pragma unroll
       for (int j = 0; j < DX_NV; j++) Lm[j] = lane < DX_NV ? s.M[lane][j] : 0.f;
       chol_rows(Lm, lane);
-      const float x = chol_solve(Lm, lane < DX_NV ? s.qfs[lane] : 0.f, lane);
+      // the dynamics region (xpos..fvec) is dead once M is assembled
+      const float x = chol_solve(Lm, lane < DX_NV ? s.qfs[lane] : 0.f, lane, &s.xpos[0][0]);
       if (lane < DX_NV) s.qas[lane] = lane < nv ? x : 0.f;
     }
 
@@ -1439,9 +1474,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
           sref = m->pair_solref[p];
           simp = m->pair_solimp[p];
         }
-        float vel = 0.f;
-#pragma unroll
-        for (int i = 0; i < DX_NV; i++) vel = fmaf(s.J[r][i], s.qvel[i], vel);
+        const float vel = dot16(s.J[r], s.qvel);
         const float imp = impedance(simp, pos, margin);
         const float R = fmaxf((1.f - imp) / imp * diag, kMinVal);
         float tc = sref[0];
@@ -1474,19 +1507,15 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         if (!(m->disableflags & 4)) {
           float maw = 0.f, mas = 0.f;
           if (lane < nv) {
-#pragma unroll
-            for (int j = 0; j < DX_NV; j++) {
-              maw = fmaf(s.M[lane][j], s.qws[j], maw);
-              mas = fmaf(s.M[lane][j], s.qas[j], mas);
-            }
+            maw = dot16(s.M[lane], s.qws);
+            mas = dot16(s.M[lane], s.qas);
           }
           const float gw = lane < nv ? (maw - s.qfs[lane]) * (s.qws[lane] - s.qas[lane]) : 0.f;
           const float gs = lane < nv ? (mas - s.qfs[lane]) * (s.qas[lane] - s.qas[lane]) : 0.f;
           float cw = 0.f, cs = 0.f;
           for (int r = lane; r < nefc; r += WAVE) {
-            float jw = -s.efc_aref[r], js = -s.efc_aref[r];
-#pragma unroll
-            for (int i = 0; i < DX_NV; i++) { jw = fmaf(s.J[r][i], s.qws[i], jw); js = fmaf(s.J[r][i], s.qas[i], js); }
+            const float jw = dot16(s.J[r], s.qws) - s.efc_aref[r];
+            const float js = dot16(s.J[r], s.qas) - s.efc_aref[r];
             const bool eq = (s.efc_src[r] >> 24) == 1;
             if (eq || jw < 0.f) cw += s.efc_D[r] * jw * jw;
             if (eq || js < 0.f) cs += s.efc_D[r] * js * js;
@@ -1501,16 +1530,10 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
         float prev_cost = 3.4e38f;
         for (int it = 0;; it++) {
           // Ma, jar, cost, grad at the current qacc
-          float ma = 0.f;
-          if (lane < nv) {
-#pragma unroll
-            for (int j = 0; j < DX_NV; j++) ma = fmaf(s.M[lane][j], s.qacc[j], ma);
-          }
+          const float ma = lane < nv ? dot16(s.M[lane], s.qacc) : 0.f;
           float cc = 0.f;
           for (int r = lane; r < nefc; r += WAVE) {
-            float jar = -s.efc_aref[r];
-#pragma unroll
-            for (int i = 0; i < DX_NV; i++) jar = fmaf(s.J[r][i], s.qacc[i], jar);
+            const float jar = dot16(s.J[r], s.qacc) - s.efc_aref[r];
             s.efc_jar[r] = jar;
             if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) cc += s.efc_D[r] * jar * jar;
           }
@@ -1537,28 +1560,24 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
               const float jar = s.efc_jar[r];
               if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) {
                 const float c = s.efc_D[r] * s.J[r][lane];
+                const float4* Jr = reinterpret_cast<const float4*>(s.J[r]);
 #pragma unroll
-                for (int j = 0; j < DX_NV; j++) h[j] = fmaf(c, s.J[r][j], h[j]);
+                for (int q = 0; q < 4; q++) {
+                  const float4 v = Jr[q];
+                  h[4 * q] = fmaf(c, v.x, h[4 * q]); h[4 * q + 1] = fmaf(c, v.y, h[4 * q + 1]);
+                  h[4 * q + 2] = fmaf(c, v.z, h[4 * q + 2]); h[4 * q + 3] = fmaf(c, v.w, h[4 * q + 3]);
+                }
               }
             }
           }
           chol_rows(h, lane);
-          const float mg = chol_solve(h, lane < nv ? grad : 0.f, lane);
+          const float mg = chol_solve(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
           const float search = lane < nv ? -mg : 0.f;
           if (lane < DX_NV) s.srch[lane] = search;
           sync();
           // Mv, jv, quadratic coefficients
-          float mvv = 0.f;
-          if (lane < nv) {
-#pragma unroll
-            for (int j = 0; j < DX_NV; j++) mvv = fmaf(s.M[lane][j], s.srch[j], mvv);
-          }
-          for (int r = lane; r < nefc; r += WAVE) {
-            float jv = 0.f;
-#pragma unroll
-            for (int i = 0; i < DX_NV; i++) jv = fmaf(s.J[r][i], s.srch[i], jv);
-            s.efc_jv[r] = jv;
-          }
+          const float mvv = lane < nv ? dot16(s.M[lane], s.srch) : 0.f;
+          for (int r = lane; r < nefc; r += WAVE) s.efc_jv[r] = dot16(s.J[r], s.srch);
           const float sn = sqrtf(wsum(search * search));
           const float gtol = m->tolerance * m->ls_tolerance * sn * m->meaninertia * (float)(nv > 1 ? nv : 1);
           float qg[3];
