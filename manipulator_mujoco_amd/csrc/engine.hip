@@ -458,7 +458,7 @@ static int launch_rollout(mpcr_engine* e, const float* in, int layout, int n, co
   float qn = std::sqrt(qtgt[0] * qtgt[0] + qtgt[1] * qtgt[1] + qtgt[2] * qtgt[2] + qtgt[3] * qtgt[3]);
   for (int k = 0; k < 4; k++) a.qtgt[k] = qtgt[k] / qn;
   if (key && reset_key) hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, key, ~0ull);
-  hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, st, a);
+  hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
   HIPCHK(hipGetLastError());
   return MPCR_OK;
 }
@@ -547,7 +547,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   for (int k = 0; k < 3; k++) { a.w[k] = w[k]; a.ptgt[k] = ptgt[k]; }
   float qn = std::sqrt(qtgt[0] * qtgt[0] + qtgt[1] * qtgt[1] + qtgt[2] * qtgt[2] + qtgt[3] * qtgt[3]);
   for (int k = 0; k < 4; k++) a.qtgt[k] = qtgt[k] / qn;
-  hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, nullptr, a);
+  hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(phases16, d_prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(d_prof);

@@ -561,7 +561,7 @@ __device__ __forceinline__ float impedance(const float* si, float pos, float mar
 // polygon edge and ballot compaction, the >4 selection is done on uniform
 // values.  Same definitions and orders as the oracle's col_box_box.
 // Appends up to 4 contacts to the active list.  Must be called by all lanes.
-__device__ void box_box_wave(const DevModel* __restrict__ m, Smem& s, int p, int lane) {
+__device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, Smem& s, int p, int lane) {
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   const float margin = m->pair_margin[p];
   float x1[3], x2[3], axA[3][3], axB[3][3], t[3], ha[3], hb[3];
@@ -857,12 +857,25 @@ __device__ __forceinline__ void ls_eval3(const Smem& s, int lane, const float qg
   p2 = ls_make(a2, q[6], q[7], q[8]);
 }
 
+// Re-derive the model pointer from the kernel argument through an opaque
+// zero offset.  The compiler then cannot hoist loop-invariant model loads out
+// of the horizon loop (which kept them all live: 244 VGPRs), while the base
+// stays a kernel-argument pointer so its loads remain global (uniform ones
+// scalar) instead of FLAT.
+#define LAUNDER_MODEL()                  \
+  do {                                   \
+    int z_ = 0;                          \
+    asm volatile("" : "+s"(z_));         \
+    m = m0 + z_;                         \
+  } while (0)
+
 // ---------------------------------------------------------------------------
 // the kernel
 
-__global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
+__global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args, const DevModel* __restrict__ mptr) {
   __shared__ Smem s;
-  const DevModel* m = args.m;
+  const DevModel* __restrict__ const m0 = mptr;
+  const DevModel* __restrict__ m = m0;
   const int lane = threadIdx.x;
   const int b = blockIdx.x;
   if (b >= args.n) return;
@@ -893,7 +906,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     // every loop-invariant model load out of the horizon loop and keeps them
     // all live across the whole step (244 VGPRs + SGPR spills).  The loads
     // stay in their phases and hit L1/L2.
-    asm volatile("" : "+s"(m));
+    LAUNDER_MODEL();
     // ---- qvel[:nctrl] = thetadot_t (basis evaluated on the fly) -------------
     if (lane < nc) {
       float v;
@@ -910,7 +923,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     sync();
 
     STAMP(0);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- kinematics: local pose per body, then pointer jumping ----------------
     {
       float q[4] = {1.f, 0.f, 0.f, 0.f}, p[3] = {0.f, 0.f, 0.f};
@@ -984,7 +997,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     sync();
 
     STAMP(1);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- geom poses, tree COMs ------------------------------------------------
     if (lane < m->ngeom) {
       const int gb = m->geom_body[lane];
@@ -1051,7 +1064,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
 
     STAMP(2);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- cinert, cdof ---------------------------------------------------------
     if (lane < nb) {
       const int tr = m->body_tree[lane];
@@ -1125,7 +1138,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     sync();
 
     STAMP(3);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- CRB, velocity, RNE + gravcomp (subtree sums by bitmask) -----------
     for (int idx = lane; idx < nb * 10; idx += WAVE) {
       const int bb = idx / 10, k = idx - bb * 10;
@@ -1204,7 +1217,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
     sync();
     STAMP(4);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // mass matrix entries (chain-masked) + bias forces
     for (int idx = lane; idx < DX_NV * DX_NV; idx += WAVE) {
       const int i = idx >> 4, j = idx & 15;
@@ -1242,7 +1255,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     sync();
 
     STAMP(5);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
     {
       float Lm[DX_NV];
@@ -1255,7 +1268,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
 
     STAMP(6);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
     //      slots; active contacts compacted into the list; box-box pairs
     //      that pass the bounding-sphere cull are solved wave-cooperatively
@@ -1342,7 +1355,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
 
     STAMP(7);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- constraint rows: equality, limits, contacts ------------------------
     {
       const int ncon = s.ncon;
@@ -1497,7 +1510,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     nefc_sum += s.nefc;
 
     STAMP(8);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- Newton solver (primal), MJX-style line search ------------------------
     {
       const int nefc = s.nefc;
@@ -1620,7 +1633,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args) {
     }
 
     STAMP(9);
-    asm volatile("" : "+s"(m));  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
     // ---- Euler: qvel += dt qacc; integrate qpos; warm start -----------------
     {
       const float dt = m->timestep;
