@@ -16,6 +16,10 @@ DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("rollout.hip", "mpcr_devic
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mpcr.h", "mpcr_model.h")]
 OUT = os.path.join(HERE, "libmpcr.so")
 ARCH = os.environ.get("MPCR_OFFLOAD_ARCH", "gfx950")
+# fp32 '/' and sqrtf map to the 1-ulp hardware v_rcp/v_sqrt (not the ~10-op
+# IEEE sequences); every other fp semantic (NaN/Inf, no reassociation) stays
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-pass-failed",
+         "-fno-hip-fp32-correctly-rounded-divide-sqrt"]
 
 
 def hipcc():
@@ -30,8 +34,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         mt = os.path.getmtime(OUT)
         if all(os.path.getmtime(d) <= mt for d in DEPS):
             return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-pass-failed", "-o", OUT + ".tmp"] + SRC
+    cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + ["-o", OUT + ".tmp"] + SRC
     if verbose:
         cmd.append("-Rpass-analysis=kernel-resource-usage")
         print(" ".join(cmd))

@@ -94,6 +94,8 @@ struct __align__(16) Smem {
       float efc_aref[DX_MAXEFC];
       float efc_jar[DX_MAXEFC];
       float efc_jv[DX_MAXEFC];
+      float efc_f[DX_MAXEFC];   // -D * jar on active rows, else 0
+      float efc_Da[DX_MAXEFC];  // D on active rows, else 0
       int efc_src[DX_MAXEFC];  // (kind << 24) | (index << 4) | side
     };
   };
@@ -550,6 +552,7 @@ __device__ __forceinline__ float impedance(const float* si, float pos, float mar
   if (x <= 0.f) return dmin;
   float y;
   if (power == 1.f) y = x;
+  else if (power == 2.f) y = x <= mid ? x * x / mid : 1.f - (1.f - x) * (1.f - x) / (1.f - mid);  // default solimp
   else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
   else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
   return dmin + y * (dmax - dmin);
@@ -1542,45 +1545,54 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args, const D
         const float scale = 1.f / (m->meaninertia * (float)(nv > 1 ? nv : 1));
         float prev_cost = 3.4e38f;
         for (int it = 0;; it++) {
-          // Ma, jar, cost, grad at the current qacc
+          // the iteration cap ends the solve before anything below matters
+          // (cost / gradient only feed the stop test)
+          if (it >= m->iterations) break;
+          // Ma, jar, cost at the current qacc; per-row force and active D
           const float ma = lane < nv ? dot16(s.M[lane], s.qacc) : 0.f;
           float cc = 0.f;
           for (int r = lane; r < nefc; r += WAVE) {
             const float jar = dot16(s.J[r], s.qacc) - s.efc_aref[r];
+            const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
+            const float D = s.efc_D[r];
             s.efc_jar[r] = jar;
-            if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) cc += s.efc_D[r] * jar * jar;
+            s.efc_f[r] = act ? -D * jar : 0.f;
+            s.efc_Da[r] = act ? D : 0.f;
+            cc += act ? D * jar * jar : 0.f;
           }
           const float gauss = wsum(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
           const float cost = 0.5f * gauss + 0.5f * wsum(cc);
           sync();
-          float grad = 0.f;
-          if (lane < nv) {
-            float qc = 0.f;
-            for (int r = 0; r < nefc; r++) {
-              const float jar = s.efc_jar[r];
-              if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) qc = fmaf(s.J[r][lane], -s.efc_D[r] * jar, qc);
-            }
-            grad = ma - s.qfs[lane] - qc;
-          }
+          // grad = Ma - qfrc_smooth - J^T f: lane (dof i, row quarter q)
+          const int gi = lane & 15, gq = lane >> 4;
+          float qc = 0.f;
+          for (int r = gq; r < nefc; r += 4) qc = fmaf(s.J[r][gi], s.efc_f[r], qc);
+          qc += __shfl_xor(qc, 16);
+          qc += __shfl_xor(qc, 32);
+          const float grad = lane < nv ? ma - s.qfs[lane] - qc : 0.f;
           const float gn = sqrtf(wsum(grad * grad));
-          if (it >= m->iterations || scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance) break;
-          // Hessian rows: H = M + J^T D_active J
-          float h[DX_NV];
-#pragma unroll
-          for (int j = 0; j < DX_NV; j++) h[j] = lane < DX_NV ? s.M[lane][j] : 0.f;
-          if (lane < nv) {
+          if (scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance) break;
+          // Hessian H = M + J^T D_active J: lane (row i, column quad q) builds
+          // H[i][4q..4q+3]; rows are gathered to lanes 0..15 through LDS
+          float* Hs = &s.gxpos[0][0];  // geom poses are dead during Newton
+          {
+            const float4 m4 = reinterpret_cast<const float4*>(s.M[gi])[gq];
+            float h0 = m4.x, h1 = m4.y, h2 = m4.z, h3 = m4.w;
             for (int r = 0; r < nefc; r++) {
-              const float jar = s.efc_jar[r];
-              if (((s.efc_src[r] >> 24) == 1) || jar < 0.f) {
-                const float c = s.efc_D[r] * s.J[r][lane];
-                const float4* Jr = reinterpret_cast<const float4*>(s.J[r]);
+              const float c = s.efc_Da[r] * s.J[r][gi];
+              const float4 v = reinterpret_cast<const float4*>(s.J[r])[gq];
+              h0 = fmaf(c, v.x, h0); h1 = fmaf(c, v.y, h1); h2 = fmaf(c, v.z, h2); h3 = fmaf(c, v.w, h3);
+            }
+            reinterpret_cast<float4*>(Hs + gi * LDL)[gq] = make_float4(h0, h1, h2, h3);
+          }
+          sync();
+          float h[DX_NV];
+          {
+            const float4* row = reinterpret_cast<const float4*>(Hs + (lane & 15) * LDL);
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                  const float4 v = Jr[q];
-                  h[4 * q] = fmaf(c, v.x, h[4 * q]); h[4 * q + 1] = fmaf(c, v.y, h[4 * q + 1]);
-                  h[4 * q + 2] = fmaf(c, v.z, h[4 * q + 2]); h[4 * q + 3] = fmaf(c, v.w, h[4 * q + 3]);
-                }
-              }
+            for (int q = 0; q < 4; q++) {
+              const float4 v = row[q];
+              h[4 * q] = v.x; h[4 * q + 1] = v.y; h[4 * q + 2] = v.z; h[4 * q + 3] = v.w;
             }
           }
           chol_rows(h, lane);

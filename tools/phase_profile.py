@@ -17,8 +17,8 @@ PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rn
 
 def main():
     so = os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr_prof.so")
-    subprocess.run([build.hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DMPCR_PROFILE",
-                    "-Wno-pass-failed", "-o", so] + build.SRC, check=True)
+    subprocess.run([build.hipcc(), "--offload-arch=gfx950"] + build.FLAGS + ["-DMPCR_PROFILE", "-o", so] + build.SRC,
+                   check=True)
     _lib.LIB_PATH = so
     lib = _lib.load()
     lib.mpcr_rollout_profile.restype = ctypes.c_int
