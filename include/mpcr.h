@@ -90,8 +90,9 @@ void mpcr_engine_free(mpcr_engine* e);
    best_key             device uint64: atomic-min of
                         (ordered(cost) << 32 | (index_base + i)), NaN first (nullable)
    status [n]           per-candidate flags (bit0: constraint rows truncated,
-                        bit1: non-finite state) | (constraint rows summed
-                        over the horizon << 8)                   (nullable)
+                        bit1: non-finite state) | (max constraint rows in
+                        one step, capped at 63, << 2) | (constraint rows
+                        summed over the horizon << 8)            (nullable)
    stream               hipStream_t or NULL (default stream)                  */
 int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
                       const float* w, const float* ptgt, const float* qtgt, float* cost4, float* theta,

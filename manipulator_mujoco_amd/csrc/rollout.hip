@@ -901,7 +901,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args, const D
   sync();
 
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
-  int status = 0, nefc_sum = 0;
+  int status = 0, nefc_sum = 0, nefc_max = 0;
   PROF_DECL
 
   for (int t = 0; t < H; t++) {
@@ -1511,6 +1511,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args, const D
       sync();
     }
     nefc_sum += s.nefc;
+    nefc_max = max(nefc_max, s.nefc);
 
     STAMP(8);
     LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
@@ -1695,7 +1696,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args, const D
     args.cost4[4 * (size_t)b + 1] = cost_g;
     args.cost4[4 * (size_t)b + 2] = cost_r;
     args.cost4[4 * (size_t)b + 3] = cost_c;
-    if (args.status) args.status[b] = status | (nefc_sum << 8);
+    if (args.status) args.status[b] = status | (min(nefc_max, 63) << 2) | (nefc_sum << 8);
     if (args.best_key) {
       const uint32_t u = __float_as_uint(cost);
       uint32_t key = isnan(cost) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));

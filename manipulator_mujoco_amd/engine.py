@@ -33,9 +33,12 @@ class Model:
         self.handle = h
 
     def __del__(self):
-        if getattr(self, "handle", None):
-            _lib.load().mpcr_model_free(self.handle)
-            self.handle = None
+        try:
+            if getattr(self, "handle", None):
+                _lib.load().mpcr_model_free(self.handle)
+        except Exception:  # interpreter shutdown
+            pass
+        self.handle = None
 
 
 class Engine:
@@ -57,9 +60,12 @@ class Engine:
         self.handle = h
 
     def __del__(self):
-        if getattr(self, "handle", None):
-            _lib.load().mpcr_engine_free(self.handle)
-            self.handle = None
+        try:
+            if getattr(self, "handle", None):
+                _lib.load().mpcr_engine_free(self.handle)
+        except Exception:  # interpreter shutdown
+            pass
+        self.handle = None
 
     @staticmethod
     def _vec(x, n, dtype):
