@@ -21,6 +21,15 @@
  *   best_key / mpcr_argmin / mpcr_best_key_decode
  *                         idx_min = argmin(cost_batch[-1])    mjx_planner.py:395
  *   mpcr_topk             compute_ellite_samples argsort     mjx_planner.py:305-310
+ *   mpcr_cem_create       cem_planner.__init__ basis + get_Q_inv mjx_planner.py:40-46,
+ *                                                             140-172
+ *   mpcr_cem_factor       the Cholesky inside jax.random.multivariate_normal
+ *                                                             mjx_planner.py:312-316
+ *   mpcr_cem_sample_project / mpcr_project
+ *                         compute_xi_samples + compute_projection_filter
+ *                         (+ compute_projection)              mjx_planner.py:312-316,
+ *                                                             180-249
+ *   mpcr_cem_update       compute_mean_cov + comp_prod       mjx_planner.py:318-335
  */
 #ifndef MPCR_H_
 #define MPCR_H_
@@ -61,6 +70,7 @@ enum {
 
 typedef struct mpcr_model mpcr_model;   /* opaque host model handle */
 typedef struct mpcr_engine mpcr_engine; /* opaque device engine      */
+typedef struct mpcr_cem mpcr_cem;       /* opaque CEM context (projection tables, Cholesky factor) */
 
 const char* mpcr_last_error(void);
 int mpcr_abi_version(void);
@@ -107,10 +117,50 @@ int mpcr_argmin(mpcr_engine* e, const float* cost, int stride, int n, int index_
 /* decode a packed best key */
 void mpcr_best_key_decode(uint64_t key, int* idx, float* cost);
 
-/* indices of the k smallest costs, ascending, NaN last, ties by index
-   (jnp.argsort is stable): compute_ellite_samples. */
+/* indices of the k smallest of cost[i*stride], ascending, NaN last, ties by
+   index, -0 == +0 (jnp.argsort is stable): compute_ellite_samples.
+   k <= min(n, 4096).  Host pointers: n <= max_n and stride <= 4. */
 int mpcr_topk(mpcr_engine* e, const float* cost, int stride, int n, int k, int* idx_out, int flags,
               void* stream);
+
+/* ---- the CEM distribution step (device pointers only: MPCR_F_DEVICE_PTRS) ----
+   num_dof <= 8 joints, nbasis = 11 (order-10 Bernstein), P/Pdot/Pddot
+   horizon x nbasis row-major fp64 (bernstein_coeff_ordern_new).  qinv
+   (nullable): the (nv+5nd)^2 fp64 KKT inverse; NULL computes get_Q_inv's
+   matrix (fp32 Gram blocks, fp64 inverse, rho_ineq = 1). */
+int mpcr_cem_create(int device, int num_dof, int horizon, int nbasis, const double* P, const double* Pdot,
+                    const double* Pddot, const double* qinv, int max_n, mpcr_cem** out);
+void mpcr_cem_free(mpcr_cem* c);
+
+/* L = chol(cov + reg I) (nv x nv fp32, reg = 0.003 in the reference) into the
+   context, for the next sampling call.  Non-PD input yields NaN samples. */
+int mpcr_cem_factor(mpcr_cem* c, const float* cov, float reg, int flags, void* stream);
+
+/* Fused sampling + projection for n candidates.
+   mean != NULL: xi_samples = mean + z L^T with z ~ N(0, I) from Philox4x32-10
+     keyed by seed, counter = (call counter), element (candidate, joint, block)
+     -- independent of the launch shape; written to xi_samples if non-NULL.
+   mean == NULL: the samples are read from xi_in (n x nv).
+   Then maxiter ADMM iterations onto |Pdot xi| <= bounds[0], |Pddot xi| <=
+   bounds[1], |P xi| <= bounds[2] with the boundary equalities b_eq
+   (n x 5nd, per joint (theta0, thetadot0, thetaddot0, 0, 0); beq_stride 0 =
+   one row shared by all candidates) and multiplier step rho; maxiter = 0
+   returns the samples.  xi_out n x nv. */
+int mpcr_cem_sample_project(mpcr_cem* c, int n, const float* mean, uint64_t seed, uint64_t counter,
+                            const float* xi_in, float* xi_samples, const float* b_eq, int beq_stride, int maxiter,
+                            const float* bounds, float rho, float* xi_out, int flags, void* stream);
+/* projection only (compute_projection_filter) */
+int mpcr_project(mpcr_cem* c, const float* xi, const float* b_eq, int beq_stride, int n, int maxiter,
+                 const float* bounds, float rho, float* xi_out, int flags, void* stream);
+
+/* Elite moments, in place: w = exp(-(c - min c)/lamda) over the k elites
+   xi[elite_idx[i]] (n x nv rows), cost[elite_idx[i]*stride];
+   mean <- (1-alpha_mean) mean + alpha_mean sum(w xi)/sum(w);
+   cov  <- (1-alpha_cov) cov + alpha_cov sum(w d d^T)/sum(w) + reg I, d = xi - mean_new.
+   k <= 4096. */
+int mpcr_cem_update(mpcr_cem* c, const float* xi, int n, const float* cost, int stride, const int* elite_idx, int k,
+                    float lamda, float alpha_mean, float alpha_cov, float reg, float* mean, float* cov, int flags,
+                    void* stream);
 
 #ifdef __cplusplus
 }

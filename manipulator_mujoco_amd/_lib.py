@@ -24,7 +24,8 @@ MPCR_F_SYNC = 4
 EXPORTS = (
     "mpcr_last_error", "mpcr_abi_version", "mpcr_device_arch", "mpcr_model_from_blob", "mpcr_model_load",
     "mpcr_model_set_timestep", "mpcr_model_info", "mpcr_model_free", "mpcr_engine_create", "mpcr_engine_free",
-    "mpcr_rollout_cost", "mpcr_argmin", "mpcr_best_key_decode", "mpcr_topk",
+    "mpcr_rollout_cost", "mpcr_argmin", "mpcr_best_key_decode", "mpcr_topk", "mpcr_cem_create", "mpcr_cem_free",
+    "mpcr_cem_factor", "mpcr_cem_sample_project", "mpcr_project", "mpcr_cem_update",
 )
 
 _lib = None
@@ -61,8 +62,17 @@ def load():
     lib.mpcr_best_key_decode.argtypes = [ctypes.c_uint64, P(i), P(f)]
     lib.mpcr_best_key_decode.restype = None
     lib.mpcr_topk.argtypes = [vp, vp, i, i, i, vp, i, vp]
+    u64 = ctypes.c_uint64
+    lib.mpcr_cem_create.argtypes = [i, i, i, i, vp, vp, vp, vp, i, P(vp)]
+    lib.mpcr_cem_free.argtypes = [vp]
+    lib.mpcr_cem_free.restype = None
+    lib.mpcr_cem_factor.argtypes = [vp, vp, f, i, vp]
+    lib.mpcr_cem_sample_project.argtypes = [vp, i, vp, u64, u64, vp, vp, vp, i, i, P(f), f, vp, i, vp]
+    lib.mpcr_project.argtypes = [vp, vp, vp, i, i, i, P(f), f, vp, i, vp]
+    lib.mpcr_cem_update.argtypes = [vp, vp, i, vp, i, vp, i, f, f, f, f, vp, vp, i, vp]
     for name in EXPORTS + ("mpcr_rollout_trace",):
-        if name not in ("mpcr_last_error", "mpcr_model_free", "mpcr_engine_free", "mpcr_best_key_decode"):
+        if name not in ("mpcr_last_error", "mpcr_model_free", "mpcr_engine_free", "mpcr_best_key_decode",
+                        "mpcr_cem_free"):
             getattr(lib, name).restype = i
     _lib = lib
     return lib

@@ -12,7 +12,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = [os.path.join(HERE, "csrc", "engine.hip")]
-DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("rollout.hip", "mpcr_device.h")] + [
+DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("rollout.hip", "cem.hip", "mpcr_device.h")] + [
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mpcr.h", "mpcr_model.h")]
 OUT = os.path.join(HERE, "libmpcr.so")
 ARCH = os.environ.get("MPCR_OFFLOAD_ARCH", "gfx950")

@@ -16,8 +16,9 @@ namespace mpcr {
 struct RolloutArgs;
 }
 
-// kernels (rollout.hip)
+// kernels (rollout.hip: the fused rollout; cem.hip: the CEM distribution step)
 #include "rollout.hip"
+#include "cem.hip"
 
 using namespace mpcr;
 
@@ -602,6 +603,226 @@ extern "C" int mpcr_argmin(mpcr_engine* e, const float* cost, int stride, int n,
 
 extern "C" int mpcr_topk(mpcr_engine* e, const float* cost, int stride, int n, int k, int* idx_out, int flags,
                          void* stream) {
-  (void)e; (void)cost; (void)stride; (void)n; (void)k; (void)idx_out; (void)flags; (void)stream;
-  return fail(MPCR_EINVAL, "mpcr_topk: not implemented in this build (host argsort is used; SURVEY 8f-2)");
+  if (!e || !cost || !idx_out || stride <= 0 || n < 0) return fail(MPCR_EINVAL, "bad topk arguments");
+  if (k < 0 || k > n || k > TOPK_MAX) return fail(MPCR_EINVAL, "k=%d outside [0, min(n=%d, %d)]", k, n, TOPK_MAX);
+  if (k == 0) return MPCR_OK;
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (flags & MPCR_F_DEVICE_PTRS) {
+    hipLaunchKernelGGL(topk_kernel, dim3(1), dim3(1024), 0, st, cost, stride, n, k, idx_out);
+    HIPCHK(hipGetLastError());
+    if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
+    return MPCR_OK;
+  }
+  if (n > e->max_n || stride > 4) return fail(MPCR_EINVAL, "host topk limited to max_n x 4");
+  HIPCHK(hipMemcpyAsync(e->d_cost, cost, sizeof(float) * (size_t)n * stride, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(topk_kernel, dim3(1), dim3(1024), 0, st, e->d_cost, stride, n, k, e->d_idx);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(idx_out, e->d_idx, sizeof(int) * k, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return MPCR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// CEM context (cem.hip kernels)
+
+struct mpcr_cem {
+  int device = 0, nd = 0, H = 0, max_n = 0;
+  float* d_X = nullptr;    // 3 x H x 12: Pdot, Pddot, P
+  float* d_QT = nullptr;   // LD x LD
+  float* d_QbT = nullptr;  // 5nd x LD
+  float* d_LT = nullptr;   // LD x LD Cholesky factor (transposed, padded)
+  bool factored = false;
+};
+
+// get_Q_inv (SBP/mjx_planner.py:166-172 as restated by oracle/cem_np.q_inv):
+// fp32 Gram blocks of kron(I, [X; -X]) promoted to fp64, fp64 KKT inverse.
+static bool kkt_inverse(int nd, int H, const float* P, const float* Pd, const float* Pdd, std::vector<double>& Kinv) {
+  const int nb = PJ_NB, nv = nd * nb, ne = 5 * nd, NK = nv + ne;
+  std::vector<double> K((size_t)NK * NK, 0.0);
+  const float* mats[3] = {Pd, Pdd, P};
+  for (int a = 0; a < nb; a++)
+    for (int b = 0; b < nb; b++) {
+      double g = 0.0;
+      for (int k = 0; k < 3; k++) {
+        float s = 0.f;  // fp32 Gram entry over the 2H rows of [X; -X]
+        for (int t = 0; t < H; t++) s += mats[k][t * nb + a] * mats[k][t * nb + b];
+        for (int t = 0; t < H; t++) s += (-mats[k][t * nb + a]) * (-mats[k][t * nb + b]);
+        g += (double)s;
+      }
+      for (int j = 0; j < nd; j++) K[(size_t)(j * nb + a) * NK + j * nb + b] = g + (a == b ? 1.0 : 0.0);
+    }
+  for (int j = 0; j < nd; j++)
+    for (int c = 0; c < nb; c++) {
+      const double rows[5] = {P[c], Pd[c], Pdd[c], Pd[(H - 1) * nb + c], Pdd[(H - 1) * nb + c]};
+      for (int m = 0; m < 5; m++) {
+        K[(size_t)(nv + j * 5 + m) * NK + j * nb + c] = rows[m];
+        K[(size_t)(j * nb + c) * NK + nv + j * 5 + m] = rows[m];
+      }
+    }
+  // Gauss-Jordan with partial pivoting
+  Kinv.assign((size_t)NK * NK, 0.0);
+  for (int i = 0; i < NK; i++) Kinv[(size_t)i * NK + i] = 1.0;
+  for (int c = 0; c < NK; c++) {
+    int piv = c;
+    for (int r = c + 1; r < NK; r++)
+      if (std::fabs(K[(size_t)r * NK + c]) > std::fabs(K[(size_t)piv * NK + c])) piv = r;
+    if (K[(size_t)piv * NK + c] == 0.0) return false;
+    if (piv != c)
+      for (int q = 0; q < NK; q++) {
+        std::swap(K[(size_t)c * NK + q], K[(size_t)piv * NK + q]);
+        std::swap(Kinv[(size_t)c * NK + q], Kinv[(size_t)piv * NK + q]);
+      }
+    const double inv = 1.0 / K[(size_t)c * NK + c];
+    for (int q = 0; q < NK; q++) { K[(size_t)c * NK + q] *= inv; Kinv[(size_t)c * NK + q] *= inv; }
+    for (int r = 0; r < NK; r++) {
+      if (r == c) continue;
+      const double f = K[(size_t)r * NK + c];
+      if (f == 0.0) continue;
+      for (int q = 0; q < NK; q++) {
+        K[(size_t)r * NK + q] -= f * K[(size_t)c * NK + q];
+        Kinv[(size_t)r * NK + q] -= f * Kinv[(size_t)c * NK + q];
+      }
+    }
+  }
+  return true;
+}
+
+extern "C" int mpcr_cem_create(int device, int num_dof, int horizon, int nbasis, const double* P, const double* Pdot,
+                               const double* Pddot, const double* qinv, int max_n, mpcr_cem** out) {
+  if (!out || !P || !Pdot || !Pddot || max_n <= 0 || horizon < 2) return fail(MPCR_EINVAL, "bad cem arguments");
+  if (nbasis != PJ_NB) return fail(MPCR_EINVAL, "nbasis=%d: the CEM kernels are built for order-10 (11)", nbasis);
+  if (num_dof < 1 || num_dof > PJ_MAXD) return fail(MPCR_EINVAL, "num_dof=%d outside [1, %d]", num_dof, PJ_MAXD);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MPCR_ENODEV, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(MPCR_ENODEV, "device %d out of range (%d)", device, ndev);
+  HIPCHK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(MPCR_ENODEV, "device %d is %s; libmpcr is built for gfx950 only", device, prop.gcnArchName);
+  const int nd = num_dof, H = horizon, nb = PJ_NB, nv = nd * nb, ne = 5 * nd, NK = nv + ne, LD = nd * PJ_BLK;
+  std::vector<float> Pf((size_t)H * nb), Pdf((size_t)H * nb), Pddf((size_t)H * nb);
+  for (int i = 0; i < H * nb; i++) { Pf[i] = (float)P[i]; Pdf[i] = (float)Pdot[i]; Pddf[i] = (float)Pddot[i]; }
+  std::vector<double> Kinv;
+  if (qinv) {
+    Kinv.assign(qinv, qinv + (size_t)NK * NK);
+  } else if (!kkt_inverse(nd, H, Pf.data(), Pdf.data(), Pddf.data(), Kinv)) {
+    return fail(MPCR_EINVAL, "singular KKT matrix");
+  }
+  std::vector<float> X((size_t)3 * H * PJ_BLK, 0.f), QT((size_t)LD * LD, 0.f), QbT((size_t)ne * LD, 0.f);
+  const float* mats[3] = {Pdf.data(), Pddf.data(), Pf.data()};
+  for (int k = 0; k < 3; k++)
+    for (int t = 0; t < H; t++)
+      for (int c = 0; c < nb; c++) X[((size_t)k * H + t) * PJ_BLK + c] = mats[k][t * nb + c];
+  auto pad = [&](int i) { return (i / nb) * PJ_BLK + i % nb; };
+  for (int r = 0; r < nv; r++) {
+    for (int c = 0; c < nv; c++) QT[(size_t)pad(c) * LD + pad(r)] = (float)Kinv[(size_t)r * NK + c];
+    for (int m = 0; m < ne; m++) QbT[(size_t)m * LD + pad(r)] = (float)Kinv[(size_t)r * NK + nv + m];
+  }
+  auto* c = new mpcr_cem;
+  c->device = device;
+  c->nd = nd;
+  c->H = H;
+  c->max_n = max_n;
+  if (hipMalloc(&c->d_X, sizeof(float) * X.size()) != hipSuccess ||
+      hipMalloc(&c->d_QT, sizeof(float) * QT.size()) != hipSuccess ||
+      hipMalloc(&c->d_QbT, sizeof(float) * QbT.size()) != hipSuccess ||
+      hipMalloc(&c->d_LT, sizeof(float) * (size_t)LD * LD) != hipSuccess) {
+    mpcr_cem_free(c);
+    return fail(MPCR_ENOMEM, "device allocation failed");
+  }
+  if (hipMemcpy(c->d_X, X.data(), sizeof(float) * X.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_QT, QT.data(), sizeof(float) * QT.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_QbT, QbT.data(), sizeof(float) * QbT.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->d_LT, 0, sizeof(float) * (size_t)LD * LD) != hipSuccess) {
+    mpcr_cem_free(c);
+    return fail(MPCR_EHIP, "table upload failed");
+  }
+  *out = c;
+  return MPCR_OK;
+}
+
+extern "C" void mpcr_cem_free(mpcr_cem* c) {
+  if (!c) return;
+  (void)hipFree(c->d_X);
+  (void)hipFree(c->d_QT);
+  (void)hipFree(c->d_QbT);
+  (void)hipFree(c->d_LT);
+  delete c;
+}
+
+extern "C" int mpcr_cem_factor(mpcr_cem* c, const float* cov, float reg, int flags, void* stream) {
+  if (!c || !cov) return fail(MPCR_EINVAL, "null argument");
+  if (!(flags & MPCR_F_DEVICE_PTRS)) return fail(MPCR_EINVAL, "mpcr_cem_factor takes device pointers");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(cholesky_kernel, dim3(1), dim3(256), 0, st, cov, c->nd, reg, c->d_LT);
+  HIPCHK(hipGetLastError());
+  c->factored = true;
+  if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_cem_sample_project(mpcr_cem* c, int n, const float* mean, uint64_t seed, uint64_t counter,
+                                       const float* xi_in, float* xi_samples, const float* b_eq, int beq_stride,
+                                       int maxiter, const float* bounds, float rho, float* xi_out, int flags,
+                                       void* stream) {
+  if (!c || !xi_out) return fail(MPCR_EINVAL, "null argument");
+  if (!(flags & MPCR_F_DEVICE_PTRS)) return fail(MPCR_EINVAL, "mpcr_cem_sample_project takes device pointers");
+  if (n < 0 || n > c->max_n) return fail(MPCR_EINVAL, "n=%d outside [0, max_n=%d]", n, c->max_n);
+  if (!mean && !xi_in) return fail(MPCR_EINVAL, "need mean (sampling) or xi_in");
+  if (mean && !c->factored) return fail(MPCR_EINVAL, "sampling before mpcr_cem_factor");
+  if (maxiter < 0 || (maxiter > 0 && (!b_eq || !bounds || beq_stride < 0)))
+    return fail(MPCR_EINVAL, "projection needs b_eq, bounds and maxiter >= 0");
+  if (n == 0) return MPCR_OK;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  ProjArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.xi_in = xi_in;
+  a.mean = mean;
+  a.L = c->d_LT;
+  a.xi_samples = xi_samples;
+  a.beq = b_eq;
+  a.xi_out = xi_out;
+  a.X = c->d_X;
+  a.QT = c->d_QT;
+  a.QbT = c->d_QbT;
+  a.seed = seed;
+  a.counter = counter;
+  a.n = n;
+  a.nd = c->nd;
+  a.H = c->H;
+  a.maxiter = maxiter;
+  a.beq_stride = beq_stride;
+  for (int k = 0; k < 3; k++) a.bound[k] = bounds ? bounds[k] : 0.f;
+  a.rho = rho;
+  const size_t lds = sizeof(float) * 64 * (c->nd * PJ_BLK + 4);
+  hipLaunchKernelGGL(sample_project_kernel, dim3((n + 63) / 64), dim3(64 * c->nd), lds, st, a);
+  HIPCHK(hipGetLastError());
+  if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_project(mpcr_cem* c, const float* xi, const float* b_eq, int beq_stride, int n, int maxiter,
+                            const float* bounds, float rho, float* xi_out, int flags, void* stream) {
+  if (!xi) return fail(MPCR_EINVAL, "null xi");
+  return mpcr_cem_sample_project(c, n, nullptr, 0, 0, xi, nullptr, b_eq, beq_stride, maxiter, bounds, rho, xi_out,
+                                 flags, stream);
+}
+
+extern "C" int mpcr_cem_update(mpcr_cem* c, const float* xi, int n, const float* cost, int stride,
+                               const int* elite_idx, int k, float lamda, float alpha_mean, float alpha_cov, float reg,
+                               float* mean, float* cov, int flags, void* stream) {
+  if (!c || !xi || !cost || !elite_idx || !mean || !cov || stride <= 0) return fail(MPCR_EINVAL, "null argument");
+  if (!(flags & MPCR_F_DEVICE_PTRS)) return fail(MPCR_EINVAL, "mpcr_cem_update takes device pointers");
+  if (k <= 0 || k > n || k > TOPK_MAX) return fail(MPCR_EINVAL, "k=%d outside [1, min(n=%d, %d)]", k, n, TOPK_MAX);
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(cem_update_kernel, dim3(1), dim3(1024), 0, st, xi, c->nd * PJ_NB, cost, stride, elite_idx, k,
+                     lamda, alpha_mean, alpha_cov, reg, mean, cov);
+  HIPCHK(hipGetLastError());
+  if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
+  return MPCR_OK;
 }

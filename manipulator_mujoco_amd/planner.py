@@ -2,12 +2,15 @@
 
 Same constructor keywords and the same ``compute_cem`` 9-tuple, so
 ``run_mpc_planner.py`` / ``mpc_planner.run_cem_planner`` only swap the import.
-Per CEM iteration (``cem_iter``, :337-362):
+Per CEM iteration (``cem_iter``, :337-362), every step a HIP kernel of
+libmpcr on the current torch stream (no host round trip inside the loop):
 
-  1. MVN samples xi ~ N(mean, cov + 0.003 I)                (:312-316)  torch
-  2. ADMM projection filter                                 (:180-249)  torch (projection.py)
-  3. thetadot = A_thetadot xi, H physics steps, cost        (:348-354)  HIP  (libmpcr)
-  4. elites (stable argsort, NaN last), mean/cov update     (:305-335)  torch
+  1. L = chol(cov + 0.003 I)                                (:312-316)  mpcr_cem_factor
+  2. MVN samples xi = mean + z L^T fused with the ADMM
+     projection filter                                      (:180-249)  mpcr_cem_sample_project
+  3. thetadot = A_thetadot xi, H physics steps, cost        (:348-354)  mpcr_rollout_cost
+  4. elites (stable argsort, NaN last)                      (:305-310)  mpcr_topk
+  5. weighted mean/cov update                               (:318-335)  mpcr_cem_update
 and finally the best candidate of the last iteration through the packed
 argmin key the rollout kernel reduces with an atomic min (:395-402).
 
@@ -16,8 +19,9 @@ Reference behaviours kept on purpose, each behind a flag:
   * the sampling key is not advanced across calls (fixed ``seed`` per call)
   * ``init_vel`` only enters the boundary vector (the rollout overwrites qvel[:6])
   * a NaN cost wins the final argmin, sorts last among elites.
-The MVN draws use torch's Philox generator, not JAX's threefry, so samples are
-statistically equivalent but not bit-identical to the reference's.
+The MVN draws use Philox4x32-10 keyed by (seed, iteration), not JAX's
+threefry, so samples are statistically equivalent but not bit-identical to
+the reference's.
 """
 
 from __future__ import annotations
@@ -28,9 +32,9 @@ import time
 import numpy as np
 
 from . import _lib, basis, models
+from .cem import CemContext, topk
 from .engine import MPCR_LAYOUT_XI, Engine
 from .mjcf import load_model
-from .projection import ProjectionFilter
 
 DEFAULT_MODEL = "planner_scene"  # SBP/ur5e_hande_mjx/scene.xml (:100)
 
@@ -81,12 +85,17 @@ class cem_planner:  # noqa: N801 (reference name)
         self.hande_id = self.model.hande_body
         self.tcp_id = self.model.tcp_site
         self.engine = Engine(self.model, self.num, self.num_batch, self.Pdot, device=dev)
-        self.proj = ProjectionFilter(self.P, self.Pdot, self.Pddot, self.num_dof, self.device,
-                                     self.v_max, self.a_max, self.p_max)
+        self.cem = CemContext(self.P, self.Pdot, self.Pddot, self.num_dof, self.num_batch, device=dev)
         f32 = dict(dtype=torch.float32, device=self.device)
-        self._cost4 = torch.empty((self.num_batch, 4), **f32)
+        N = self.num_batch
         self._key = torch.empty(1, dtype=torch.int64, device=self.device)
         self._eye = torch.eye(self.nvar, **f32)
+        self._mean = torch.empty(self.nvar, **f32)
+        self._cov = torch.empty((self.nvar, self.nvar), **f32)
+        self._xs = torch.empty((N, self.nvar), **f32)  # xi_samples
+        self._xf = torch.empty((N, self.nvar), **f32)  # xi_filtered
+        self._idx = torch.empty(max(self.ellite_num, 1), dtype=torch.int32, device=self.device)
+        self._beq = torch.empty(5 * self.num_dof, **f32)
         if verbose:
             self.print_info()
 
@@ -113,34 +122,28 @@ class cem_planner:  # noqa: N801 (reference name)
         w = (self.cost_weights["w_pos"], self.cost_weights["w_rot"], self.cost_weights["w_col"])
         f32 = dict(dtype=torch.float32, device=self.device)
 
-        mean = torch.as_tensor(np.asarray(xi_mean, np.float32).reshape(self.nvar), **f32)
-        cov = 10.0 * self._eye
-        b_eq = self.proj.boundary(init_pos, init_vel, init_acc, N)
-        gen = torch.Generator(device=self.device)
-        gen.manual_seed(self.seed)
+        if self.ellite_num < 1:
+            raise ValueError("num_elite * num_batch must select at least one elite")
+        self._mean.copy_(torch.as_tensor(np.asarray(xi_mean, np.float32).reshape(self.nvar)))
+        self._cov.copy_(10.0 * self._eye)  # xi_cov (:386)
+        st = np.stack([init_pos, init_vel, init_acc, np.zeros(d), np.zeros(d)], axis=1)  # state_term (:374-384)
+        self._beq.copy_(torch.as_tensor(st.reshape(5 * d).astype(np.float32)))  # compute_boundary_vec (:174-178)
+        bounds = (self.v_max, self.a_max, self.p_max)
         thetadot = torch.empty((it_n, N, d * H), **f32)
         theta = torch.empty((it_n, N, d * H), **f32)
         costs = torch.empty((it_n, N, 4), **f32)
+        src = self._xf if self.elite_from_filtered else self._xs
         for it in range(it_n):
-            L = torch.linalg.cholesky(cov + 0.003 * self._eye)
-            z = torch.randn((N, self.nvar), generator=gen, **f32)
-            xi_samples = mean + z @ L.T
-            xi_filtered = self.proj(xi_samples, b_eq, self.maxiter_projection) if self.maxiter_projection > 0 \
-                else xi_samples.contiguous()
-            self.engine.rollout_cost(xi_filtered, MPCR_LAYOUT_XI, init_pos, w, target_pos, target_rot,
+            self.cem.factor(self._cov, 0.003)
+            self.cem.sample_project(N, self._mean, self.seed, it, self._beq, self.maxiter_projection, bounds,
+                                    rho=1.0, xi_samples=self._xs, out=self._xf)
+            self.engine.rollout_cost(self._xf, MPCR_LAYOUT_XI, init_pos, w, target_pos, target_rot,
                                      cost4=costs[it], theta=theta[it], thetadot=thetadot[it],
                                      best_key=self._key if it == it_n - 1 else None)
-            cost = costs[it, :, 0]
-            order = torch.sort(cost, stable=True).indices[: self.ellite_num]
-            src = xi_filtered if self.elite_from_filtered else xi_samples
-            xi_e = src[order]
-            c_e = cost[order]
-            wgt = torch.exp(-(1.0 / self.lamda) * (c_e - c_e.min()))
-            sw = wgt.sum()
-            mean_new = (1 - self.alpha_mean) * mean + self.alpha_mean * (wgt[:, None] * xi_e).sum(0) / sw
-            dif = xi_e - mean_new
-            cov = (1 - self.alpha_cov) * cov + self.alpha_cov * (dif.T * wgt) @ dif / sw + 1e-4 * self._eye
-            mean = mean_new
+            topk(self.engine, costs[it], self.ellite_num, stride=4, out=self._idx)
+            self.cem.update(src, costs[it], 4, self._idx, self.lamda, self.alpha_mean, self.alpha_cov,
+                            self._mean, self._cov, reg=1e-4)
+        mean = self._mean
         key = int(self._key.item())
         idx, _ = _lib.decode_key(key & 0xFFFFFFFFFFFFFFFF)
         cost_min = torch.amin(costs[:, :, 0], dim=1)
