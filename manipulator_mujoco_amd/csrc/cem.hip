@@ -398,7 +398,7 @@ __global__ void __launch_bounds__(1024) cem_update_kernel(const float* __restric
       if (ent < nv * nv) {
         const int r = ent / nv, c = ent % nv;
         float s = acc[q];
-        for (int e = 0; e < ne; e++) s = fmaf(w[e0 + e] * d[e][r], d[e][c], s);
+        for (int e = 0; e < ne; e++) s = fmaf(d[e][r] * d[e][c], w[e0 + e], s);  // outer(d, d) * w: symmetric
         acc[q] = s;
       }
     }

@@ -875,7 +875,15 @@ __device__ __forceinline__ void ls_eval3(const Smem& s, int lane, const float qg
 // ---------------------------------------------------------------------------
 // the kernel
 
-__global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args, const DevModel* __restrict__ mptr) {
+// occupancy experiments: -DMPCR_WAVES_PER_EU=n asks the compiler for n waves/SIMD
+#ifdef MPCR_WAVES_PER_EU
+#define MPCR_ROLLOUT_ATTR __attribute__((amdgpu_waves_per_eu(MPCR_WAVES_PER_EU, MPCR_WAVES_PER_EU)))
+#else
+#define MPCR_ROLLOUT_ATTR
+#endif
+
+__global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
+                                                                        const DevModel* __restrict__ mptr) {
   __shared__ Smem s;
   const DevModel* __restrict__ const m0 = mptr;
   const DevModel* __restrict__ m = m0;
@@ -1290,7 +1298,7 @@ __global__ void __launch_bounds__(WAVE) rollout_kernel(RolloutArgs args, const D
           run = sqrtf(dx * dx + dy * dy + dz * dz) <= m->geom_rbound[g1] + m->geom_rbound[g2] + m->pair_margin[p];
         }
       }
-      float dist[4] = {1e30f, 1e30f, 1e30f, 1e30f}, pos[4][3], nrm[4][3];
+      float dist[4] = {1e30f, 1e30f, 1e30f, 1e30f}, pos[4][3] = {}, nrm[4][3] = {};
       int nsl = 0;
       if (run && func != 4) nsl = narrow_lane(m, s, p, dist, pos, nrm);
       const unsigned long long bbm = __ballot(run && func == 4);

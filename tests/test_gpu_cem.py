@@ -91,7 +91,8 @@ def test_projection_given_qinv_and_identity(torch_cuda):
     beq = torch.tensor(cem_np.boundary_vec(_state(1, rng)).astype(np.float32).reshape(-1), device="cuda")
     a = ctx_a.project(xi, beq, 10, BOUNDS).cpu().numpy()
     b = ctx_b.project(xi, beq, 10, BOUNDS).cpu().numpy()
-    assert np.abs(a - b).max() < 1e-4
+    # the two inverses differ only by the fp32 Gram blocks' summation order
+    assert (np.abs(a - b) <= 1e-4 + 1e-4 * np.abs(b)).all(), np.abs(a - b).max()
     same = ctx_a.project(xi, beq, 0, BOUNDS)
     assert torch.equal(same, xi)
 

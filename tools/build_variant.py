@@ -1,0 +1,19 @@
+"""Build libmpcr.so with extra compiler flags into build_variants/<name>.so
+(for tools/ab_session.sh interleaved timing).
+
+    python tools/build_variant.py NAME [extra hipcc flags...]
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from manipulator_mujoco_amd import build  # noqa: E402
+
+name, extra = sys.argv[1], sys.argv[2:]
+out = os.path.join(ROOT, "build_variants", name + ".so")
+os.makedirs(os.path.dirname(out), exist_ok=True)
+cmd = [build.hipcc(), f"--offload-arch={build.ARCH}"] + build.FLAGS + extra + ["-o", out] + build.SRC
+subprocess.run(cmd, check=True)
+print(out)
