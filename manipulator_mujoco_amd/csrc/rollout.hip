@@ -239,6 +239,9 @@ __device__ __forceinline__ void cross_force(float r[6], const float v[6], const 
 // of A in a[]; rows >= n must be identity rows.  On return a[] holds row i of
 // the lower Cholesky factor.  x = A^-1 b for b held one value per lane.
 
+// All DX_NV pivots run even when nv is smaller: a run-time exit inside the
+// unrolled chain breaks it into blocks the scheduler cannot overlap
+// (measured 4.07 -> 4.94 ms), while the padded pivots cost 2/16 of it.
 __device__ __forceinline__ void chol_rows(float (&a)[DX_NV], int lane) {
 #pragma unroll
   for (int k = 0; k < DX_NV; k++) {
@@ -871,6 +874,17 @@ __device__ __forceinline__ void ls_eval3(const Smem& s, int lane, const float qg
     asm volatile("" : "+s"(z_));         \
     m = m0 + z_;                         \
   } while (0)
+// phase-boundary launders (-DMPCR_PHASE_LAUNDER=0 keeps only the per-step one)
+#ifndef MPCR_PHASE_LAUNDER
+#define MPCR_PHASE_LAUNDER 0
+#endif
+#if MPCR_PHASE_LAUNDER
+#define LAUNDER_PHASE() LAUNDER_MODEL()
+#else
+#define LAUNDER_PHASE() \
+  do {                  \
+  } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // the kernel
@@ -934,7 +948,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     sync();
 
     STAMP(0);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- kinematics: local pose per body, then pointer jumping ----------------
     {
       float q[4] = {1.f, 0.f, 0.f, 0.f}, p[3] = {0.f, 0.f, 0.f};
@@ -1008,7 +1022,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     sync();
 
     STAMP(1);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- geom poses, tree COMs ------------------------------------------------
     if (lane < m->ngeom) {
       const int gb = m->geom_body[lane];
@@ -1075,7 +1089,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     }
 
     STAMP(2);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- cinert, cdof ---------------------------------------------------------
     if (lane < nb) {
       const int tr = m->body_tree[lane];
@@ -1149,7 +1163,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     sync();
 
     STAMP(3);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- CRB, velocity, RNE + gravcomp (subtree sums by bitmask) -----------
     for (int idx = lane; idx < nb * 10; idx += WAVE) {
       const int bb = idx / 10, k = idx - bb * 10;
@@ -1228,7 +1242,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     }
     sync();
     STAMP(4);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // mass matrix entries (chain-masked) + bias forces
     for (int idx = lane; idx < DX_NV * DX_NV; idx += WAVE) {
       const int i = idx >> 4, j = idx & 15;
@@ -1266,7 +1280,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     sync();
 
     STAMP(5);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
     {
       float Lm[DX_NV];
@@ -1279,7 +1293,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     }
 
     STAMP(6);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
     //      slots; active contacts compacted into the list; box-box pairs
     //      that pass the bounding-sphere cull are solved wave-cooperatively
@@ -1301,6 +1315,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
       float dist[4] = {1e30f, 1e30f, 1e30f, 1e30f}, pos[4][3] = {}, nrm[4][3] = {};
       int nsl = 0;
       if (run && func != 4) nsl = narrow_lane(m, s, p, dist, pos, nrm);
+      STAMP(11);
       const unsigned long long bbm = __ballot(run && func == 4);
       int act = 0;
       if (valid && func != 4) {
@@ -1349,6 +1364,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
       sync();
       if (lane == 0) s.ncon = base + tot;
       sync();
+      STAMP(12);
       if (bbm && !(m->disableflags & 16)) {
         unsigned long long mm = bbm;
         while (mm) {
@@ -1366,7 +1382,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     }
 
     STAMP(7);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- constraint rows: equality, limits, contacts ------------------------
     {
       const int ncon = s.ncon;
@@ -1522,7 +1538,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     nefc_max = max(nefc_max, s.nefc);
 
     STAMP(8);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- Newton solver (primal), MJX-style line search ------------------------
     {
       const int nefc = s.nefc;
@@ -1551,6 +1567,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         }
         if (lane < DX_NV) s.qacc[lane] = qacc_l;
         sync();
+        STAMP(13);
         const float scale = 1.f / (m->meaninertia * (float)(nv > 1 ? nv : 1));
         float prev_cost = 3.4e38f;
         for (int it = 0;; it++) {
@@ -1607,6 +1624,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           chol_rows(h, lane);
           const float mg = chol_solve(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
           const float search = lane < nv ? -mg : 0.f;
+          STAMP(14);
           if (lane < DX_NV) s.srch[lane] = search;
           sync();
           // Mv, jv, quadratic coefficients
@@ -1654,7 +1672,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     }
 
     STAMP(9);
-    LAUNDER_MODEL();  // phase boundary: no cross-phase model-load CSE
+    LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- Euler: qvel += dt qacc; integrate qpos; warm start -----------------
     {
       const float dt = m->timestep;

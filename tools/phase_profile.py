@@ -12,7 +12,8 @@ sys.path.insert(0, ROOT)
 from manipulator_mujoco_amd import _lib, basis, build, models  # noqa: E402
 
 PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rne", "M/bias", "M solve",
-          "collision", "constraint rows", "newton", "euler"]
+          "coll: box-box", "constraint rows", "newton: line search", "euler", "coll: narrow", "coll: cost+compact",
+          "newton: warm start", "newton: grad/H/chol"]
 
 
 def main():
@@ -44,7 +45,7 @@ def main():
         ph = (ctypes.c_ulonglong * 16)()
         _lib.check(lib.mpcr_rollout_profile(e.handle, xi.ctypes.data, MPCR_LAYOUT_XI, n,
                                             q0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), f(w), f(pt), f(qt), ph))
-    tot = sum(ph[:11])
+    tot = sum(ph[:15])
     print(f"{name}: n={n} H={H} cycles/wave-step {tot / n / H:.0f}")
     for i, p in enumerate(PHASES):
         print(f"  {p:16s} {ph[i] / n / H:10.0f} cyc  {100 * ph[i] / tot:5.1f}%")
