@@ -30,6 +30,14 @@
  *                         (+ compute_projection)              mjx_planner.py:312-316,
  *                                                             180-249
  *   mpcr_cem_update       compute_mean_cov + comp_prod       mjx_planner.py:318-335
+ *   mpcr_rollout_cost_dp  mpcr_rollout_cost with the per-tick arguments
+ *                         (init_pos, weights, target pose) read from device
+ *                         memory, so a whole cem_iter can be graph-captured
+ *                         once and replayed every tick       mjx_planner.py:364-406
+ *   mpcr_plant_*          the closed-loop plant: data.qvel[:num_dof] = thetadot;
+ *                         mujoco.mj_step / mj_forward on the planner's model
+ *                         (CPU MjData in the reference)      mpc_planner.py:109-114,
+ *                                                             120-121,173-184
  */
 #ifndef MPCR_H_
 #define MPCR_H_
@@ -109,6 +117,33 @@ int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, con
                       float* thetadot, uint64_t* best_key, int index_base, int* status, int flags,
                       void* stream);
 
+/* Same as mpcr_rollout_cost with MPCR_F_DEVICE_PTRS, except that the
+   per-call arguments are a device block read when the kernel runs:
+   params[20] = init_pos[8] | (w_pos, w_rot, w_col, 0) | ptgt[3], 0 | qtgt[4]
+   (wxyz, normalised by the kernel).  Graph-capturable. */
+int mpcr_rollout_cost_dp(mpcr_engine* e, const float* input, int layout, int n, const float* params,
+                         float* cost4, float* theta, float* thetadot, uint64_t* best_key, int index_base,
+                         int* status, int flags, void* stream);
+
+/* Closed-loop plant: one environment of the model, stepped by the rollout
+   kernel (fp32 state resident on the device).  Created at the template
+   state (qpos_init, qvel_init, zero warm start). */
+typedef struct mpcr_plant mpcr_plant;
+int mpcr_plant_create(const mpcr_model* m, int device, mpcr_plant** out);
+void mpcr_plant_free(mpcr_plant* p);
+/* Overwrite the state (NULL leaves a part unchanged): qpos[nq], qvel[nv],
+   qacc_warmstart[nv]. */
+int mpcr_plant_set_state(mpcr_plant* p, const double* qpos, const double* qvel, const double* qacc_warmstart);
+/* Read qpos[nq], qvel[nv], qacc[nv] (of the last step / forward) and eef[7] =
+   tcp site position | hande body quaternion (wxyz) evaluated at the state the
+   last step / forward started from (mj_step's kinematics run before the
+   integration).  NULL skips a part. */
+int mpcr_plant_get_state(mpcr_plant* p, double* qpos, double* qvel, double* qacc, double* eef);
+/* commit = 1: mj_step with qvel[:nctrl] = qvel_ctrl first (NULL keeps the
+   current velocities).  commit = 0: mj_forward, the state is not advanced.
+   Blocks until done. */
+int mpcr_plant_step(mpcr_plant* p, const double* qvel_ctrl, int commit, void* stream);
+
 /* argmin over cost[i*stride] with NaN-first / first-index semantics
    (jnp.argmin).  key_out (device, nullable) receives the packed key. */
 int mpcr_argmin(mpcr_engine* e, const float* cost, int stride, int n, int index_base, uint64_t* key_out,
@@ -147,7 +182,7 @@ int mpcr_cem_factor(mpcr_cem* c, const float* cov, float reg, int flags, void* s
    one row shared by all candidates) and multiplier step rho; maxiter = 0
    returns the samples.  xi_out n x nv. */
 int mpcr_cem_sample_project(mpcr_cem* c, int n, const float* mean, uint64_t seed, uint64_t counter,
-                            const float* xi_in, float* xi_samples, const float* b_eq, int beq_stride, int maxiter,
+                            int index_base, const float* xi_in, float* xi_samples, const float* b_eq, int beq_stride, int maxiter,
                             const float* bounds, float rho, float* xi_out, int flags, void* stream);
 /* projection only (compute_projection_filter) */
 int mpcr_project(mpcr_cem* c, const float* xi, const float* b_eq, int beq_stride, int n, int maxiter,

@@ -25,8 +25,11 @@ EXPORTS = (
     "mpcr_last_error", "mpcr_abi_version", "mpcr_device_arch", "mpcr_model_from_blob", "mpcr_model_load",
     "mpcr_model_set_timestep", "mpcr_model_info", "mpcr_model_free", "mpcr_engine_create", "mpcr_engine_free",
     "mpcr_rollout_cost", "mpcr_argmin", "mpcr_best_key_decode", "mpcr_topk", "mpcr_cem_create", "mpcr_cem_free",
-    "mpcr_cem_factor", "mpcr_cem_sample_project", "mpcr_project", "mpcr_cem_update",
+    "mpcr_cem_factor", "mpcr_cem_sample_project", "mpcr_project", "mpcr_cem_update", "mpcr_rollout_cost_dp",
+    "mpcr_plant_create", "mpcr_plant_free", "mpcr_plant_set_state", "mpcr_plant_get_state", "mpcr_plant_step",
 )
+_VOID = ("mpcr_last_error", "mpcr_model_free", "mpcr_engine_free", "mpcr_best_key_decode", "mpcr_cem_free",
+         "mpcr_plant_free")
 
 _lib = None
 
@@ -67,12 +70,18 @@ def load():
     lib.mpcr_cem_free.argtypes = [vp]
     lib.mpcr_cem_free.restype = None
     lib.mpcr_cem_factor.argtypes = [vp, vp, f, i, vp]
-    lib.mpcr_cem_sample_project.argtypes = [vp, i, vp, u64, u64, vp, vp, vp, i, i, P(f), f, vp, i, vp]
+    lib.mpcr_cem_sample_project.argtypes = [vp, i, vp, u64, u64, i, vp, vp, vp, i, i, P(f), f, vp, i, vp]
     lib.mpcr_project.argtypes = [vp, vp, vp, i, i, i, P(f), f, vp, i, vp]
     lib.mpcr_cem_update.argtypes = [vp, vp, i, vp, i, vp, i, f, f, f, f, vp, vp, i, vp]
+    lib.mpcr_rollout_cost_dp.argtypes = [vp, vp, i, i, vp, vp, vp, vp, vp, i, vp, i, vp]
+    lib.mpcr_plant_create.argtypes = [vp, i, P(vp)]
+    lib.mpcr_plant_free.argtypes = [vp]
+    lib.mpcr_plant_free.restype = None
+    lib.mpcr_plant_set_state.argtypes = [vp, P(d), P(d), P(d)]
+    lib.mpcr_plant_get_state.argtypes = [vp, P(d), P(d), P(d), P(d)]
+    lib.mpcr_plant_step.argtypes = [vp, P(d), i, vp]
     for name in EXPORTS + ("mpcr_rollout_trace",):
-        if name not in ("mpcr_last_error", "mpcr_model_free", "mpcr_engine_free", "mpcr_best_key_decode",
-                        "mpcr_cem_free"):
+        if name not in _VOID:
             getattr(lib, name).restype = i
     _lib = lib
     return lib

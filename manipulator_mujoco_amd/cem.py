@@ -84,9 +84,10 @@ class CemContext:
                                           self._stream(cov, stream)))
 
     def sample_project(self, n, mean, seed, counter, b_eq, maxiter, bounds, rho=1.0, xi_samples=None, out=None,
-                       xi_in=None, beq_shared=True, stream=None):
-        """xi_samples = mean + z L^T (Philox (seed, counter)); or ``xi_in`` when
-        mean is None; then ``maxiter`` ADMM iterations.  Returns the projected
+                       xi_in=None, beq_shared=True, index_base=0, stream=None):
+        """xi_samples = mean + z L^T (Philox (seed, counter), candidate i drawn
+        as global candidate ``index_base + i``); or ``xi_in`` when mean is
+        None; then ``maxiter`` ADMM iterations.  Returns the projected
         (n, nvar) tensor."""
         import torch
         ref = mean if mean is not None else xi_in
@@ -103,7 +104,7 @@ class CemContext:
         stride = 0 if beq_shared else 5 * self.num_dof
         check(_lib.load().mpcr_cem_sample_project(
             self.handle, int(n), _ptr(mean), ctypes.c_uint64(int(seed) & (2**64 - 1)),
-            ctypes.c_uint64(int(counter) & (2**64 - 1)), _ptr(xi_in), _ptr(xi_samples), _ptr(b_eq), stride,
+            ctypes.c_uint64(int(counter) & (2**64 - 1)), int(index_base), _ptr(xi_in), _ptr(xi_samples), _ptr(b_eq), stride,
             int(maxiter), bnd, float(rho), _ptr(out), MPCR_F_DEVICE_PTRS, self._stream(ref, stream)))
         return out
 

@@ -40,6 +40,7 @@ struct ProjArgs {
   const float* QbT;       // 5nd x nd*12:   QbT[m][r] = Qinv[r][nv + m]
   unsigned long long seed, counter;
   int n, nd, H, maxiter, beq_stride;
+  int index_base;         // global index of candidate 0 (Philox counter word 0)
   float bound[3];         // v_max, a_max, p_max
   float rho;
 };
@@ -87,7 +88,7 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
     float z[PJ_BLK];
 #pragma unroll
     for (int q = 0; q < 3; q++) {
-      uint32_t c[4] = {(uint32_t)cand, (uint32_t)(j * 3 + q), (uint32_t)a.counter, (uint32_t)(a.counter >> 32)};
+      uint32_t c[4] = {(uint32_t)(cand + a.index_base), (uint32_t)(j * 3 + q), (uint32_t)a.counter, (uint32_t)(a.counter >> 32)};
       philox4(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
       box_muller(c[0], c[1], z[4 * q + 0], z[4 * q + 1]);
       box_muller(c[2], c[3], z[4 * q + 2], z[4 * q + 3]);

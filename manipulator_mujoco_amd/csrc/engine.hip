@@ -433,33 +433,51 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   delete e;
 }
 
-static int launch_rollout(mpcr_engine* e, const float* in, int layout, int n, const double* q0, const float* w,
-                          const float* ptgt, const float* qtgt, float* cost4, float* theta, float* thetadot,
-                          unsigned long long* key, int index_base, int* status, float* trace_eef,
-                          float* trace_slots, bool reset_key, hipStream_t st) {
+// per-call parameter block of the kernel (RolloutArgs::par layout)
+static void fill_par(float* par, int nc, const double* q0, const float* w, const float* ptgt, const float* qtgt) {
+  for (int k = 0; k < PAR_N; k++) par[k] = 0.f;
+  if (q0)
+    for (int k = 0; k < nc; k++) par[PAR_Q0 + k] = (float)q0[k];
+  for (int k = 0; k < 3; k++) { par[PAR_W + k] = w[k]; par[PAR_PT + k] = ptgt[k]; }
+  for (int k = 0; k < 4; k++) par[PAR_QT + k] = qtgt[k];
+}
+
+struct Launch {
+  const float* in = nullptr;
+  int layout = 0, n = 0, index_base = 0, plant = 0;
+  const float* dpar = nullptr;  // device parameter block (else par)
+  float par[PAR_N] = {};
+  float* state = nullptr;
+  float *cost4 = nullptr, *theta = nullptr, *thetadot = nullptr, *trace_eef = nullptr, *trace_slots = nullptr;
+  unsigned long long* key = nullptr;
+  int* status = nullptr;
+  bool reset_key = false;
+};
+
+static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   RolloutArgs a;
   std::memset(&a, 0, sizeof(a));
   a.m = e->d_model;
-  a.input = in;
+  a.input = l.in;
   a.pdot = e->d_pdot;
-  a.cost4 = cost4;
-  a.theta = theta;
-  a.thetadot = thetadot;
-  a.best_key = key;
-  a.status = status;
-  a.trace_eef = trace_eef;
-  a.trace_slots = trace_slots;
-  a.layout = layout;
-  a.n = n;
+  a.cost4 = l.cost4;
+  a.theta = l.theta;
+  a.thetadot = l.thetadot;
+  a.best_key = l.key;
+  a.status = l.status;
+  a.trace_eef = l.trace_eef;
+  a.trace_slots = l.trace_slots;
+  a.dpar = l.dpar;
+  a.state = l.state;
+  a.plant = l.plant;
+  a.layout = l.layout;
+  a.n = l.n;
   a.H = e->H;
   a.nbasis = e->nbasis;
-  a.index_base = index_base;
-  for (int k = 0; k < e->host.nctrl; k++) a.q0[k] = (float)q0[k];
-  for (int k = 0; k < 3; k++) { a.w[k] = w[k]; a.ptgt[k] = ptgt[k]; }
-  float qn = std::sqrt(qtgt[0] * qtgt[0] + qtgt[1] * qtgt[1] + qtgt[2] * qtgt[2] + qtgt[3] * qtgt[3]);
-  for (int k = 0; k < 4; k++) a.qtgt[k] = qtgt[k] / qn;
-  if (key && reset_key) hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, key, ~0ull);
-  hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
+  a.index_base = l.index_base;
+  std::memcpy(a.par, l.par, sizeof(a.par));
+  if (l.key && l.reset_key) hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, l.key, ~0ull);
+  hipLaunchKernelGGL(rollout_kernel, dim3(l.n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
   HIPCHK(hipGetLastError());
   return MPCR_OK;
 }
@@ -477,17 +495,24 @@ extern "C" int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout,
   auto* key = reinterpret_cast<unsigned long long*>(best_key);
   const int nc = e->host.nctrl;
   const size_t cols = layout == MPCR_LAYOUT_XI ? (size_t)nc * e->nbasis : (size_t)nc * e->H;
+  Launch l;
+  l.layout = layout;
+  l.n = n;
+  l.index_base = index_base;
+  fill_par(l.par, nc, q0, w, ptgt, qtgt);
   if (flags & MPCR_F_DEVICE_PTRS) {
-    int rc = launch_rollout(e, input, layout, n, q0, w, ptgt, qtgt, cost4, theta, thetadot, key, index_base, status,
-                            nullptr, nullptr, (flags & MPCR_F_RESET_BEST) != 0, st);
+    l.in = input; l.cost4 = cost4; l.theta = theta; l.thetadot = thetadot; l.key = key; l.status = status;
+    l.reset_key = (flags & MPCR_F_RESET_BEST) != 0;
+    int rc = launch_rollout(e, l, st);
     if (rc) return rc;
     if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
     return MPCR_OK;
   }
   HIPCHK(hipMemcpyAsync(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice, st));
-  int rc = launch_rollout(e, e->d_in, layout, n, q0, w, ptgt, qtgt, e->d_cost, theta ? e->d_theta : nullptr,
-                          thetadot ? e->d_thetadot : nullptr, best_key ? e->d_key : nullptr, index_base,
-                          status ? e->d_status : nullptr, nullptr, nullptr, true, st);
+  l.in = e->d_in; l.cost4 = e->d_cost; l.theta = theta ? e->d_theta : nullptr;
+  l.thetadot = thetadot ? e->d_thetadot : nullptr; l.key = best_key ? e->d_key : nullptr;
+  l.status = status ? e->d_status : nullptr; l.reset_key = true;
+  int rc = launch_rollout(e, l, st);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(cost4, e->d_cost, sizeof(float) * 4 * n, hipMemcpyDeviceToHost, st));
   if (theta) HIPCHK(hipMemcpyAsync(theta, e->d_theta, sizeof(float) * n * nc * e->H, hipMemcpyDeviceToHost, st));
@@ -495,6 +520,133 @@ extern "C" int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout,
     HIPCHK(hipMemcpyAsync(thetadot, e->d_thetadot, sizeof(float) * n * nc * e->H, hipMemcpyDeviceToHost, st));
   if (best_key) HIPCHK(hipMemcpyAsync(best_key, e->d_key, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   if (status) HIPCHK(hipMemcpyAsync(status, e->d_status, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_rollout_cost_dp(mpcr_engine* e, const float* input, int layout, int n, const float* params,
+                                    float* cost4, float* theta, float* thetadot, uint64_t* best_key, int index_base,
+                                    int* status, int flags, void* stream) {
+  if (!e || !input || !params || !cost4) return fail(MPCR_EINVAL, "null argument");
+  if (n < 0 || n > e->max_n) return fail(MPCR_EINVAL, "n=%d outside [0, max_n=%d]", n, e->max_n);
+  if (layout != MPCR_LAYOUT_XI && layout != MPCR_LAYOUT_THETADOT) return fail(MPCR_EINVAL, "bad layout %d", layout);
+  if (n == 0) return MPCR_OK;
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  Launch l;
+  l.layout = layout; l.n = n; l.index_base = index_base; l.dpar = params;
+  l.in = input; l.cost4 = cost4; l.theta = theta; l.thetadot = thetadot;
+  l.key = reinterpret_cast<unsigned long long*>(best_key); l.status = status;
+  l.reset_key = (flags & MPCR_F_RESET_BEST) != 0;
+  int rc = launch_rollout(e, l, st);
+  if (rc) return rc;
+  if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
+  return MPCR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// closed-loop plant: one environment stepped by the same kernel (n = 1, H = 1,
+// qvel[:nctrl] overridden like SBP/mpc_planner.py:179-180), state resident on
+// the device between calls
+
+struct mpcr_plant {
+  mpcr_engine* e = nullptr;
+  float* d_state = nullptr;  // ST_N floats (rollout.hip layout)
+  float* d_in = nullptr;     // nctrl joint velocities
+  float* d_cost = nullptr;   // unused cost4 of the single "candidate"
+  float h_state[ST_N] = {};
+};
+
+extern "C" void mpcr_plant_free(mpcr_plant* p) {
+  if (!p) return;
+  (void)hipFree(p->d_state);
+  (void)hipFree(p->d_in);
+  (void)hipFree(p->d_cost);
+  mpcr_engine_free(p->e);
+  delete p;
+}
+
+extern "C" int mpcr_plant_create(const mpcr_model* m, int device, mpcr_plant** out) {
+  if (!m || !out) return fail(MPCR_EINVAL, "null argument");
+  const float pdot[1] = {0.f};
+  auto* p = new mpcr_plant;
+  int rc = mpcr_engine_create(m, device, 1, 1, pdot, 1, &p->e);
+  if (rc) { delete p; return rc; }
+  if (hipMalloc(&p->d_state, sizeof(float) * ST_N) != hipSuccess ||
+      hipMalloc(&p->d_in, sizeof(float) * DX_NCTRL) != hipSuccess ||
+      hipMalloc(&p->d_cost, sizeof(float) * 4) != hipSuccess) {
+    mpcr_plant_free(p);
+    return fail(MPCR_ENOMEM, "device allocation failed");
+  }
+  const mpcr_model_t& h = p->e->host;
+  for (int i = 0; i < h.nq; i++) p->h_state[ST_QPOS + i] = (float)h.qpos_init[i];
+  for (int i = 0; i < h.nv; i++) p->h_state[ST_QVEL + i] = (float)h.qvel_init[i];
+  if (hipMemcpy(p->d_state, p->h_state, sizeof(float) * ST_N, hipMemcpyHostToDevice) != hipSuccess) {
+    mpcr_plant_free(p);
+    return fail(MPCR_EHIP, "state upload failed");
+  }
+  *out = p;
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_plant_set_state(mpcr_plant* p, const double* qpos, const double* qvel,
+                                    const double* qacc_warmstart) {
+  if (!p) return fail(MPCR_EINVAL, "null plant");
+  HIPCHK(hipSetDevice(p->e->device));
+  const mpcr_model_t& h = p->e->host;
+  HIPCHK(hipMemcpy(p->h_state, p->d_state, sizeof(float) * ST_N, hipMemcpyDeviceToHost));
+  if (qpos)
+    for (int i = 0; i < h.nq; i++) p->h_state[ST_QPOS + i] = (float)qpos[i];
+  if (qvel)
+    for (int i = 0; i < h.nv; i++) p->h_state[ST_QVEL + i] = (float)qvel[i];
+  if (qacc_warmstart)
+    for (int i = 0; i < h.nv; i++) p->h_state[ST_QWS + i] = (float)qacc_warmstart[i];
+  HIPCHK(hipMemcpy(p->d_state, p->h_state, sizeof(float) * ST_N, hipMemcpyHostToDevice));
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_plant_get_state(mpcr_plant* p, double* qpos, double* qvel, double* qacc, double* eef) {
+  if (!p) return fail(MPCR_EINVAL, "null plant");
+  HIPCHK(hipSetDevice(p->e->device));
+  const mpcr_model_t& h = p->e->host;
+  HIPCHK(hipMemcpy(p->h_state, p->d_state, sizeof(float) * ST_N, hipMemcpyDeviceToHost));
+  if (qpos)
+    for (int i = 0; i < h.nq; i++) qpos[i] = p->h_state[ST_QPOS + i];
+  if (qvel)
+    for (int i = 0; i < h.nv; i++) qvel[i] = p->h_state[ST_QVEL + i];
+  if (qacc)
+    for (int i = 0; i < h.nv; i++) qacc[i] = p->h_state[ST_QACC + i];
+  if (eef)
+    for (int i = 0; i < 7; i++) eef[i] = p->h_state[ST_EEF + i];
+  return MPCR_OK;
+}
+
+// commit = 0: mj_forward (qacc and the eef pose of the current state, nothing
+// advanced; qvel_ctrl ignored); commit = 1: mj_step with qvel[:nctrl] =
+// qvel_ctrl (NULL keeps the current joint velocities)
+extern "C" int mpcr_plant_step(mpcr_plant* p, const double* qvel_ctrl, int commit, void* stream) {
+  if (!p) return fail(MPCR_EINVAL, "null plant");
+  mpcr_engine* e = p->e;
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int nc = e->host.nctrl;
+  float v[DX_NCTRL] = {};
+  if (!commit || !qvel_ctrl) {
+    HIPCHK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(float) * ST_N, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int k = 0; k < nc; k++) v[k] = p->h_state[ST_QVEL + e->host.ctrl_dofadr[k]];
+  } else {
+    for (int k = 0; k < nc; k++) v[k] = (float)qvel_ctrl[k];
+  }
+  HIPCHK(hipMemcpyAsync(p->d_in, v, sizeof(float) * nc, hipMemcpyHostToDevice, st));
+  Launch l;
+  l.layout = MPCR_LAYOUT_THETADOT; l.n = 1; l.in = p->d_in; l.cost4 = p->d_cost;
+  l.state = p->d_state; l.plant = commit ? 3 : 1;
+  const double q0[DX_NCTRL] = {};
+  const float w[3] = {0.f, 0.f, 0.f}, pt[3] = {0.f, 0.f, 0.f}, qt[4] = {1.f, 0.f, 0.f, 0.f};
+  fill_par(l.par, nc, q0, w, pt, qt);
+  int rc = launch_rollout(e, l, st);
+  if (rc) return rc;
   HIPCHK(hipStreamSynchronize(st));
   return MPCR_OK;
 }
@@ -514,8 +666,11 @@ extern "C" int mpcr_rollout_trace(mpcr_engine* e, const float* input, int layout
   HIPCHK(hipMalloc(&d_eef, sizeof(float) * n * e->H * 7));
   HIPCHK(hipMalloc(&d_slots, sizeof(float) * n * e->H * nslot));
   HIPCHK(hipMemcpy(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice));
-  int rc = launch_rollout(e, e->d_in, layout, n, q0, w, ptgt, qtgt, e->d_cost, e->d_theta, nullptr, nullptr, 0,
-                          e->d_status, d_eef, d_slots, false, nullptr);
+  Launch l;
+  l.layout = layout; l.n = n; l.in = e->d_in; l.cost4 = e->d_cost; l.theta = e->d_theta; l.status = e->d_status;
+  l.trace_eef = d_eef; l.trace_slots = d_slots;
+  fill_par(l.par, nc, q0, w, ptgt, qtgt);
+  int rc = launch_rollout(e, l, nullptr);
   if (rc == 0) {
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(cost4, e->d_cost, sizeof(float) * 4 * n, hipMemcpyDeviceToHost));
@@ -544,10 +699,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   std::memset(&a, 0, sizeof(a));
   a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
-  for (int k = 0; k < nc; k++) a.q0[k] = (float)q0[k];
-  for (int k = 0; k < 3; k++) { a.w[k] = w[k]; a.ptgt[k] = ptgt[k]; }
-  float qn = std::sqrt(qtgt[0] * qtgt[0] + qtgt[1] * qtgt[1] + qtgt[2] * qtgt[2] + qtgt[3] * qtgt[3]);
-  for (int k = 0; k < 4; k++) a.qtgt[k] = qtgt[k] / qn;
+  fill_par(a.par, nc, q0, w, ptgt, qtgt);
   hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(phases16, d_prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -765,7 +917,7 @@ extern "C" int mpcr_cem_factor(mpcr_cem* c, const float* cov, float reg, int fla
 }
 
 extern "C" int mpcr_cem_sample_project(mpcr_cem* c, int n, const float* mean, uint64_t seed, uint64_t counter,
-                                       const float* xi_in, float* xi_samples, const float* b_eq, int beq_stride,
+                                       int index_base, const float* xi_in, float* xi_samples, const float* b_eq, int beq_stride,
                                        int maxiter, const float* bounds, float rho, float* xi_out, int flags,
                                        void* stream) {
   if (!c || !xi_out) return fail(MPCR_EINVAL, "null argument");
@@ -791,6 +943,7 @@ extern "C" int mpcr_cem_sample_project(mpcr_cem* c, int n, const float* mean, ui
   a.QbT = c->d_QbT;
   a.seed = seed;
   a.counter = counter;
+  a.index_base = index_base;
   a.n = n;
   a.nd = c->nd;
   a.H = c->H;
@@ -808,7 +961,7 @@ extern "C" int mpcr_cem_sample_project(mpcr_cem* c, int n, const float* mean, ui
 extern "C" int mpcr_project(mpcr_cem* c, const float* xi, const float* b_eq, int beq_stride, int n, int maxiter,
                             const float* bounds, float rho, float* xi_out, int flags, void* stream) {
   if (!xi) return fail(MPCR_EINVAL, "null xi");
-  return mpcr_cem_sample_project(c, n, nullptr, 0, 0, xi, nullptr, b_eq, beq_stride, maxiter, bounds, rho, xi_out,
+  return mpcr_cem_sample_project(c, n, nullptr, 0, 0, 0, xi, nullptr, b_eq, beq_stride, maxiter, bounds, rho, xi_out,
                                  flags, stream);
 }
 

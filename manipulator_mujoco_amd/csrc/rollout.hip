@@ -23,6 +23,11 @@ constexpr float kMinVal = 1e-15f;
 constexpr float kMinImp = 0.0001f;
 constexpr float kMaxImp = 0.9999f;
 
+// per-call parameter block (RolloutArgs::par / dpar) and plant state layout
+enum { PAR_Q0 = 0, PAR_W = 8, PAR_PT = 12, PAR_QT = 16, PAR_N = 20 };
+enum { ST_QPOS = 0, ST_QVEL = DX_NQ, ST_QWS = ST_QVEL + DX_NV, ST_QACC = ST_QWS + DX_NV, ST_EEF = ST_QACC + DX_NV,
+       ST_N = ST_EEF + 8 };
+
 struct RolloutArgs {
   const DevModel* m;
   const float* input;
@@ -35,11 +40,16 @@ struct RolloutArgs {
   float* trace_eef;    // n x H x 7 (debug)
   float* trace_slots;  // n x H x nslot (debug)
   unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
-  int layout, n, H, nbasis, index_base, pad_;
-  float q0[DX_NCTRL];
-  float w[4];
-  float ptgt[4];
-  float qtgt[4];  // normalised
+  // per-call parameters: by value (par) or, for graph-captured ticks, read
+  // from device memory (dpar, same layout) when the launch runs
+  const float* dpar;
+  // plant mode (single environment, mpcr_plant_*): plant & 1 starts from
+  // state (qpos | qvel | qacc_warmstart) instead of the template,
+  // plant & 2 writes the final state back; qacc and the pre-integration eef
+  // pose of the last step always go to state when plant != 0
+  float* state;
+  int layout, n, H, nbasis, index_base, plant;
+  float par[PAR_N];  // q0[8] | w[4] | ptgt[4] | qtgt[4] (any norm)
 };
 
 // Row stride 20 floats (80 B): rows are 16-byte aligned for ds_read_b128 and
@@ -66,6 +76,7 @@ struct __align__(16) Smem {
   alignas(16) float gxpos[DX_NG][4];   // gxpos+gxmat (dead during Newton) double as the
   float gxmat[DX_NG][12];  // Hessian solve's LDS scratch
   float cprev[DX_NSLOT];  // previous-step masked slot distances (cost_c)
+  float par[PAR_N];       // q0 | w | ptgt | qtgt (normalised)
   int ncon, nefc, pad_[2];
   // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the
   //      contact / constraint arrays (collision .. Newton) ----
@@ -908,14 +919,25 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
   const int nv = m->nv, nb = m->nbody, nc = m->nctrl;
 
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
-  for (int i = lane; i < DX_NQ; i += WAVE) s.qpos[i] = i < m->nq ? m->qpos_init[i] : 0.f;
+  //      (plant mode: the caller's state, no init_pos override)
+  if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
+  const bool from_state = (args.plant & 1) != 0;
+  for (int i = lane; i < DX_NQ; i += WAVE)
+    s.qpos[i] = i < m->nq ? (from_state ? args.state[ST_QPOS + i] : m->qpos_init[i]) : 0.f;
   if (lane < DX_NV) {
-    s.qvel[lane] = lane < nv ? m->qvel_init[lane] : 0.f;
-    s.qws[lane] = 0.f;
+    const bool v = lane < nv;
+    s.qvel[lane] = v ? (from_state ? args.state[ST_QVEL + lane] : m->qvel_init[lane]) : 0.f;
+    s.qws[lane] = v && from_state ? args.state[ST_QWS + lane] : 0.f;
     s.qacc[lane] = 0.f;
   }
   sync();
-  if (lane < nc) s.qpos[m->ctrl_qposadr[lane]] = args.q0[lane];
+  if (lane == 0) {  // normalise the target quaternion once
+    const float* q = &s.par[PAR_QT];
+    const float qn = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    s.par[PAR_QT] = q[0] / qn; s.par[PAR_QT + 1] = q[1] / qn; s.par[PAR_QT + 2] = q[2] / qn;
+    s.par[PAR_QT + 3] = q[3] / qn;
+  }
+  if (lane < nc && !from_state) s.qpos[m->ctrl_qposadr[lane]] = s.par[PAR_Q0 + lane];
   if (args.layout == 0) {
     const int nx = nc * args.nbasis;
     for (int i = lane; i < nx; i += WAVE) s.xi[i] = args.input[(size_t)b * nx + i];
@@ -1077,13 +1099,19 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         eq[0] = s.xquat[m->hande_body][0]; eq[1] = s.xquat[m->hande_body][1];
         eq[2] = s.xquat[m->hande_body][2]; eq[3] = s.xquat[m->hande_body][3];
       }
-      float dx = ep[0] - args.ptgt[0], dy = ep[1] - args.ptgt[1], dz = ep[2] - args.ptgt[2];
+      const float* pt = &s.par[PAR_PT];
+      const float* qt = &s.par[PAR_QT];
+      float dx = ep[0] - pt[0], dy = ep[1] - pt[1], dz = ep[2] - pt[2];
       cost_g += sqrtf(dx * dx + dy * dy + dz * dz);
       float qn = sqrtf(eq[0] * eq[0] + eq[1] * eq[1] + eq[2] * eq[2] + eq[3] * eq[3]);
-      float dq = fabsf((eq[0] * args.qtgt[0] + eq[1] * args.qtgt[1] + eq[2] * args.qtgt[2] + eq[3] * args.qtgt[3]) / qn);
+      float dq = fabsf((eq[0] * qt[0] + eq[1] * qt[1] + eq[2] * qt[2] + eq[3] * qt[3]) / qn);
       cost_r += 2.f * acosf(clampf(dq, -1.f, 1.f));
       if (args.trace_eef) {
         float* e = args.trace_eef + ((size_t)b * H + t) * 7;
+        e[0] = ep[0]; e[1] = ep[1]; e[2] = ep[2]; e[3] = eq[0]; e[4] = eq[1]; e[5] = eq[2]; e[6] = eq[3];
+      }
+      if (args.plant && t == H - 1) {
+        float* e = args.state + ST_EEF;
         e[0] = ep[0]; e[1] = ep[1]; e[2] = ep[2]; e[3] = eq[0]; e[4] = eq[1]; e[5] = eq[2]; e[6] = eq[3];
       }
     }
@@ -1710,6 +1738,16 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
 
   STAMP(10);
   PROF_FLUSH
+  if (args.plant) {  // single-environment plant: qacc of the last step, state back
+    if (lane < nv) args.state[ST_QACC + lane] = s.qacc[lane];
+    if (args.plant & 2) {
+      if (lane < m->nq) args.state[ST_QPOS + lane] = s.qpos[lane];
+      if (lane < nv) {
+        args.state[ST_QVEL + lane] = s.qvel[lane];
+        args.state[ST_QWS + lane] = s.qws[lane];
+      }
+    }
+  }
   // ---- final reductions, outputs ----------------------------------------------
   cost_c = wsum(cost_c);
   bool finite = true;
@@ -1717,7 +1755,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
   finite = __all(finite);
   if (!finite) status |= 2;
   if (lane == 0) {
-    const float cost = args.w[0] * cost_g + args.w[1] * cost_r + args.w[2] * cost_c;
+    const float cost = s.par[PAR_W] * cost_g + s.par[PAR_W + 1] * cost_r + s.par[PAR_W + 2] * cost_c;
     args.cost4[4 * (size_t)b + 0] = cost;
     args.cost4[4 * (size_t)b + 1] = cost_g;
     args.cost4[4 * (size_t)b + 2] = cost_r;

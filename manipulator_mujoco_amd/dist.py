@@ -1,11 +1,20 @@
-"""Multi-GPU selection: one process per GPU, candidates sharded by rank.
+"""Multi-GPU exchanges: one process per GPU, candidates sharded by rank.
 
-The only exchange the rollout path needs is the global best candidate
+Rollouts need one exchange, the global best candidate
 (``idx_min = argmin(cost_batch[-1])``, SBP/mjx_planner.py:395).  Each rank's
 rollout kernel atomically min-reduces a packed 64-bit key
 ``ordered(cost) << 32 | global_index`` (NaN first, ties to the lowest index:
 jnp.argmin semantics); ranks then all-reduce that single int64 with MIN —
 one 8-byte RCCL collective over xGMI (``nccl`` backend) or gloo on CPU.
+
+A sharded CEM iteration adds the elite exchange
+(``gather_elites``): every global elite is among its rank's local top-E, so
+ranks all-gather their local top-E rows (cost + xi) and every rank selects
+the same global top-E from the gathered block.  Gathered positions are
+rank-major and each rank's rows are in (cost, index) order, so ties broken
+by position are ties broken by global index: the selection equals the
+single-GPU ``argsort(kind="stable")[:E]`` in order and the replicated
+mean/cov update is bit-identical to the single-GPU one.
 """
 
 from __future__ import annotations
@@ -59,3 +68,46 @@ def shard(n_total: int, rank: int, world: int):
 def env_rank():
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
             int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def gather_elites(cost, xi, k, topk_fn, group=None):
+    """Global top-``k`` elites of a sharded batch.
+
+    cost: local (n,) float32; xi: local (n, nv) rows the update reads;
+    topk_fn(cost_1d, k) -> int indices of the k smallest in stable-argsort
+    order, NaN last (``mpcr_topk`` on a GPU rank).  Every rank must hold the
+    same n.  Returns (gathered cost (G*kl,), gathered rows (G*kl, nv),
+    selected positions (k,)); gathered[sel] are the global elites in order.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    n, nv = xi.shape
+    kl = min(int(k), n)
+    if kl * world < k:
+        raise ValueError(f"k={k} elites need more than {world} x {n} candidates")
+    lidx = topk_fn(cost, kl).long()
+    pack = torch.empty((kl, nv + 1), dtype=xi.dtype, device=xi.device)
+    pack[:, :nv] = xi.index_select(0, lidx)
+    pack[:, nv] = cost.index_select(0, lidx)
+    out = torch.empty((world * kl, nv + 1), dtype=xi.dtype, device=xi.device)
+    dist.all_gather_into_tensor(out, pack, group=group)
+    g_cost = out[:, nv].contiguous()
+    g_xi = out[:, :nv].contiguous()
+    sel = topk_fn(g_cost, int(k))
+    return g_cost, g_xi, sel
+
+
+def allgather_min(values, group=None):
+    """Elementwise NaN-propagating min over ranks (jnp.min semantics) of a
+    small 1-D tensor; returned on the host as float32 numpy."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    out = torch.empty((world,) + tuple(values.shape), dtype=values.dtype, device=values.device)
+    dist.all_gather_into_tensor(out, values.contiguous(), group=group)
+    a = out.cpu().numpy()
+    return np.where(np.isnan(a).any(axis=0), np.nan, np.nanmin(np.where(np.isnan(a), np.inf, a), axis=0)).astype(
+        np.float32)

@@ -119,6 +119,36 @@ class Engine:
             best_key[...] = key
         return cost4
 
+    @staticmethod
+    def params(q0, w, ptgt, qtgt):
+        """The 20-float parameter block ``mpcr_rollout_cost_dp`` reads on the
+        device: init_pos[8] | w[3], 0 | ptgt[3], 0 | qtgt[4]."""
+        p = np.zeros(20, dtype=np.float32)
+        q0 = np.asarray(q0, dtype=np.float64).reshape(-1)
+        p[: q0.size] = q0
+        p[8:11] = np.asarray(w, dtype=np.float32).reshape(-1)[:3]
+        p[12:15] = np.asarray(ptgt, dtype=np.float32).reshape(-1)[:3]
+        p[16:20] = np.asarray(qtgt, dtype=np.float32).reshape(-1)[:4]
+        return p
+
+    def rollout_cost_dp(self, inp, layout: int, params, cost4, theta=None, thetadot=None, best_key=None,
+                        index_base: int = 0, status=None, reset_best: bool = True, stream=None):
+        """``rollout_cost`` with the per-call arguments in a device tensor
+        (``params``, 20 float32, see ``Engine.params``): graph-capturable."""
+        import torch
+        for name, t in (("input", inp), ("params", params), ("cost4", cost4)):
+            if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous float32 CUDA tensor")
+        if params.numel() < 20:
+            raise ValueError("params needs 20 floats")
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        st = stream if stream is not None else torch.cuda.current_stream(inp.device).cuda_stream
+        flags = MPCR_F_DEVICE_PTRS | (MPCR_F_RESET_BEST if reset_best else 0)
+        check(_lib.load().mpcr_rollout_cost_dp(self.handle, ptr(inp), layout, int(inp.shape[0]), ptr(params),
+                                               ptr(cost4), ptr(theta), ptr(thetadot), ptr(best_key),
+                                               int(index_base), ptr(status), flags, ctypes.c_void_p(st)))
+        return cost4
+
     def trace(self, inp, layout: int, q0, w, ptgt, qtgt):
         """Debug/parity run (host arrays): cost4, theta, per-step eef pose, masked slot distances."""
         lib = _lib.load()
@@ -140,4 +170,72 @@ class Engine:
         return dict(cost4=cost4, theta=theta, eef=eef, slots=slots[:, :, : self.nslot])
 
 
-__all__ = ["Engine", "Model", "MPCR_LAYOUT_XI", "MPCR_LAYOUT_THETADOT"]
+class Plant:
+    """One environment of a compiled model stepped on the GPU by the rollout
+    kernel (``mpcr_plant_*``): the closed-loop plant of
+    ``run_cem_planner`` (CPU ``MjData`` + ``mj_step`` in the reference,
+    SBP/mpc_planner.py:109-114,179-180).  State is fp32 on the device."""
+
+    def __init__(self, compiled_model, device: int = 0):
+        lib = _lib.load()
+        self.model = Model(compiled_model)
+        self.nq, self.nv = int(compiled_model.nq), int(compiled_model.nv)
+        self.nctrl = int(compiled_model.nctrl)
+        h = ctypes.c_void_p()
+        check(lib.mpcr_plant_create(self.model.handle, int(device), ctypes.byref(h)))
+        self.handle = h
+        self.qpos = np.zeros(self.nq)
+        self.qvel = np.zeros(self.nv)
+        self.qacc = np.zeros(self.nv)
+        self.eef = np.zeros(7)
+        self._pull()
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                _lib.load().mpcr_plant_free(self.handle)
+        except Exception:  # interpreter shutdown
+            pass
+        self.handle = None
+
+    def _pull(self):
+        dp = ctypes.POINTER(ctypes.c_double)
+        check(_lib.load().mpcr_plant_get_state(self.handle, self.qpos.ctypes.data_as(dp),
+                                               self.qvel.ctypes.data_as(dp), self.qacc.ctypes.data_as(dp),
+                                               self.eef.ctypes.data_as(dp)))
+
+    def set_state(self, qpos=None, qvel=None, qacc_warmstart=None):
+        dp = ctypes.POINTER(ctypes.c_double)
+        arr = lambda x, n: None if x is None else np.ascontiguousarray(x, dtype=np.float64).reshape(n)  # noqa: E731
+        qp, qv, qw = arr(qpos, self.nq), arr(qvel, self.nv), arr(qacc_warmstart, self.nv)
+        check(_lib.load().mpcr_plant_set_state(self.handle, None if qp is None else qp.ctypes.data_as(dp),
+                                               None if qv is None else qv.ctypes.data_as(dp),
+                                               None if qw is None else qw.ctypes.data_as(dp)))
+        self._pull()
+
+    def forward(self):
+        """mj_forward: qacc and the eef pose at the current state."""
+        check(_lib.load().mpcr_plant_step(self.handle, None, 0, None))
+        self._pull()
+
+    def step(self, qvel_ctrl=None):
+        """qvel[:nctrl] = qvel_ctrl; mj_step.  Afterwards ``eef`` holds the tcp
+        position / hande quaternion of the state the step started from (as
+        MjData.site_xpos / xquat after mj_step)."""
+        dp = ctypes.POINTER(ctypes.c_double)
+        v = None
+        if qvel_ctrl is not None:
+            v = np.ascontiguousarray(qvel_ctrl, dtype=np.float64).reshape(self.nctrl)
+        check(_lib.load().mpcr_plant_step(self.handle, None if v is None else v.ctypes.data_as(dp), 1, None))
+        self._pull()
+
+    @property
+    def site_xpos_tcp(self):
+        return self.eef[:3].copy()
+
+    @property
+    def xquat_hande(self):
+        return self.eef[3:7].copy()
+
+
+__all__ = ["Engine", "Model", "Plant", "MPCR_LAYOUT_XI", "MPCR_LAYOUT_THETADOT"]

@@ -51,3 +51,52 @@ def test_global_best_two_ranks(case):
     for r in range(2):
         idx, val = md.decode_key(out[r])
         assert idx == expect
+
+
+def _stable_topk(cost, k):
+    import torch
+    c = cost.numpy()
+    return torch.as_tensor(np.argsort(np.where(np.isnan(c), np.inf, c), kind="stable")[:k].copy())
+
+
+def _elite_worker(rank, world, port, costs, xi, k, out):
+    import torch
+    import torch.distributed as dist
+
+    from manipulator_mujoco_amd import dist as md
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = len(costs) // world
+    lo = rank * n
+    c = torch.tensor(costs[lo:lo + n], dtype=torch.float32)
+    x = torch.tensor(xi[lo:lo + n], dtype=torch.float32)
+    g_cost, g_xi, sel = md.gather_elites(c, x, k, _stable_topk)
+    out[rank] = (g_cost[sel.long()].numpy().tolist(), g_xi[sel.long()].numpy().tolist())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["plain", "ties", "nan", "k_gt_shard"])
+def test_elite_exchange_equals_global_stable_argsort(case):
+    """gather_elites on 2 gloo ranks selects exactly the rows (in order) of the
+    single-process argsort(kind='stable')[:k], NaN last (SBP/mjx_planner.py:305-310)."""
+    rng = np.random.default_rng(4)
+    N, k = 64, 7
+    costs = rng.uniform(0, 10, N).astype(np.float32)
+    if case == "ties":
+        costs[[3, 40, 41, 10]] = -1.0  # ties across and within shards
+    if case == "nan":
+        costs[[0, 33]] = np.nan
+        costs[5] = -np.inf
+    if case == "k_gt_shard":
+        k = 40  # more elites than one shard holds
+    xi = rng.normal(size=(N, 5)).astype(np.float32)
+    xi[:, 0] = np.arange(N)  # row identity
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_elite_worker, args=(2, _free_port(), costs.tolist(), xi.tolist(), k, out), nprocs=2, join=True)
+    order = np.argsort(np.where(np.isnan(costs), np.inf, costs), kind="stable")[:k]
+    for r in range(2):
+        ec, ex = out[r]
+        np.testing.assert_array_equal(np.asarray(ex)[:, 0], order)
+        np.testing.assert_array_equal(np.asarray(ec, np.float32), costs[order])
