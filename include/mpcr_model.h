@@ -23,23 +23,29 @@ extern "C" {
 #endif
 
 #define MPCR_MODEL_MAGIC   0x4d504352u /* 'MPCR' */
-#define MPCR_MODEL_VERSION 3
+#define MPCR_MODEL_VERSION 4
 
-#define MPCR_MAX_BODY   32
-#define MPCR_MAX_JNT    24
-#define MPCR_MAX_DOF    32
-#define MPCR_MAX_NQ     40
-#define MPCR_MAX_GEOM   64
-#define MPCR_MAX_SITE   16
-#define MPCR_MAX_PAIR   256
+#define MPCR_MAX_BODY   48
+#define MPCR_MAX_JNT    40
+#define MPCR_MAX_DOF    32   /* dof bitmasks are 32-bit */
+#define MPCR_MAX_NQ     48
+#define MPCR_MAX_GEOM   128
+#define MPCR_MAX_SITE   24
+#define MPCR_MAX_PAIR   768
 #define MPCR_MAX_EQ     8
 #define MPCR_MAX_SLOT   512  /* robot-masked contact slots (cost_c) */
 #define MPCR_MAX_CTRL   8    /* planner-controlled dofs (num_dof) */
+#define MPCR_MAX_ACT    16   /* actuators */
+#define MPCR_MAX_HULLV  8192 /* convex-hull vertices of all collision meshes */
+#define MPCR_MAX_HULLA  49152 /* hull-graph adjacency entries */
 
 /* joint types (MuJoCo mjtJoint) */
 enum { MPCR_JNT_FREE = 0, MPCR_JNT_BALL = 1, MPCR_JNT_SLIDE = 2, MPCR_JNT_HINGE = 3 };
 /* geom types (MuJoCo mjtGeom order; only these collide here) */
-enum { MPCR_GEOM_PLANE = 0, MPCR_GEOM_SPHERE = 2, MPCR_GEOM_CAPSULE = 3, MPCR_GEOM_BOX = 6, MPCR_GEOM_MESH = 7 };
+enum {
+  MPCR_GEOM_PLANE = 0, MPCR_GEOM_SPHERE = 2, MPCR_GEOM_CAPSULE = 3, MPCR_GEOM_CYLINDER = 5, MPCR_GEOM_BOX = 6,
+  MPCR_GEOM_MESH = 7
+};
 /* narrow-phase functions; pair_ncon gives the contact slots each one owns */
 enum {
   MPCR_COL_PLANE_CAPSULE = 0, /* 2 slots: one per capsule end        */
@@ -51,10 +57,19 @@ enum {
   MPCR_COL_SPHERE_SPHERE = 6, /* 1 slot                              */
   MPCR_COL_SPHERE_CAPSULE = 7, /* 1 slot                             */
   MPCR_COL_SPHERE_BOX    = 8, /* 1 slot                              */
-  MPCR_COL_NTYPES        = 9
+  MPCR_COL_CONVEX        = 9, /* 1 slot: general convex pair (capsule,
+                                 cylinder, box, sphere, mesh hull) by
+                                 Minkowski portal refinement (penetration) */
+  MPCR_COL_PLANE_CONVEX  = 10, /* 1 slot: deepest support point along -n */
+  MPCR_COL_NTYPES        = 11
 };
-/* equality types */
-enum { MPCR_EQ_JOINT = 2 };
+/* equality types (mjtEq) */
+enum { MPCR_EQ_CONNECT = 0, MPCR_EQ_JOINT = 2 };
+/* integrators (mjtIntegrator) */
+enum { MPCR_INT_EULER = 0, MPCR_INT_IMPLICITFAST = 3 };
+/* actuator gain / bias types (mjtGain / mjtBias) */
+enum { MPCR_GAIN_FIXED = 0, MPCR_GAIN_AFFINE = 1 };
+enum { MPCR_BIAS_NONE = 0, MPCR_BIAS_AFFINE = 1 };
 /* disable flags (subset of mjtDisableBit semantics) */
 enum {
   MPCR_DSBL_EULERDAMP = 1 << 0,
@@ -79,8 +94,11 @@ typedef struct mpcr_model_t {
   int32_t hande_body;  /* body whose xquat is the eef rotation (-1: none)    */
   int32_t tcp_site;    /* site whose xpos is the eef position  (-1: none)    */
   int32_t iterations, ls_iterations, disableflags;
-  int32_t integrator, cone;  /* 0 = Euler, 0 = pyramidal (only these built) */
+  int32_t integrator, cone;  /* MPCR_INT_*, 0 = pyramidal (only one built)   */
   int32_t ntree;       /* kinematic trees (roots with dofs)                  */
+  int32_t nu;          /* actuators                                          */
+  int32_t nhullv, nhulla; /* convex-hull vertices / adjacency entries       */
+  int32_t pad_sz;
 
   /* options (mjOption) and statistics */
   double timestep, tolerance, ls_tolerance, impratio, meaninertia;
@@ -117,6 +135,10 @@ typedef struct mpcr_model_t {
   double jnt_solref[MPCR_MAX_JNT][2];
   double jnt_solimp[MPCR_MAX_JNT][5];
   double jnt_margin[MPCR_MAX_JNT];
+  double jnt_stiffness[MPCR_MAX_JNT];
+  double jnt_springref[MPCR_MAX_JNT];
+  int32_t jnt_actfrclimited[MPCR_MAX_JNT];
+  double jnt_actfrcrange[MPCR_MAX_JNT][2];
 
   /* dofs */
   int32_t dof_bodyid[MPCR_MAX_DOF];
@@ -171,7 +193,8 @@ typedef struct mpcr_model_t {
   int32_t eq_obj1[MPCR_MAX_EQ];
   int32_t eq_obj2[MPCR_MAX_EQ];
   int32_t pad3;
-  double eq_data[MPCR_MAX_EQ][5];
+  double eq_data[MPCR_MAX_EQ][6];  /* joint: polycoef[5]; connect: anchor in
+                                      body1 | the same point in body2 at qpos0 */
   double eq_solref[MPCR_MAX_EQ][2];
   double eq_solimp[MPCR_MAX_EQ][5];
 
@@ -179,6 +202,35 @@ typedef struct mpcr_model_t {
      (SBP/mjx_planner.py:254,267-270 use qpos[:num_dof], qvel[:num_dof]) */
   int32_t ctrl_qposadr[MPCR_MAX_CTRL];
   int32_t ctrl_dofadr[MPCR_MAX_CTRL];
+
+  /* actuators (mjModel actuator_*): joint or fixed-tendon transmissions,
+     flattened to at most 2 (dof, moment) entries; force = gain*ctrl + bias,
+     gain = gainprm[0] (+ gainprm[1] len + gainprm[2] vel if affine), bias =
+     biasprm[0] + biasprm[1] len + biasprm[2] vel, len / vel = moment . qpos /
+     qvel; ctrl is the constant actuator_ctrl (the keyframe's) */
+  int32_t act_ntrn[MPCR_MAX_ACT];
+  int32_t act_dof[MPCR_MAX_ACT][2];
+  int32_t act_qadr[MPCR_MAX_ACT][2];
+  int32_t act_gaintype[MPCR_MAX_ACT];
+  int32_t act_biastype[MPCR_MAX_ACT];
+  int32_t act_ctrllimited[MPCR_MAX_ACT];
+  int32_t act_forcelimited[MPCR_MAX_ACT];
+  int32_t pad4;
+  double act_moment[MPCR_MAX_ACT][2];
+  double act_gainprm[MPCR_MAX_ACT][3];
+  double act_biasprm[MPCR_MAX_ACT][3];
+  double act_ctrlrange[MPCR_MAX_ACT][2];
+  double act_forcerange[MPCR_MAX_ACT][2];
+  double act_ctrl[MPCR_MAX_ACT];
+
+  /* convex hulls of mesh geoms (geom frame) and their vertex graphs (the
+     neighbours of every hull vertex, for hill-climbing support queries) */
+  int32_t geom_hulladr[MPCR_MAX_GEOM];  /* first vertex, -1: no hull        */
+  int32_t geom_hullnum[MPCR_MAX_GEOM];
+  int32_t hull_adjadr[MPCR_MAX_HULLV];
+  int32_t hull_adjnum[MPCR_MAX_HULLV];
+  int32_t hull_adj[MPCR_MAX_HULLA];     /* global vertex indices            */
+  double hull_vert[MPCR_MAX_HULLV][3];
 } mpcr_model_t;
 
 #ifdef __cplusplus

@@ -11,15 +11,20 @@ import ctypes
 import numpy as np
 
 MAGIC = 0x4D504352
-VERSION = 3
+VERSION = 4
 
-MAX_BODY, MAX_JNT, MAX_DOF, MAX_NQ = 32, 24, 32, 40
-MAX_GEOM, MAX_SITE, MAX_PAIR, MAX_EQ = 64, 16, 256, 8
-MAX_SLOT, MAX_CTRL = 512, 8
+MAX_BODY, MAX_JNT, MAX_DOF, MAX_NQ = 48, 40, 32, 48
+MAX_GEOM, MAX_SITE, MAX_PAIR, MAX_EQ = 128, 24, 768, 8
+MAX_SLOT, MAX_CTRL, MAX_ACT = 512, 8, 16
+MAX_HULLV, MAX_HULLA = 8192, 49152
 
 COL_PLANE_CAPSULE, COL_PLANE_BOX, COL_CAPSULE_CAPSULE, COL_CAPSULE_BOX, COL_BOX_BOX = 0, 1, 2, 3, 4
 COL_PLANE_SPHERE, COL_SPHERE_SPHERE, COL_SPHERE_CAPSULE, COL_SPHERE_BOX = 5, 6, 7, 8
-EQ_JOINT = 2
+COL_CONVEX, COL_PLANE_CONVEX = 9, 10
+EQ_CONNECT, EQ_JOINT = 0, 2
+INT_EULER, INT_IMPLICITFAST = 0, 3
+GAIN_FIXED, GAIN_AFFINE = 0, 1
+BIAS_NONE, BIAS_AFFINE = 0, 1
 
 DSBL_EULERDAMP, DSBL_REFSAFE, DSBL_WARMSTART, DSBL_GRAVITY = 1, 2, 4, 8
 DSBL_CONTACT, DSBL_LIMIT, DSBL_EQUALITY, DSBL_PASSIVE, DSBL_FILTERPARENT = 16, 32, 64, 128, 256
@@ -40,6 +45,7 @@ class mpcr_model_t(ctypes.Structure):
         ("npair", _i), ("neq", _i), ("ncon", _i), ("nslot", _i), ("nctrl", _i),
         ("hande_body", _i), ("tcp_site", _i), ("iterations", _i), ("ls_iterations", _i),
         ("disableflags", _i), ("integrator", _i), ("cone", _i), ("ntree", _i),
+        ("nu", _i), ("nhullv", _i), ("nhulla", _i), ("pad_sz", _i),
         ("timestep", _d), ("tolerance", _d), ("ls_tolerance", _d), ("impratio", _d),
         ("meaninertia", _d), ("gravity", _a(_d, 3)), ("pad1", _d),
         ("body_parentid", _a(_i, MAX_BODY)), ("body_rootid", _a(_i, MAX_BODY)),
@@ -56,6 +62,8 @@ class mpcr_model_t(ctypes.Structure):
         ("jnt_pos", _a(_d, MAX_JNT, 3)), ("jnt_axis", _a(_d, MAX_JNT, 3)),
         ("jnt_range", _a(_d, MAX_JNT, 2)), ("jnt_solref", _a(_d, MAX_JNT, 2)),
         ("jnt_solimp", _a(_d, MAX_JNT, 5)), ("jnt_margin", _a(_d, MAX_JNT)),
+        ("jnt_stiffness", _a(_d, MAX_JNT)), ("jnt_springref", _a(_d, MAX_JNT)),
+        ("jnt_actfrclimited", _a(_i, MAX_JNT)), ("jnt_actfrcrange", _a(_d, MAX_JNT, 2)),
         ("dof_bodyid", _a(_i, MAX_DOF)), ("dof_jntid", _a(_i, MAX_DOF)),
         ("dof_parentid", _a(_i, MAX_DOF)), ("dof_treeid", _a(_i, MAX_DOF)),
         ("dof_armature", _a(_d, MAX_DOF)), ("dof_damping", _a(_d, MAX_DOF)),
@@ -76,14 +84,24 @@ class mpcr_model_t(ctypes.Structure):
         ("pair_solimp", _a(_d, MAX_PAIR, 5)), ("pair_margin", _a(_d, MAX_PAIR)),
         ("pair_gap", _a(_d, MAX_PAIR)),
         ("eq_type", _a(_i, MAX_EQ)), ("eq_obj1", _a(_i, MAX_EQ)), ("eq_obj2", _a(_i, MAX_EQ)),
-        ("pad3", _i), ("eq_data", _a(_d, MAX_EQ, 5)), ("eq_solref", _a(_d, MAX_EQ, 2)),
+        ("pad3", _i), ("eq_data", _a(_d, MAX_EQ, 6)), ("eq_solref", _a(_d, MAX_EQ, 2)),
         ("eq_solimp", _a(_d, MAX_EQ, 5)),
         ("ctrl_qposadr", _a(_i, MAX_CTRL)), ("ctrl_dofadr", _a(_i, MAX_CTRL)),
+        ("act_ntrn", _a(_i, MAX_ACT)), ("act_dof", _a(_i, MAX_ACT, 2)), ("act_qadr", _a(_i, MAX_ACT, 2)),
+        ("act_gaintype", _a(_i, MAX_ACT)), ("act_biastype", _a(_i, MAX_ACT)),
+        ("act_ctrllimited", _a(_i, MAX_ACT)), ("act_forcelimited", _a(_i, MAX_ACT)), ("pad4", _i),
+        ("act_moment", _a(_d, MAX_ACT, 2)), ("act_gainprm", _a(_d, MAX_ACT, 3)),
+        ("act_biasprm", _a(_d, MAX_ACT, 3)), ("act_ctrlrange", _a(_d, MAX_ACT, 2)),
+        ("act_forcerange", _a(_d, MAX_ACT, 2)), ("act_ctrl", _a(_d, MAX_ACT)),
+        ("geom_hulladr", _a(_i, MAX_GEOM)), ("geom_hullnum", _a(_i, MAX_GEOM)),
+        ("hull_adjadr", _a(_i, MAX_HULLV)), ("hull_adjnum", _a(_i, MAX_HULLV)),
+        ("hull_adj", _a(_i, MAX_HULLA)), ("hull_vert", _a(_d, MAX_HULLV, 3)),
     ]
 
 
 _LIMITS = dict(nbody=MAX_BODY, njnt=MAX_JNT, nv=MAX_DOF, nq=MAX_NQ, ngeom=MAX_GEOM,
-               nsite=MAX_SITE, npair=MAX_PAIR, neq=MAX_EQ, nslot=MAX_SLOT, nctrl=MAX_CTRL)
+               nsite=MAX_SITE, npair=MAX_PAIR, neq=MAX_EQ, nslot=MAX_SLOT, nctrl=MAX_CTRL, nu=MAX_ACT,
+               nhullv=MAX_HULLV, nhulla=MAX_HULLA)
 
 # struct field -> Model attribute (when the names differ)
 _ALIASES = {}
@@ -93,21 +111,19 @@ def _fill(dst, src):
     src = np.asarray(src)
     if src.size == 0:
         return
+    view = np.ctypeslib.as_array(dst)
     flat = np.ravel(src)
-    if isinstance(dst[0], ctypes.Array):
-        inner = len(dst[0])
-        rows = flat.reshape(-1, inner)
-        for r in range(rows.shape[0]):
-            for c in range(inner):
-                dst[r][c] = type(dst[r][c])(rows[r, c]) if not isinstance(dst[r][c], float) else float(rows[r, c])
-    else:
-        for k, v in enumerate(flat):
-            dst[k] = int(v) if isinstance(dst[k], int) else float(v)
+    inner = view.shape[1] if view.ndim == 2 else 1
+    if view.ndim == 2 and src.ndim == 2 and src.shape[1] != inner:
+        rows = np.zeros((src.shape[0], inner))
+        rows[:, :src.shape[1]] = src
+        flat = rows.ravel()
+    view.reshape(-1)[:flat.size] = flat.astype(view.dtype)
 
 
 def pack(m) -> mpcr_model_t:
     for k, lim in _LIMITS.items():
-        if getattr(m, k) > lim:
+        if getattr(m, k, 0) > lim:
             raise ValueError(f"model {k}={getattr(m, k)} exceeds capacity {lim}")
     s = mpcr_model_t()
     s.magic = MAGIC
@@ -116,15 +132,17 @@ def pack(m) -> mpcr_model_t:
     scalars = ("nbody", "njnt", "nq", "nv", "ngeom", "nsite", "npair", "neq", "ncon", "nslot",
                "nctrl", "hande_body", "tcp_site", "iterations", "ls_iterations", "disableflags",
                "ntree", "timestep", "tolerance", "ls_tolerance", "impratio", "meaninertia")
+    for k in ("nu", "nhullv", "nhulla", "integrator"):
+        setattr(s, k, int(getattr(m, k, 0)))
     for k in scalars:
         setattr(s, k, getattr(m, k))
-    s.integrator = 0
     s.cone = 0
     for k in range(3):
         s.gravity[k] = float(m.gravity[k])
     for name, _ in mpcr_model_t._fields_:
-        if name in scalars or name.startswith("pad") or name in ("magic", "version", "nbytes",
-                                                                 "gravity", "integrator", "cone"):
+        if name in scalars or name.startswith("pad") or name in ("magic", "version", "nbytes", "gravity",
+                                                                 "integrator", "cone", "nu", "nhullv",
+                                                                 "nhulla"):
             continue
         attr = _ALIASES.get(name, name)
         if hasattr(m, attr):

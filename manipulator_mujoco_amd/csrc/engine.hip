@@ -40,7 +40,26 @@ struct mpcr_engine {
   unsigned long long* d_key = nullptr;
   int* d_status = nullptr;
   int* d_idx = nullptr;
+  // convex hulls (dual-arm class)
+  float4* d_hull_vert = nullptr;
+  int2* d_hull_info = nullptr;
+  int* d_hull_adj = nullptr;
+  bool wide = false;  // kernel variant: rollout_kernel<32, 32, 72, true>
 };
+
+// The narrow variant (16-wide solves, 16 bodies, 24 collision geoms, Euler,
+// joint equalities only) covers the single-arm scenes; anything else runs the
+// wide one (dual-arm class).
+static bool needs_wide(const mpcr_model_t& m, const DevModel& d) {
+  if (m.nv > 16 || d.nbody > 16 || d.ngeom > 24 || m.nq > 24 || m.nu > 0 || d.has_spring ||
+      m.integrator != MPCR_INT_EULER)
+    return true;
+  for (int e = 0; e < m.neq; e++)
+    if (m.eq_type[e] != MPCR_EQ_JOINT) return true;
+  for (int p = 0; p < m.npair; p++)
+    if (m.pair_func[p] == MPCR_COL_CONVEX || m.pair_func[p] == MPCR_COL_PLANE_CONVEX) return true;
+  return false;
+}
 
 static thread_local std::string g_err;
 
@@ -79,9 +98,24 @@ static int check_model(const mpcr_model_t& m) {
   if (m.version != MPCR_MODEL_VERSION) return fail(MPCR_EMODEL, "model version %u != %d", m.version, MPCR_MODEL_VERSION);
   if (m.nbytes != sizeof(mpcr_model_t)) return fail(MPCR_EMODEL, "model size %u != %zu", m.nbytes, sizeof(mpcr_model_t));
   if (m.nbody > MPCR_MAX_BODY || m.njnt > MPCR_MAX_JNT || m.nv > MPCR_MAX_DOF || m.nq > MPCR_MAX_NQ ||
-      m.ngeom > MPCR_MAX_GEOM || m.npair > MPCR_MAX_PAIR || m.neq > MPCR_MAX_EQ || m.nctrl > MPCR_MAX_CTRL)
+      m.ngeom > MPCR_MAX_GEOM || m.npair > MPCR_MAX_PAIR || m.neq > MPCR_MAX_EQ || m.nctrl > MPCR_MAX_CTRL ||
+      m.nu > MPCR_MAX_ACT || m.nhullv > MPCR_MAX_HULLV || m.nhulla > MPCR_MAX_HULLA || m.nu < 0 || m.nhullv < 0 ||
+      m.nhulla < 0)
     return fail(MPCR_EMODEL, "model exceeds blob capacity");
-  if (m.integrator != 0 || m.cone != 0) return fail(MPCR_EMODEL, "only Euler + pyramidal supported");
+  if ((m.integrator != MPCR_INT_EULER && m.integrator != MPCR_INT_IMPLICITFAST) || m.cone != 0)
+    return fail(MPCR_EMODEL, "only Euler / implicitfast with pyramidal cones supported");
+  for (int g = 0; g < m.ngeom; g++)
+    if (m.geom_hulladr[g] >= 0 && m.geom_hulladr[g] + m.geom_hullnum[g] > m.nhullv)
+      return fail(MPCR_EMODEL, "geom %d hull outside the vertex table", g);
+  for (int v = 0; v < m.nhullv; v++)
+    if (m.hull_adjadr[v] < 0 || m.hull_adjadr[v] + m.hull_adjnum[v] > m.nhulla)
+      return fail(MPCR_EMODEL, "hull vertex %d adjacency outside the table", v);
+  for (int k = 0; k < m.nhulla; k++)
+    if (m.hull_adj[k] < 0 || m.hull_adj[k] >= m.nhullv) return fail(MPCR_EMODEL, "bad hull adjacency entry");
+  for (int p = 0; p < m.npair; p++)
+    for (int g : {m.pair_geom1[p], m.pair_geom2[p]})
+      if (m.geom_type[g] == MPCR_GEOM_MESH && m.geom_hulladr[g] < 0)
+        return fail(MPCR_EMODEL, "mesh geom %d in a pair has no convex hull", g);
   return MPCR_OK;
 }
 
@@ -309,7 +343,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
   for (int p = 0; p < m.npair; p++)
     for (int g : {m.pair_geom1[p], m.pair_geom2[p]})
       if (gmap[g] < 0) gmap[g] = ng++;
-  if (ng > DX_NG) return fail(MPCR_EMODEL, "%d collision geoms > %d", ng, DX_NG);
+  if (ng > DX_NG || ng > WAVE) return fail(MPCR_EMODEL, "%d collision geoms > %d", ng, DX_NG < WAVE ? DX_NG : WAVE);
   d.ngeom = ng;
   for (int g = 0; g < m.ngeom; g++) {
     int i = gmap[g];
@@ -317,6 +351,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     int b = m.geom_bodyid[g];
     d.geom_type[i] = m.geom_type[g];
     d.geom_rbound[i] = (float)m.geom_rbound[g];
+    d.geom_hulladr[i] = m.geom_hulladr[g];
     for (int k = 0; k < 3; k++) d.geom_size[i][k] = (float)m.geom_size[g][k];
     if (dmap[b] >= 0) {
       d.geom_body[i] = dmap[b];
@@ -351,16 +386,101 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     for (int k = 0; k < 5; k++) d.pair_solimp[p][k] = (float)m.pair_solimp[p][k];
     d.pair_diag[p] = (float)(m.body_invweight0[m.geom_bodyid[g1]][0] + m.body_invweight0[m.geom_bodyid[g2]][0]);
   }
-  // equalities
+  // equalities: joint (1 row) and connect (3 rows), rows in model order
+  int nrow = 0;
   for (int e = 0; e < m.neq; e++) {
-    if (m.eq_type[e] != MPCR_EQ_JOINT) return fail(MPCR_EMODEL, "only joint equalities supported");
-    d.eq_j1[e] = m.eq_obj1[e];
-    d.eq_j2[e] = m.eq_obj2[e];
-    for (int k = 0; k < 5; k++) { d.eq_data[e][k] = (float)m.eq_data[e][k]; d.eq_solimp[e][k] = (float)m.eq_solimp[e][k]; }
+    d.eq_type[e] = m.eq_type[e];
+    for (int k = 0; k < 5; k++) d.eq_solimp[e][k] = (float)m.eq_solimp[e][k];
     for (int k = 0; k < 2; k++) d.eq_solref[e][k] = (float)m.eq_solref[e][k];
-    double diag = m.dof_invweight0[m.jnt_dofadr[m.eq_obj1[e]]];
-    if (m.eq_obj2[e] >= 0) diag += m.dof_invweight0[m.jnt_dofadr[m.eq_obj2[e]]];
-    d.eq_diag[e] = (float)diag;
+    if (m.eq_type[e] == MPCR_EQ_JOINT) {
+      d.eq_j1[e] = m.eq_obj1[e];
+      d.eq_j2[e] = m.eq_obj2[e];
+      for (int k = 0; k < 5; k++) d.eq_data[e][k] = (float)m.eq_data[e][k];
+      double diag = m.dof_invweight0[m.jnt_dofadr[m.eq_obj1[e]]];
+      if (m.eq_obj2[e] >= 0) diag += m.dof_invweight0[m.jnt_dofadr[m.eq_obj2[e]]];
+      d.eq_diag[e] = (float)diag;
+      if (nrow + 1 > DX_NEQROW) return fail(MPCR_EMODEL, "too many equality rows");
+      d.eqrow_eq[nrow] = e; d.eqrow_k[nrow] = 0; nrow++;
+    } else if (m.eq_type[e] == MPCR_EQ_CONNECT) {
+      for (int side = 0; side < 2; side++) {
+        int b = side ? m.eq_obj2[e] : m.eq_obj1[e];
+        const double* a = m.eq_data[e] + 3 * side;
+        int db = b > 0 ? dmap[b] : -1;
+        (side ? d.eq_b2 : d.eq_b1)[e] = db;
+        double pw[3] = {a[0], a[1], a[2]};
+        if (db < 0) {  // static body: anchor in world once
+          double r[3];
+          h_rot(r, &wquat[4 * b], a);
+          for (int k = 0; k < 3; k++) pw[k] = wpos[3 * b + k] + r[k];
+        }
+        for (int k = 0; k < 3; k++) d.eq_data[e][4 * side + k] = (float)pw[k];
+      }
+      d.eq_diag[e] = (float)(m.body_invweight0[m.eq_obj1[e]][0] + m.body_invweight0[m.eq_obj2[e]][0]);
+      if (nrow + 3 > DX_NEQROW) return fail(MPCR_EMODEL, "too many equality rows");
+      for (int k = 0; k < 3; k++) { d.eqrow_eq[nrow] = e; d.eqrow_k[nrow] = k + 1; nrow++; }
+    } else {
+      return fail(MPCR_EMODEL, "equality type %d not supported (joint, connect)", m.eq_type[e]);
+    }
+  }
+  d.neqrow = nrow;
+  // springs
+  for (int i = 0; i < m.nv; i++) {
+    int j = m.dof_jntid[i];
+    d.dof_qposadr[i] = m.jnt_qposadr[j];
+    if (!no_passive && (m.jnt_type[j] == MPCR_JNT_HINGE || m.jnt_type[j] == MPCR_JNT_SLIDE) &&
+        m.jnt_stiffness[j] != 0) {
+      d.dof_stiffness[i] = (float)m.jnt_stiffness[j];
+      d.dof_springref[i] = (float)m.jnt_springref[j];
+      d.has_spring = 1;
+    }
+    d.dof_actfrc[i][0] = -3e38f;
+    d.dof_actfrc[i][1] = 3e38f;
+    if (m.jnt_actfrclimited[j]) {
+      d.dof_actfrc[i][0] = (float)m.jnt_actfrcrange[j][0];
+      d.dof_actfrc[i][1] = (float)m.jnt_actfrcrange[j][1];
+    }
+  }
+  // actuators (ctrl constant: clamped once here)
+  if (m.nu > DX_NU) return fail(MPCR_EMODEL, "%d actuators > %d", m.nu, DX_NU);
+  d.nu = m.nu;
+  for (int a = 0; a < m.nu; a++) {
+    d.act_ntrn[a] = m.act_ntrn[a];
+    for (int k = 0; k < m.act_ntrn[a]; k++) {
+      int v = m.act_dof[a][k];
+      d.act_dof[a][k] = v;
+      d.act_qadr[a][k] = m.act_qadr[a][k];
+      d.act_moment[a][k] = (float)m.act_moment[a][k];
+      if (d.dof_actn[v] >= 2) return fail(MPCR_EMODEL, "more than 2 actuators on dof %d", v);
+      d.dof_acta[v][d.dof_actn[v]] = a;
+      d.dof_actm[v][d.dof_actn[v]] = (float)m.act_moment[a][k];
+      d.dof_actn[v]++;
+    }
+    double ctrl = m.act_ctrl[a];
+    if (m.act_ctrllimited[a]) ctrl = std::fmin(std::fmax(ctrl, m.act_ctrlrange[a][0]), m.act_ctrlrange[a][1]);
+    d.act_gaffine[a] = m.act_gaintype[a] == MPCR_GAIN_AFFINE;
+    d.act_baffine[a] = m.act_biastype[a] == MPCR_BIAS_AFFINE;
+    for (int k = 0; k < 3; k++) { d.act_gain[a][k] = (float)m.act_gainprm[a][k]; d.act_bias[a][k] = (float)m.act_biasprm[a][k]; }
+    d.act_gain[a][3] = (float)ctrl;
+    d.act_frc[a][0] = m.act_forcelimited[a] ? (float)m.act_forcerange[a][0] : -3e38f;
+    d.act_frc[a][1] = m.act_forcelimited[a] ? (float)m.act_forcerange[a][1] : 3e38f;
+  }
+  // implicitfast: D = -qDeriv = damping + sum_a (-dforce/dvel) m m^T (fp64, then rounded)
+  d.integrator = m.integrator;
+  if (m.integrator == MPCR_INT_IMPLICITFAST) {
+    std::vector<double> D((size_t)m.nv * m.nv, 0.0);
+    for (int i = 0; i < m.nv; i++) D[(size_t)i * m.nv + i] = no_passive ? 0.0 : m.dof_damping[i];
+    for (int a = 0; a < m.nu; a++) {
+      double dv = 0;
+      if (m.act_biastype[a] == MPCR_BIAS_AFFINE) dv += m.act_biasprm[a][2];
+      if (m.act_gaintype[a] == MPCR_GAIN_AFFINE) dv += m.act_gainprm[a][2] * (double)d.act_gain[a][3];
+      for (int k = 0; k < m.act_ntrn[a]; k++)
+        for (int l = 0; l < m.act_ntrn[a]; l++)
+          D[(size_t)m.act_dof[a][k] * m.nv + m.act_dof[a][l]] -= dv * m.act_moment[a][k] * m.act_moment[a][l];
+    }
+    for (int i = 0; i < m.nv; i++)
+      for (int j = 0; j < m.nv; j++) d.impl_D[i][j] = (float)D[(size_t)i * m.nv + j];
+  } else if (m.integrator != MPCR_INT_EULER) {
+    return fail(MPCR_EMODEL, "integrator %d not supported (Euler, implicitfast)", m.integrator);
   }
   // planner ids
   d.hande_body = m.hande_body >= 0 ? dmap[m.hande_body] : -1;
@@ -396,6 +516,29 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
   e->host = m->m;
   int rc = build_dev_model(e->host, e->dev);
   if (rc) { delete e; return rc; }
+  e->wide = needs_wide(e->host, e->dev);
+  if (e->host.nhullv > 0) {  // hull vertices (float4) + graph, pointed to by the device model
+    const mpcr_model_t& h = e->host;
+    std::vector<float4> hv(h.nhullv);
+    std::vector<int2> hi(h.nhullv);
+    std::vector<int> ha(h.hull_adj, h.hull_adj + h.nhulla);
+    for (int v = 0; v < h.nhullv; v++) {
+      hv[v] = make_float4((float)h.hull_vert[v][0], (float)h.hull_vert[v][1], (float)h.hull_vert[v][2], 0.f);
+      hi[v] = make_int2(h.hull_adjadr[v], h.hull_adjnum[v]);
+    }
+    if (hipMalloc(&e->d_hull_vert, sizeof(float4) * hv.size()) != hipSuccess ||
+        hipMalloc(&e->d_hull_info, sizeof(int2) * hi.size()) != hipSuccess ||
+        hipMalloc(&e->d_hull_adj, sizeof(int) * (ha.size() ? ha.size() : 1)) != hipSuccess ||
+        hipMemcpy(e->d_hull_vert, hv.data(), sizeof(float4) * hv.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_hull_info, hi.data(), sizeof(int2) * hi.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        (ha.size() && hipMemcpy(e->d_hull_adj, ha.data(), sizeof(int) * ha.size(), hipMemcpyHostToDevice) != hipSuccess)) {
+      mpcr_engine_free(e);
+      return fail(MPCR_ENOMEM, "hull upload failed");
+    }
+    e->dev.hull_vert = e->d_hull_vert;
+    e->dev.hull_info = e->d_hull_info;
+    e->dev.hull_adj = e->d_hull_adj;
+  }
   const int nc = e->host.nctrl;
   const size_t in_cols = (size_t)nc * (horizon > nbasis ? horizon : nbasis);
   if (hipMalloc(&e->d_model, sizeof(DevModel)) != hipSuccess ||
@@ -430,6 +573,9 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_key);
   (void)hipFree(e->d_status);
   (void)hipFree(e->d_idx);
+  (void)hipFree(e->d_hull_vert);
+  (void)hipFree(e->d_hull_info);
+  (void)hipFree(e->d_hull_adj);
   delete e;
 }
 
@@ -477,7 +623,10 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.index_base = l.index_base;
   std::memcpy(a.par, l.par, sizeof(a.par));
   if (l.key && l.reset_key) hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, l.key, ~0ull);
-  hipLaunchKernelGGL(rollout_kernel, dim3(l.n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
+  if (e->wide)
+    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(l.n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
+  else
+    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(l.n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
   HIPCHK(hipGetLastError());
   return MPCR_OK;
 }
@@ -700,7 +849,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
-  hipLaunchKernelGGL(rollout_kernel, dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
+  hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(phases16, d_prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(d_prof);

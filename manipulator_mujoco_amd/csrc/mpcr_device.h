@@ -9,13 +9,17 @@
 namespace mpcr {
 
 constexpr int WAVE = 64;
-constexpr int DX_NB = 16;    // moving bodies
-constexpr int DX_NV = 16;    // dofs (padded register width of the dense solves)
-constexpr int DX_NQ = 24;
-constexpr int DX_NJ = 16;
-constexpr int DX_NG = 24;    // collision geoms (remapped)
-constexpr int DX_NP = 256;   // pairs
-constexpr int DX_NEQ = 4;
+// capacities of the device model (the kernel variants size their LDS by
+// their own widths, rollout.hip SmemT)
+constexpr int DX_NB = 32;    // moving bodies (32-bit subtree masks)
+constexpr int DX_NV = 32;    // dofs (32-bit dof masks; widest dense solve)
+constexpr int DX_NQ = 32;
+constexpr int DX_NJ = 32;
+constexpr int DX_NG = 72;    // collision geoms (remapped)
+constexpr int DX_NP = 768;   // pairs
+constexpr int DX_NEQ = 8;
+constexpr int DX_NEQROW = 24;  // equality constraint rows (joint 1, connect 3)
+constexpr int DX_NU = 16;    // actuators
 constexpr int DX_NCTRL = 8;
 constexpr int DX_NTREE = 4;
 constexpr int DX_MAXACT = 20;  // active contacts kept per step
@@ -30,7 +34,8 @@ struct DevModel {
   int nctrl, ntree, hande_body, tcp_body;
   int iterations, ls_iterations, disableflags, jump_rounds;
   int nhdof;  // number of dofs, rounded to the solve width
-  int pad_[3];
+  int nu, neqrow, integrator;  // actuators, equality rows, 0 Euler / 3 implicitfast
+  int has_spring;
   float timestep, tolerance, ls_tolerance, meaninertia;
   float gravity[4];
   float tcp_pos[4];  // tcp site position in tcp_body frame
@@ -79,9 +84,32 @@ struct DevModel {
   float pair_solref[DX_NP][2], pair_solimp[DX_NP][5];
   float pair_diag[DX_NP];        // tran invweight of the two bodies
 
-  // joint equalities ------------------------------------------------------
-  int eq_j1[DX_NEQ], eq_j2[DX_NEQ];
-  float eq_data[DX_NEQ][5], eq_solref[DX_NEQ][2], eq_solimp[DX_NEQ][5], eq_diag[DX_NEQ];
+  // equalities: joint (eq_j1/j2, polycoef in eq_data) and connect (moving
+  // bodies eq_b1/b2 or -1 for a static body, whose anchor eq_data[4*side..]
+  // is then already in world coordinates) -----------------------------------
+  int eq_type[DX_NEQ], eq_j1[DX_NEQ], eq_j2[DX_NEQ], eq_b1[DX_NEQ], eq_b2[DX_NEQ];
+  float eq_data[DX_NEQ][8], eq_solref[DX_NEQ][2], eq_solimp[DX_NEQ][5], eq_diag[DX_NEQ];
+  int eqrow_eq[DX_NEQROW], eqrow_k[DX_NEQROW];  // row -> (equality, component)
+
+  // passive springs and actuation per dof --------------------------------------
+  float dof_stiffness[DX_NV], dof_springref[DX_NV];
+  int dof_qposadr[DX_NV];
+  int dof_actn[DX_NV], dof_acta[DX_NV][2];  // actuators driving this dof
+  float dof_actm[DX_NV][2];                  // their moments on it
+  float dof_actfrc[DX_NV][2];                // joint-level actuator force range
+  // actuators: force = gain * ctrl + bias, gain = g0 (+ g1 len + g2 vel),
+  // bias = b0 + b1 len + b2 vel, clamped to act_frc
+  int act_ntrn[DX_NU], act_qadr[DX_NU][2], act_dof[DX_NU][2], act_gaffine[DX_NU], act_baffine[DX_NU];
+  float act_moment[DX_NU][2], act_gain[DX_NU][4], act_bias[DX_NU][4], act_frc[DX_NU][2];
+  // implicitfast: D = -qDeriv (damping + actuator velocity derivatives), the
+  // integrator solves (M + dt D) qacc = qfrc_smooth + qfrc_constraint
+  float impl_D[DX_NV][DX_NV];
+
+  // convex hulls of mesh geoms (geom frame), hill-climbing graph -----------------
+  int geom_hulladr[DX_NG];
+  const float4* hull_vert;  // xyz, w unused
+  const int2* hull_info;    // (adjacency start, count) per vertex
+  const int* hull_adj;
 
   int ctrl_qposadr[DX_NCTRL], ctrl_dofadr[DX_NCTRL];
 };

@@ -52,46 +52,51 @@ struct RolloutArgs {
   float par[PAR_N];  // q0[8] | w[4] | ptgt[4] | qtgt[4] (any norm)
 };
 
-// Row stride 20 floats (80 B): rows are 16-byte aligned for ds_read_b128 and
-// a 16-lane ds_read_b128 group touching 16 different rows covers all 64
-// banks exactly once (20*r mod 64 are distinct multiples of 4) -> conflict
-// free for row-parallel access, 4x fewer LDS instructions than b32.
-constexpr int LDM = 20;
-constexpr int LDJ = 20;
-constexpr int LDL = 20;
-
-struct __align__(16) Smem {
+// Per-block LDS image, sized by the kernel variant: NVW = dense-solve width
+// (16 or 32 dofs), NBW = moving bodies, NGW = collision geoms.  Row stride
+// LD = NVW + 4 floats: rows are 16-byte aligned for ds_read_b128 and 16 lanes
+// reading 16 different rows hit distinct bank quads (LD*r mod 64 distinct
+// multiples of 4 for LD = 20 and 36) -> conflict free, 4x fewer LDS
+// instructions than b32.
+template <int NVW_, int NBW_, int NGW_>
+struct __align__(16) SmemT {
+  static constexpr int NVW = NVW_, NBW = NBW_, NGW = NGW_, LD = NVW_ + 4;
+  static constexpr int LOG_NVW = NVW_ == 32 ? 5 : 4;
+  static constexpr bool WIDE = NVW_ == 32;  // dual-arm class: equalities, actuators, convex hulls
+  static constexpr int NQW = WIDE ? DX_NQ : 24, NEQP = WIDE ? DX_NEQ : 1, NACT = WIDE ? DX_NU : 1;
   // ---- persistent across the step ----
   float xi[DX_NCTRL * 16];
-  float qpos[DX_NQ];
-  alignas(16) float qvel[DX_NV];
-  alignas(16) float qacc[DX_NV];
-  alignas(16) float qws[DX_NV];
-  alignas(16) float qfs[DX_NV];   // qfrc_smooth
-  alignas(16) float qas[DX_NV];   // qacc_smooth
-  alignas(16) float srch[DX_NV];  // Newton search direction
+  float qpos[NQW];
+  alignas(16) float qvel[NVW];
+  alignas(16) float qacc[NVW];
+  alignas(16) float qws[NVW];
+  alignas(16) float qfs[NVW];   // qfrc_smooth
+  alignas(16) float qas[NVW];   // qacc_smooth
+  alignas(16) float srch[NVW];  // Newton search direction
   float com[DX_NTREE][4];
-  float cdof[DX_NV][8];
-  alignas(16) float M[DX_NV][LDM];
-  alignas(16) float gxpos[DX_NG][4];   // gxpos+gxmat (dead during Newton) double as the
-  float gxmat[DX_NG][12];  // Hessian solve's LDS scratch
+  float cdof[NVW][8];
+  alignas(16) float M[NVW][LD];
+  alignas(16) float gxpos[NGW][4];   // gxpos+gxmat (dead during Newton) double as the
+  float gxmat[NGW][12];  // Hessian solve's LDS scratch (NGW*16 >= NVW*LD)
   float cprev[DX_NSLOT];  // previous-step masked slot distances (cost_c)
   float par[PAR_N];       // q0 | w | ptgt | qtgt (normalised)
+  float eqp[NEQP][2][4];  // connect anchors in world (body1, body2)
+  float actf[NACT];       // actuator forces
   int ncon, nefc, pad_[2];
   // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the
   //      contact / constraint arrays (collision .. Newton) ----
   union {
     struct {
-      alignas(16) float xpos[DX_NB][4];
-      float xquat[DX_NB][4];
-      float xmat[DX_NB][12];
-      float xipos[DX_NB][4];
-      float cinert[DX_NB][12];
-      float crb[DX_NB][12];
-      float cvel[DX_NB][8];
-      float cfrc[DX_NB][8];
-      float cdofdot[DX_NV][8];
-      float fvec[DX_NV][8];
+      alignas(16) float xpos[NBW][4];
+      float xquat[NBW][4];
+      float xmat[NBW][12];
+      float xipos[NBW][4];
+      float cinert[NBW][12];
+      float crb[NBW][12];
+      float cvel[NBW][8];
+      float cfrc[NBW][8];
+      float cdofdot[NVW][8];
+      float fvec[NVW][8];
     };
     struct {
       float con_pos[DX_MAXACT][4];
@@ -100,7 +105,7 @@ struct __align__(16) Smem {
       int con_pair[DX_MAXACT];
       int con_row[DX_MAXACT];
       float poly[2][8][4];  // box-box clipping polygon (double buffered)
-      alignas(16) float J[DX_MAXEFC][LDJ];
+      alignas(16) float J[DX_MAXEFC][LD];
       float efc_D[DX_MAXEFC];
       float efc_aref[DX_MAXEFC];
       float efc_jar[DX_MAXEFC];
@@ -111,6 +116,11 @@ struct __align__(16) Smem {
     };
   };
 };
+// the two variants: single-arm scenes (nv <= 16) and the dual-arm class
+using SmemN = SmemT<16, 16, 24>;
+using SmemW = SmemT<32, 32, 72>;
+static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
+static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 
 // ---------------------------------------------------------------------------
 // diagnostic phase stamps (separate -DMPCR_PROFILE build; never in the timed one)
@@ -206,13 +216,14 @@ __device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
 }
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
-// 16-wide dot product of an LDS row (16-byte aligned) with an LDS vector
-__device__ __forceinline__ float dot16(const float* row, const float* vec) {
+// N-wide dot product of an LDS row (16-byte aligned) with an LDS vector
+template <int N>
+__device__ __forceinline__ float dotN(const float* row, const float* vec) {
   const float4* r = reinterpret_cast<const float4*>(row);
   const float4* v = reinterpret_cast<const float4*>(vec);
   float acc = 0.f;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
+  for (int q = 0; q < N / 4; q++) {
     const float4 a = r[q], x = v[q];
     acc = fmaf(a.x, x.x, acc); acc = fmaf(a.y, x.y, acc); acc = fmaf(a.z, x.z, acc); acc = fmaf(a.w, x.w, acc);
   }
@@ -253,14 +264,15 @@ __device__ __forceinline__ void cross_force(float r[6], const float v[6], const 
 // All DX_NV pivots run even when nv is smaller: a run-time exit inside the
 // unrolled chain breaks it into blocks the scheduler cannot overlap
 // (measured 4.07 -> 4.94 ms), while the padded pivots cost 2/16 of it.
-__device__ __forceinline__ void chol_rows(float (&a)[DX_NV], int lane) {
+template <int N>
+__device__ __forceinline__ void chol_rows(float (&a)[N], int lane) {
 #pragma unroll
-  for (int k = 0; k < DX_NV; k++) {
+  for (int k = 0; k < N; k++) {
     float dkk = sqrtf(fmaxf(rdlane(a[k], k), kMinVal));
     float lik = lane == k ? dkk : (lane > k ? a[k] / dkk : 0.f);
     a[k] = lik;
 #pragma unroll
-    for (int j = k + 1; j < DX_NV; j++) {
+    for (int j = k + 1; j < N; j++) {
       float ljk = rdlane(lik, j);
       a[j] = fmaf(-lik, ljk, a[j]);
     }
@@ -274,24 +286,25 @@ __device__ __forceinline__ void chol_rows(float (&a)[DX_NV], int lane) {
 // Lt[DX_NV][LDL] once, each lane reads its column back with 4 ds_read_b128,
 // and the same broadcast chain runs backwards.  32 readlanes per solve.
 // Returns x[lane].  Must be called by all lanes (one barrier).
-__device__ __forceinline__ float chol_solve(const float (&l)[DX_NV], float b, int lane, float* Lt) {
-  if (lane < DX_NV) {
+template <int N, int LDL>
+__device__ __forceinline__ float chol_solve(const float (&l)[N], float b, int lane, float* Lt) {
+  if (lane < N) {
 #pragma unroll
-    for (int j = 0; j < DX_NV; j++) Lt[j * LDL + lane] = l[j];
+    for (int j = 0; j < N; j++) Lt[j * LDL + lane] = l[j];
   }
   float acc = b, y = 0.f;
 #pragma unroll
-  for (int k = 0; k < DX_NV; k++) {
+  for (int k = 0; k < N; k++) {
     const float yk = rdlane(acc, k) / rdlane(l[k], k);
     if (lane > k) acc = fmaf(-l[k], yk, acc);
     if (lane == k) y = yk;
   }
   sync();
-  float lt[DX_NV];
+  float lt[N];
   {
-    const float4* col = reinterpret_cast<const float4*>(Lt + (lane < DX_NV ? lane : 0) * LDL);
+    const float4* col = reinterpret_cast<const float4*>(Lt + (lane < N ? lane : 0) * LDL);
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < N / 4; q++) {
       const float4 v = col[q];
       lt[4 * q] = v.x; lt[4 * q + 1] = v.y; lt[4 * q + 2] = v.z; lt[4 * q + 3] = v.w;
     }
@@ -299,7 +312,7 @@ __device__ __forceinline__ float chol_solve(const float (&l)[DX_NV], float b, in
   float x = 0.f;
   acc = y;
 #pragma unroll
-  for (int k = DX_NV - 1; k >= 0; k--) {
+  for (int k = N - 1; k >= 0; k--) {
     const float xk = rdlane(acc, k) / rdlane(l[k], k);
     if (lane < k) acc = fmaf(-lt[k], xk, acc);
     if (lane == k) x = xk;
@@ -363,9 +376,240 @@ __device__ __forceinline__ float point_box(const float p[3], const float h[3], f
   return g;
 }
 
+// ---------------------------------------------------------------------------
+// general convex narrow phase (dual-arm class only): support functions of
+// sphere / capsule / cylinder / box / mesh convex hull and Minkowski portal
+// refinement, the same algorithm and tolerances as the oracle's mpr()
+// (libccd MPR; one penetration contact per pair)
+
+constexpr float kMprTol = 1e-6f;
+constexpr int kMprIter = 50;
+constexpr float kMprEps = 1.1920929e-07f;
+__device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
+
+template <class S>
+__device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
+                                             float out[3]) {
+  const float* R = s.gxmat[g];
+  const float* sz = m->geom_size[g];
+  float l[3], p[3] = {0.f, 0.f, 0.f};
+  mtv(l, R, dir);
+  const int type = m->geom_type[g];
+  if (type == 2 || type == 3) {  // sphere, capsule
+    const float n = sqrtf(dot3(l, l));
+    if (n > 0.f) { p[0] = sz[0] * l[0] / n; p[1] = sz[0] * l[1] / n; p[2] = sz[0] * l[2] / n; }
+    if (type == 3) p[2] += l[2] >= 0.f ? sz[1] : -sz[1];
+  } else if (type == 5) {  // cylinder
+    const float r = sqrtf(l[0] * l[0] + l[1] * l[1]);
+    if (r > 0.f) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
+    p[2] = l[2] >= 0.f ? sz[1] : -sz[1];
+  } else if (type == 6) {  // box
+    p[0] = l[0] >= 0.f ? sz[0] : -sz[0];
+    p[1] = l[1] >= 0.f ? sz[1] : -sz[1];
+    p[2] = l[2] >= 0.f ? sz[2] : -sz[2];
+  } else if (type == 7) {  // mesh hull: steepest ascent on the vertex graph from its first vertex
+    int v = m->geom_hulladr[g];
+    float4 hv = m->hull_vert[v];
+    float best = hv.x * l[0] + hv.y * l[1] + hv.z * l[2];
+    for (int guard = 0; guard < 4096; guard++) {
+      const int2 info = m->hull_info[v];
+      int nb = v;
+      for (int k = info.x; k < info.x + info.y; k++) {
+        const int u = m->hull_adj[k];
+        const float4 w = m->hull_vert[u];
+        const float du = w.x * l[0] + w.y * l[1] + w.z * l[2];
+        if (du > best) { best = du; nb = u; }
+      }
+      if (nb == v) break;
+      v = nb;
+    }
+    hv = m->hull_vert[v];
+    p[0] = hv.x; p[1] = hv.y; p[2] = hv.z;
+  }
+  mv(out, R, p);
+  out[0] += s.gxpos[g][0]; out[1] += s.gxpos[g][1]; out[2] += s.gxpos[g][2];
+}
+
+struct MprPt { float v[3], a[3], b[3]; };
+
+template <class S>
+__device__ __forceinline__ void mpr_support(const DevModel* __restrict__ m, const S& s, int g1, int g2,
+                                            const float dir[3], MprPt& o) {
+  const float nd[3] = {-dir[0], -dir[1], -dir[2]};
+  support_geom(m, s, g1, dir, o.a);
+  support_geom(m, s, g2, nd, o.b);
+  o.v[0] = o.a[0] - o.b[0]; o.v[1] = o.a[1] - o.b[1]; o.v[2] = o.a[2] - o.b[2];
+}
+__device__ __forceinline__ void nrm3(float v[3]) {
+  const float n = sqrtf(dot3(v, v));
+  if (n > 0.f) { v[0] /= n; v[1] /= n; v[2] /= n; }
+}
+__device__ __forceinline__ void mpr_dir(const MprPt p[4], float dir[3]) {
+  float a[3] = {p[2].v[0] - p[1].v[0], p[2].v[1] - p[1].v[1], p[2].v[2] - p[1].v[2]};
+  float b[3] = {p[3].v[0] - p[1].v[0], p[3].v[1] - p[1].v[1], p[3].v[2] - p[1].v[2]};
+  cross(dir, a, b);
+  nrm3(dir);
+}
+__device__ __forceinline__ bool mpr_reach(const MprPt p[4], const MprPt& v4, const float dir[3]) {
+  const float d4 = dot3(v4.v, dir);
+  const float t = fminf(d4 - dot3(p[1].v, dir), fminf(d4 - dot3(p[2].v, dir), d4 - dot3(p[3].v, dir)));
+  return fabsf(t - kMprTol) < kMprEps || t < kMprTol;
+}
+__device__ __forceinline__ void mpr_expand(MprPt p[4], const MprPt& v4) {
+  float x[3];
+  cross(x, v4.v, p[0].v);
+  if (dot3(p[1].v, x) > 0.f) {
+    if (dot3(p[2].v, x) > 0.f) p[1] = v4; else p[3] = v4;
+  } else {
+    if (dot3(p[3].v, x) > 0.f) p[2] = v4; else p[1] = v4;
+  }
+}
+__device__ __forceinline__ void tri_closest(const float a[3], const float b[3], const float c[3], float out[3]) {
+  float ab[3], ac[3], ap[3], bp[3], cp[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; ap[k] = -a[k]; bp[k] = -b[k]; cp[k] = -c[k]; }
+  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0.f && d2 <= 0.f) { out[0] = a[0]; out[1] = a[1]; out[2] = a[2]; return; }
+  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0.f && d4 <= d3) { out[0] = b[0]; out[1] = b[1]; out[2] = b[2]; return; }
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+    const float t = d1 / (d1 - d3);
+    out[0] = a[0] + t * ab[0]; out[1] = a[1] + t * ab[1]; out[2] = a[2] + t * ab[2];
+    return;
+  }
+  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0.f && d5 <= d6) { out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; return; }
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+    const float t = d2 / (d2 - d6);
+    out[0] = a[0] + t * ac[0]; out[1] = a[1] + t * ac[1]; out[2] = a[2] + t * ac[2];
+    return;
+  }
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+    const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+#pragma unroll
+    for (int k = 0; k < 3; k++) out[k] = b[k] + t * (c[k] - b[k]);
+    return;
+  }
+  const float den = 1.f / (va + vb + vc), v = vb * den, w = vc * den;
+#pragma unroll
+  for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
+}
+
+// returns true and (depth, dir g1 -> g2, pos) when the geoms overlap
+template <class S>
+__device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int g2, float& depth, float dir[3],
+                         float pos[3]) {
+  MprPt p[4], v4;
+  float va[3], vb[3], dd;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    p[0].a[k] = s.gxpos[g1][k];
+    p[0].b[k] = s.gxpos[g2][k];
+    p[0].v[k] = p[0].a[k] - p[0].b[k];
+  }
+  if (mpr_zero(p[0].v[0]) && mpr_zero(p[0].v[1]) && mpr_zero(p[0].v[2])) p[0].v[0] += 10.f * kMprEps;
+  dir[0] = -p[0].v[0]; dir[1] = -p[0].v[1]; dir[2] = -p[0].v[2];
+  nrm3(dir);
+  mpr_support(m, s, g1, g2, dir, p[1]);
+  dd = dot3(p[1].v, dir);
+  if (mpr_zero(dd) || dd < 0.f) return false;
+  cross(dir, p[0].v, p[1].v);
+  if (mpr_zero(dot3(dir, dir))) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].a[k] + p[1].b[k]);
+    if (mpr_zero(p[1].v[0]) && mpr_zero(p[1].v[1]) && mpr_zero(p[1].v[2])) {
+      depth = 0.f;
+      dir[0] = dir[1] = dir[2] = 0.f;
+    } else {
+      dir[0] = p[1].v[0]; dir[1] = p[1].v[1]; dir[2] = p[1].v[2];
+      depth = sqrtf(dot3(dir, dir));
+      nrm3(dir);
+    }
+    return true;
+  }
+  nrm3(dir);
+  mpr_support(m, s, g1, g2, dir, p[2]);
+  dd = dot3(p[2].v, dir);
+  if (mpr_zero(dd) || dd < 0.f) return false;
+#pragma unroll
+  for (int k = 0; k < 3; k++) { va[k] = p[1].v[k] - p[0].v[k]; vb[k] = p[2].v[k] - p[0].v[k]; }
+  cross(dir, va, vb);
+  nrm3(dir);
+  if (dot3(dir, p[0].v) > 0.f) {
+    const MprPt t = p[1]; p[1] = p[2]; p[2] = t;
+    dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
+  }
+  for (int guard = 0;; guard++) {
+    if (guard > kMprIter) return false;
+    mpr_support(m, s, g1, g2, dir, p[3]);
+    dd = dot3(p[3].v, dir);
+    if (mpr_zero(dd) || dd < 0.f) return false;
+    bool cont = false;
+    cross(va, p[1].v, p[3].v);
+    dd = dot3(va, p[0].v);
+    if (dd < 0.f && !mpr_zero(dd)) { p[2] = p[3]; cont = true; }
+    if (!cont) {
+      cross(va, p[3].v, p[2].v);
+      dd = dot3(va, p[0].v);
+      if (dd < 0.f && !mpr_zero(dd)) { p[1] = p[3]; cont = true; }
+    }
+    if (!cont) break;
+#pragma unroll
+    for (int k = 0; k < 3; k++) { va[k] = p[1].v[k] - p[0].v[k]; vb[k] = p[2].v[k] - p[0].v[k]; }
+    cross(dir, va, vb);
+    nrm3(dir);
+  }
+  for (int it = 0;; it++) {
+    mpr_dir(p, dir);
+    dd = dot3(dir, p[1].v);
+    if (mpr_zero(dd) || dd > 0.f) break;
+    mpr_support(m, s, g1, g2, dir, v4);
+    dd = dot3(v4.v, dir);
+    if (!(mpr_zero(dd) || dd > 0.f) || mpr_reach(p, v4, dir) || it > kMprIter) return false;
+    mpr_expand(p, v4);
+  }
+  for (int it = 0;; it++) {
+    mpr_dir(p, dir);
+    mpr_support(m, s, g1, g2, dir, v4);
+    if (mpr_reach(p, v4, dir) || it > kMprIter) break;
+    mpr_expand(p, v4);
+  }
+  float w[3];
+  tri_closest(p[1].v, p[2].v, p[3].v, w);
+  depth = sqrtf(dot3(w, w));
+  if (mpr_zero(depth)) { dir[0] = dir[1] = dir[2] = 0.f; }
+  else { dir[0] = w[0] / depth; dir[1] = w[1] / depth; dir[2] = w[2] / depth; }
+  float pd[3], b[4], x[3];
+  mpr_dir(p, pd);
+  cross(x, p[2].v, p[3].v); b[0] = dot3(x, p[1].v);
+  cross(x, p[3].v, p[2].v); b[1] = dot3(x, p[0].v);
+  cross(x, p[0].v, p[1].v); b[2] = dot3(x, p[3].v);
+  cross(x, p[2].v, p[1].v); b[3] = dot3(x, p[0].v);
+  float sum = b[0] + b[1] + b[2] + b[3];
+  if (mpr_zero(sum) || sum < 0.f) {
+    b[0] = 0.f;
+    cross(x, p[2].v, p[3].v); b[1] = dot3(x, pd);
+    cross(x, p[3].v, p[1].v); b[2] = dot3(x, pd);
+    cross(x, p[1].v, p[2].v); b[3] = dot3(x, pd);
+    sum = b[1] + b[2] + b[3];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    float pa = 0.f, pb = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { pa += b[i] * p[i].a[k]; pb += b[i] * p[i].b[k]; }
+    pos[k] = 0.5f * (pa + pb) / sum;
+  }
+  return true;
+}
+
 // per-lane narrow phase for plane/capsule/box-vs-capsule pairs (box-box is
 // wave-cooperative, below).  out: dist[4], pos[4][3], nrm[4][3]
-__device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const Smem& s, int p, float dist[4],
+template <class S>
+__device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const S& s, int p, float dist[4],
                             float pos[4][3], float nrm[4][3]) {
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   const int func = m->pair_func[p];
@@ -543,6 +787,27 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
     }
     return 2;
   }
+  if constexpr (S::WIDE) {
+    if (func == 9) {  // general convex (MPR)
+      float depth, n[3], pp[3];
+      if (mpr_lane(m, s, g1, g2, depth, n, pp)) {
+        if (n[0] == 0.f && n[1] == 0.f && n[2] == 0.f) n[2] = 1.f;
+        dist[0] = -depth;
+#pragma unroll
+        for (int c = 0; c < 3; c++) { pos[0][c] = pp[c]; nrm[0][c] = n[c]; }
+      }
+      return 1;
+    }
+    if (func == 10) {  // plane - convex: deepest support point
+      float n[3] = {R1[2], R1[5], R1[8]}, nn[3] = {-R1[2], -R1[5], -R1[8]}, q[3];
+      support_geom(m, s, g2, nn, q);
+      const float d = n[0] * (q[0] - x1[0]) + n[1] * (q[1] - x1[1]) + n[2] * (q[2] - x1[2]);
+      dist[0] = d;
+#pragma unroll
+      for (int c = 0; c < 3; c++) { pos[0][c] = q[c] - 0.5f * d * n[c]; nrm[0][c] = n[c]; }
+      return 1;
+    }
+  }
   return 0;
 }
 
@@ -578,7 +843,8 @@ __device__ __forceinline__ float impedance(const float* si, float pos, float mar
 // polygon edge and ballot compaction, the >4 selection is done on uniform
 // values.  Same definitions and orders as the oracle's col_box_box.
 // Appends up to 4 contacts to the active list.  Must be called by all lanes.
-__device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, Smem& s, int p, int lane) {
+template <class S>
+__device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& s, int p, int lane) {
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   const float margin = m->pair_margin[p];
   float x1[3], x2[3], axA[3][3], axB[3][3], t[3], ha[3], hb[3];
@@ -820,7 +1086,8 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, Sme
 
 struct LsPt { float alpha, cost, d0, d1; };
 
-__device__ __forceinline__ void ls_rows(const Smem& s, int lane, float alpha, float& q0, float& q1, float& q2) {
+template <class S>
+__device__ __forceinline__ void ls_rows(const S& s, int lane, float alpha, float& q0, float& q1, float& q2) {
   q0 = q1 = q2 = 0.f;
   for (int r = lane; r < s.nefc; r += WAVE) {
     float jar = s.efc_jar[r], jv = s.efc_jv[r];
@@ -843,7 +1110,8 @@ __device__ __forceinline__ LsPt ls_make(float alpha, float q0, float q1, float q
   return p;
 }
 
-__device__ __forceinline__ LsPt ls_eval(const Smem& s, int lane, const float qg[3], float alpha) {
+template <class S>
+__device__ __forceinline__ LsPt ls_eval(const S& s, int lane, const float qg[3], float alpha) {
   float q0, q1, q2;
   ls_rows(s, lane, alpha, q0, q1, q2);
   q0 = wsum(q0) + qg[0];
@@ -854,7 +1122,8 @@ __device__ __forceinline__ LsPt ls_eval(const Smem& s, int lane, const float qg[
 
 // three line-search points in one pass over the rows; the 9 reductions are
 // independent so their DPP chains interleave
-__device__ __forceinline__ void ls_eval3(const Smem& s, int lane, const float qg[3], float a0, float a1, float a2,
+template <class S>
+__device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3], float a0, float a1, float a2,
                                          LsPt& p0, LsPt& p1, LsPt& p2) {
   float q[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const float al[3] = {a0, a1, a2};
@@ -907,9 +1176,11 @@ __device__ __forceinline__ void ls_eval3(const Smem& s, int lane, const float qg
 #define MPCR_ROLLOUT_ATTR
 #endif
 
+template <int NVW, int NBW, int NGW, bool WIDE>
 __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
-  __shared__ Smem s;
+  using S = SmemT<NVW, NBW, NGW>;
+  __shared__ S s;
   const DevModel* __restrict__ const m0 = mptr;
   const DevModel* __restrict__ m = m0;
   const int lane = threadIdx.x;
@@ -922,9 +1193,9 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
   //      (plant mode: the caller's state, no init_pos override)
   if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
   const bool from_state = (args.plant & 1) != 0;
-  for (int i = lane; i < DX_NQ; i += WAVE)
+  for (int i = lane; i < S::NQW; i += WAVE)
     s.qpos[i] = i < m->nq ? (from_state ? args.state[ST_QPOS + i] : m->qpos_init[i]) : 0.f;
-  if (lane < DX_NV) {
+  if (lane < NVW) {
     const bool v = lane < nv;
     s.qvel[lane] = v ? (from_state ? args.state[ST_QVEL + lane] : m->qvel_init[lane]) : 0.f;
     s.qws[lane] = v && from_state ? args.state[ST_QWS + lane] : 0.f;
@@ -1072,6 +1343,22 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         for (int k = 0; k < 9; k++) s.gxmat[lane][k] = Rr[k];
       }
     }
+    if constexpr (S::WIDE) {  // connect anchors in world (the body frames die with the dynamics region)
+      if (lane < 2 * m->neq && m->eq_type[lane >> 1] == 0) {
+        const int e = lane >> 1, side = lane & 1;
+        const int bb = side ? m->eq_b2[e] : m->eq_b1[e];
+        const float* a = &m->eq_data[e][4 * side];
+        float pw[3] = {a[0], a[1], a[2]};
+        if (bb >= 0) {
+          float R[9], w[3];
+#pragma unroll
+          for (int k = 0; k < 9; k++) R[k] = s.xmat[bb][k];
+          mv(w, R, a);
+          pw[0] = s.xpos[bb][0] + w[0]; pw[1] = s.xpos[bb][1] + w[1]; pw[2] = s.xpos[bb][2] + w[2];
+        }
+        s.eqp[e][side][0] = pw[0]; s.eqp[e][side][1] = pw[1]; s.eqp[e][side][2] = pw[2];
+      }
+    }
     for (int tr = 0; tr < m->ntree; tr++) {
       float mm = (lane < nb && m->body_tree[lane] == tr) ? m->body_mass[lane] : 0.f;
       float cx = wsum(mm * (lane < nb ? s.xipos[lane][0] : 0.f));
@@ -1118,7 +1405,22 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
 
     STAMP(2);
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
-    // ---- cinert, cdof ---------------------------------------------------------
+    // ---- cinert, cdof (+ actuator forces) -------------------------------------
+    if constexpr (S::WIDE) {
+      if (lane < m->nu) {
+        float len = 0.f, vel = 0.f;
+        for (int k = 0; k < m->act_ntrn[lane]; k++) {
+          len = fmaf(m->act_moment[lane][k], s.qpos[m->act_qadr[lane][k]], len);
+          vel = fmaf(m->act_moment[lane][k], s.qvel[m->act_dof[lane][k]], vel);
+        }
+        const float* g = m->act_gain[lane];
+        const float* bp = m->act_bias[lane];
+        float gain = g[0];
+        if (m->act_gaffine[lane]) gain += g[1] * len + g[2] * vel;
+        const float bias = m->act_baffine[lane] ? bp[0] + bp[1] * len + bp[2] * vel : 0.f;
+        s.actf[lane] = clampf(gain * g[3] + bias, m->act_frc[lane][0], m->act_frc[lane][1]);
+      }
+    }
     if (lane < nb) {
       const int tr = m->body_tree[lane];
       float R[9], I[6];
@@ -1272,8 +1574,8 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     STAMP(4);
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // mass matrix entries (chain-masked) + bias forces
-    for (int idx = lane; idx < DX_NV * DX_NV; idx += WAVE) {
-      const int i = idx >> 4, j = idx & 15;
+    for (int idx = lane; idx < NVW * NVW; idx += WAVE) {
+      const int i = idx >> S::LOG_NVW, j = idx & (NVW - 1);
       float v = 0.f;
       if (i < nv && j < nv) {
         if ((m->dof_chainmask[i] >> j) & 1u) {
@@ -1301,8 +1603,15 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
       float bias = 0.f;
 #pragma unroll
       for (int k = 0; k < 6; k++) bias = fmaf(s.cdof[lane][k], f[k], bias);
-      s.qfs[lane] = -bias - m->dof_damping[lane] * s.qvel[lane];
-    } else if (lane < DX_NV) {
+      float qf = -bias - m->dof_damping[lane] * s.qvel[lane];
+      if constexpr (S::WIDE) {
+        if (m->has_spring) qf -= m->dof_stiffness[lane] * (s.qpos[m->dof_qposadr[lane]] - m->dof_springref[lane]);
+        float fa = 0.f;
+        for (int k = 0; k < m->dof_actn[lane]; k++) fa = fmaf(m->dof_actm[lane][k], s.actf[m->dof_acta[lane][k]], fa);
+        qf += clampf(fa, m->dof_actfrc[lane][0], m->dof_actfrc[lane][1]);
+      }
+      s.qfs[lane] = qf;
+    } else if (lane < NVW) {
       s.qfs[lane] = 0.f;
     }
     sync();
@@ -1311,13 +1620,13 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
     {
-      float Lm[DX_NV];
+      float Lm[NVW];
 #pragma unroll
-      for (int j = 0; j < DX_NV; j++) Lm[j] = lane < DX_NV ? s.M[lane][j] : 0.f;
+      for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? s.M[lane][j] : 0.f;
       chol_rows(Lm, lane);
       // the dynamics region (xpos..fvec) is dead once M is assembled
-      const float x = chol_solve(Lm, lane < DX_NV ? s.qfs[lane] : 0.f, lane, &s.xpos[0][0]);
-      if (lane < DX_NV) s.qas[lane] = lane < nv ? x : 0.f;
+      const float x = chol_solve<NVW, S::LD>(Lm, lane < NVW ? s.qfs[lane] : 0.f, lane, &s.xpos[0][0]);
+      if (lane < NVW) s.qas[lane] = lane < nv ? x : 0.f;
     }
 
     STAMP(6);
@@ -1414,7 +1723,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     // ---- constraint rows: equality, limits, contacts ------------------------
     {
       const int ncon = s.ncon;
-      const int neq = (m->disableflags & 64) ? 0 : m->neq;
+      const int neq = (m->disableflags & 64) ? 0 : (S::WIDE ? m->neqrow : m->neq);
       int nlim_l = 0, lsides = 0;
       if (lane < m->njnt && !(m->disableflags & 32) && m->jnt_limited[lane] &&
           (m->jnt_type[lane] == 2 || m->jnt_type[lane] == 3)) {
@@ -1437,7 +1746,9 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         nefc = neq + nlim + (keep_con > 0 ? __shfl(con_pre + ncr, keep_con - 1) : 0);
         status |= 1;
       }
-      if (lane < neq) s.efc_src[lane] = (1 << 24) | (lane << 4);
+      // equality rows: joint (side 0) or connect component side - 1
+      if (lane < neq)
+        s.efc_src[lane] = S::WIDE ? ((1 << 24) | (m->eqrow_eq[lane] << 4) | m->eqrow_k[lane]) : ((1 << 24) | (lane << 4));
       if (nlim_l) {
         int o = neq + lim_pre;
         if (lsides & 1) s.efc_src[o++] = (2 << 24) | (lane << 4) | 0;
@@ -1452,11 +1763,28 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
       sync();
       // Jacobian entries of equality/limit rows: (row, dof)
       const int nsimple = neq + nlim;
-      for (int idx = lane; idx < nsimple * DX_NV; idx += WAVE) {
-        const int r = idx >> 4, i = idx & 15;
+      for (int idx = lane; idx < nsimple * NVW; idx += WAVE) {
+        const int r = idx >> S::LOG_NVW, i = idx & (NVW - 1);
         const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
         float v = 0.f;
-        if (kind == 1) {
+        if (S::WIDE && kind == 1 && side > 0) {  // connect: (J_p(b1, p1) - J_p(b2, p2))[side - 1]
+          const int comp = side - 1;
+          if (i < nv) {
+            const float* cd = s.cdof[i];
+#pragma unroll
+            for (int e2 = 0; e2 < 2; e2++) {
+              const int bb = e2 == 0 ? m->eq_b1[id] : m->eq_b2[id];
+              if (bb >= 0 && ((m->body_dofmask[bb] >> i) & 1u)) {
+                const int tr = m->body_tree[bb];
+                float r[3] = {s.eqp[id][e2][0] - s.com[tr][0], s.eqp[id][e2][1] - s.com[tr][1],
+                              s.eqp[id][e2][2] - s.com[tr][2]}, cr[3];
+                cross(cr, cd, r);
+                const float jv = cd[3 + comp] + cr[comp];
+                v += e2 == 0 ? jv : -jv;
+              }
+            }
+          }
+        } else if (kind == 1) {
           const int j1 = m->eq_j1[id], j2 = m->eq_j2[id];
           if (i == m->jnt_dofadr[j1]) v += 1.f;
           if (j2 >= 0 && i == m->jnt_dofadr[j2]) {
@@ -1470,8 +1798,8 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         s.J[r][i] = v;
       }
       // contact Jacobians: (contact, dof) -> J_n +- mu J_t rows
-      for (int idx = lane; idx < keep_con * DX_NV; idx += WAVE) {
-        const int c = idx >> 4, i = idx & 15;
+      for (int idx = lane; idx < keep_con * NVW; idx += WAVE) {
+        const int c = idx >> S::LOG_NVW, i = idx & (NVW - 1);
         const int p = s.con_pair[c];
         const int b1 = m->geom_body[m->pair_g1[p]], b2 = m->geom_body[m->pair_g2[p]];
         float jd[3] = {0.f, 0.f, 0.f};
@@ -1512,7 +1840,13 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         float pos, margin, diag;
         const float* sref;
         const float* simp;
-        if (kind == 1) {
+        if (S::WIDE && kind == 1 && side > 0) {  // connect component
+          pos = s.eqp[id][0][side - 1] - s.eqp[id][1][side - 1];
+          margin = 0.f;
+          diag = m->eq_diag[id];
+          sref = m->eq_solref[id];
+          simp = m->eq_solimp[id];
+        } else if (kind == 1) {
           const int j1 = m->eq_j1[id], j2 = m->eq_j2[id];
           const float* c = m->eq_data[id];
           const float q1 = s.qpos[m->jnt_qposadr[j1]] - m->jnt_qpos0[j1];
@@ -1542,7 +1876,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           sref = m->pair_solref[p];
           simp = m->pair_solimp[p];
         }
-        const float vel = dot16(s.J[r], s.qvel);
+        const float vel = dotN<NVW>(s.J[r], s.qvel);
         const float imp = impedance(simp, pos, margin);
         const float R = fmaxf((1.f - imp) / imp * diag, kMinVal);
         float tc = sref[0];
@@ -1570,30 +1904,30 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     // ---- Newton solver (primal), MJX-style line search ------------------------
     {
       const int nefc = s.nefc;
-      float qacc_l = lane < DX_NV ? s.qas[lane] : 0.f;  // this lane's dof value
+      float qacc_l = lane < NVW ? s.qas[lane] : 0.f;  // this lane's dof value
       if (nefc > 0) {
         // warm start: the better of qacc_warmstart and qacc_smooth
         if (!(m->disableflags & 4)) {
           float maw = 0.f, mas = 0.f;
           if (lane < nv) {
-            maw = dot16(s.M[lane], s.qws);
-            mas = dot16(s.M[lane], s.qas);
+            maw = dotN<NVW>(s.M[lane], s.qws);
+            mas = dotN<NVW>(s.M[lane], s.qas);
           }
           const float gw = lane < nv ? (maw - s.qfs[lane]) * (s.qws[lane] - s.qas[lane]) : 0.f;
           const float gs = lane < nv ? (mas - s.qfs[lane]) * (s.qas[lane] - s.qas[lane]) : 0.f;
           float cw = 0.f, cs = 0.f;
           for (int r = lane; r < nefc; r += WAVE) {
-            const float jw = dot16(s.J[r], s.qws) - s.efc_aref[r];
-            const float js = dot16(s.J[r], s.qas) - s.efc_aref[r];
+            const float jw = dotN<NVW>(s.J[r], s.qws) - s.efc_aref[r];
+            const float js = dotN<NVW>(s.J[r], s.qas) - s.efc_aref[r];
             const bool eq = (s.efc_src[r] >> 24) == 1;
             if (eq || jw < 0.f) cw += s.efc_D[r] * jw * jw;
             if (eq || js < 0.f) cs += s.efc_D[r] * js * js;
           }
           const float costw = 0.5f * wsum(gw) + 0.5f * wsum(cw);
           const float costs = 0.5f * wsum(gs) + 0.5f * wsum(cs);
-          if (costw < costs && lane < DX_NV) qacc_l = s.qws[lane];
+          if (costw < costs && lane < NVW) qacc_l = s.qws[lane];
         }
-        if (lane < DX_NV) s.qacc[lane] = qacc_l;
+        if (lane < NVW) s.qacc[lane] = qacc_l;
         sync();
         STAMP(13);
         const float scale = 1.f / (m->meaninertia * (float)(nv > 1 ? nv : 1));
@@ -1603,10 +1937,10 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           // (cost / gradient only feed the stop test)
           if (it >= m->iterations) break;
           // Ma, jar, cost at the current qacc; per-row force and active D
-          const float ma = lane < nv ? dot16(s.M[lane], s.qacc) : 0.f;
+          const float ma = lane < nv ? dotN<NVW>(s.M[lane], s.qacc) : 0.f;
           float cc = 0.f;
           for (int r = lane; r < nefc; r += WAVE) {
-            const float jar = dot16(s.J[r], s.qacc) - s.efc_aref[r];
+            const float jar = dotN<NVW>(s.J[r], s.qacc) - s.efc_aref[r];
             const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
             const float D = s.efc_D[r];
             s.efc_jar[r] = jar;
@@ -1617,47 +1951,57 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           const float gauss = wsum(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
           const float cost = 0.5f * gauss + 0.5f * wsum(cc);
           sync();
-          // grad = Ma - qfrc_smooth - J^T f: lane (dof i, row quarter q)
-          const int gi = lane & 15, gq = lane >> 4;
+          // grad = Ma - qfrc_smooth - J^T f: lane (dof i, row group q); RPW
+          // lanes share a dof (4 at NVW 16, 2 at NVW 32)
+          constexpr int RPW = WAVE / NVW;
+          const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
           float qc = 0.f;
-          for (int r = gq; r < nefc; r += 4) qc = fmaf(s.J[r][gi], s.efc_f[r], qc);
-          qc += __shfl_xor(qc, 16);
-          qc += __shfl_xor(qc, 32);
+          for (int r = gq; r < nefc; r += RPW) qc = fmaf(s.J[r][gi], s.efc_f[r], qc);
+#pragma unroll
+          for (int o = NVW; o < WAVE; o <<= 1) qc += __shfl_xor(qc, o);
           const float grad = lane < nv ? ma - s.qfs[lane] - qc : 0.f;
           const float gn = sqrtf(wsum(grad * grad));
           if (scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance) break;
-          // Hessian H = M + J^T D_active J: lane (row i, column quad q) builds
-          // H[i][4q..4q+3]; rows are gathered to lanes 0..15 through LDS
+          // Hessian H = M + J^T D_active J: lane (row i, column quads q, q + RPW,
+          // ...) builds QPL float4s of row i; rows are gathered to lanes
+          // 0..NVW-1 through LDS
+          constexpr int QPL = NVW / 4 / RPW;
           float* Hs = &s.gxpos[0][0];  // geom poses are dead during Newton
           {
-            const float4 m4 = reinterpret_cast<const float4*>(s.M[gi])[gq];
-            float h0 = m4.x, h1 = m4.y, h2 = m4.z, h3 = m4.w;
+            float4 hq[QPL];
+#pragma unroll
+            for (int k = 0; k < QPL; k++) hq[k] = reinterpret_cast<const float4*>(s.M[gi])[gq + RPW * k];
             for (int r = 0; r < nefc; r++) {
               const float c = s.efc_Da[r] * s.J[r][gi];
-              const float4 v = reinterpret_cast<const float4*>(s.J[r])[gq];
-              h0 = fmaf(c, v.x, h0); h1 = fmaf(c, v.y, h1); h2 = fmaf(c, v.z, h2); h3 = fmaf(c, v.w, h3);
+#pragma unroll
+              for (int k = 0; k < QPL; k++) {
+                const float4 v = reinterpret_cast<const float4*>(s.J[r])[gq + RPW * k];
+                hq[k].x = fmaf(c, v.x, hq[k].x); hq[k].y = fmaf(c, v.y, hq[k].y);
+                hq[k].z = fmaf(c, v.z, hq[k].z); hq[k].w = fmaf(c, v.w, hq[k].w);
+              }
             }
-            reinterpret_cast<float4*>(Hs + gi * LDL)[gq] = make_float4(h0, h1, h2, h3);
+#pragma unroll
+            for (int k = 0; k < QPL; k++) reinterpret_cast<float4*>(Hs + gi * S::LD)[gq + RPW * k] = hq[k];
           }
           sync();
-          float h[DX_NV];
+          float h[NVW];
           {
-            const float4* row = reinterpret_cast<const float4*>(Hs + (lane & 15) * LDL);
+            const float4* row = reinterpret_cast<const float4*>(Hs + (lane & (NVW - 1)) * S::LD);
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < NVW / 4; q++) {
               const float4 v = row[q];
               h[4 * q] = v.x; h[4 * q + 1] = v.y; h[4 * q + 2] = v.z; h[4 * q + 3] = v.w;
             }
           }
           chol_rows(h, lane);
-          const float mg = chol_solve(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
+          const float mg = chol_solve<NVW, S::LD>(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
           const float search = lane < nv ? -mg : 0.f;
           STAMP(14);
-          if (lane < DX_NV) s.srch[lane] = search;
+          if (lane < NVW) s.srch[lane] = search;
           sync();
           // Mv, jv, quadratic coefficients
-          const float mvv = lane < nv ? dot16(s.M[lane], s.srch) : 0.f;
-          for (int r = lane; r < nefc; r += WAVE) s.efc_jv[r] = dot16(s.J[r], s.srch);
+          const float mvv = lane < nv ? dotN<NVW>(s.M[lane], s.srch) : 0.f;
+          for (int r = lane; r < nefc; r += WAVE) s.efc_jv[r] = dotN<NVW>(s.J[r], s.srch);
           const float sn = sqrtf(wsum(search * search));
           const float gtol = m->tolerance * m->ls_tolerance * sn * m->meaninertia * (float)(nv > 1 ? nv : 1);
           float qg[3];
@@ -1689,23 +2033,52 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           }
           const bool improved = lo.cost < p0.cost || hi.cost < p0.cost;
           const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
-          if (improved && lane < DX_NV) s.qacc[lane] = s.qacc[lane] + alpha * s.srch[lane];
+          if (improved && lane < NVW) s.qacc[lane] = s.qacc[lane] + alpha * s.srch[lane];
           prev_cost = cost;
           sync();
         }
       } else {
-        if (lane < DX_NV) s.qacc[lane] = qacc_l;
+        if (lane < NVW) s.qacc[lane] = qacc_l;
         sync();
       }
     }
 
     STAMP(9);
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
+    // ---- implicitfast (dual-arm class): (M + dt D) a = qfrc_smooth + J^T f at
+    //      the final qacc; the velocity update uses a, the warm start qacc --
+    bool implicit = false;
+    if constexpr (S::WIDE) {
+      if (m->integrator == 3) {
+        implicit = true;
+        const int nefc = s.nefc;
+        for (int r = lane; r < nefc; r += WAVE) {
+          const float jar = dotN<NVW>(s.J[r], s.qacc) - s.efc_aref[r];
+          const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
+          s.efc_f[r] = act ? -s.efc_D[r] * jar : 0.f;
+        }
+        sync();
+        constexpr int RPW = WAVE / NVW;
+        const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
+        float qc = 0.f;
+        for (int r = gq; r < nefc; r += RPW) qc = fmaf(s.J[r][gi], s.efc_f[r], qc);
+#pragma unroll
+        for (int o = NVW; o < WAVE; o <<= 1) qc += __shfl_xor(qc, o);
+        const float dt = m->timestep;
+        float Lm[NVW];
+#pragma unroll
+        for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? fmaf(dt, m->impl_D[lane][j], s.M[lane][j]) : 0.f;
+        chol_rows(Lm, lane);
+        const float a = chol_solve<NVW, S::LD>(Lm, lane < nv ? s.qfs[lane] + qc : 0.f, lane, &s.gxpos[0][0]);
+        if (lane < NVW) s.srch[lane] = lane < nv ? a : 0.f;
+        sync();
+      }
+    }
     // ---- Euler: qvel += dt qacc; integrate qpos; warm start -----------------
     {
       const float dt = m->timestep;
       if (lane < nv) {
-        s.qvel[lane] = s.qvel[lane] + dt * s.qacc[lane];
+        s.qvel[lane] = s.qvel[lane] + dt * (implicit ? s.srch[lane] : s.qacc[lane]);
         s.qws[lane] = s.qacc[lane];
       }
       sync();

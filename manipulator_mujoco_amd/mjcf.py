@@ -118,6 +118,22 @@ COLLISION_FUNC = {
     (6, 6): (cmodel.COL_BOX_BOX, 4),
 }
 
+CONVEX_TYPES = (2, 3, 5, 6, 7)  # sphere, capsule, cylinder, box, mesh (convex hull)
+
+
+def collision_func(t1, t2):
+    """(func, contact slots) of a pair with t1 <= t2: the dedicated primitive
+    functions, else the general convex one (one contact, MuJoCo's own
+    general-convex path also yields one)."""
+    if (t1, t2) in COLLISION_FUNC:
+        return COLLISION_FUNC[(t1, t2)]
+    if t1 == 0 and t2 in CONVEX_TYPES:
+        return (cmodel.COL_PLANE_CONVEX, 1)
+    if t1 in CONVEX_TYPES and t2 in CONVEX_TYPES:
+        return (cmodel.COL_CONVEX, 1)
+    return None
+
+
 ROBOT_GEOM_NAMES = tuple(f"robot_{i}" for i in range(10))  # SBP/mjx_planner.py:113
 
 
@@ -445,8 +461,9 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
                         disable &= ~flag_bits[k]
     if timestep is not None:
         opt["timestep"] = float(timestep)  # SBP/mjx_planner.py:103
-    if opt["integrator"] != "Euler":
-        raise MJCFError(f"integrator {opt['integrator']!r} not supported yet (SURVEY §8f-4)")
+    integrators = {"Euler": cmodel.INT_EULER, "implicitfast": cmodel.INT_IMPLICITFAST}
+    if opt["integrator"] not in integrators:
+        raise MJCFError(f"integrator {opt['integrator']!r} not supported (Euler, implicitfast)")
     if opt["cone"] != "pyramidal":
         raise MJCFError("only pyramidal friction cones are supported")
     if opt["solver"] != "Newton":
@@ -460,9 +477,10 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
     meshes = {}
     for asset in root.findall("asset"):
         for m in asset.findall("mesh"):
-            fname = m.get("file")
-            name = m.get("name") or os.path.splitext(os.path.basename(fname))[0]
-            scale = _floats(m.get("scale", "1 1 1"), 3)
+            a = defaults.attrs(m.get("class", "main"), "mesh", m)  # mesh scale may come from a class
+            fname = a.get("file")
+            name = a.get("name") or os.path.splitext(os.path.basename(fname))[0]
+            scale = _floats(a.get("scale", "1 1 1"), 3)
             meshes[name] = (os.path.join(basedir, meshdir, fname), np.array(scale))
 
     # ---- body tree (preorder) ---------------------------------------------
@@ -531,6 +549,11 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
                 solimp=(_floats(a.get("solimplimit", " ".join(map(str, DEFAULT_SOLIMP))))
                         + list(DEFAULT_SOLIMP))[:5],
                 margin=float(a.get("margin", 0.0)),
+                stiffness=float(a.get("stiffness", 0.0)),
+                springref=float(a.get("springref", 0.0)) * (angle_scale if jt == 3 else 1.0),
+                actfrcrange=_floats(a["actuatorfrcrange"], 2) if "actuatorfrcrange" in a else [0.0, 0.0],
+                actfrclimited=(a.get("actuatorfrclimited") == "true" or (
+                    a.get("actuatorfrclimited", "auto") == "auto" and autolimits and "actuatorfrcrange" in a)),
             ))
             if np.linalg.norm(jnt[-1]["axis"]) > 0:
                 jnt[-1]["axis"] = jnt[-1]["axis"] / np.linalg.norm(jnt[-1]["axis"])
@@ -740,21 +763,26 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
                 continue
             a, bb = (i, j) if g1["type"] <= g2["type"] else (j, i)
             key = (geoms[a]["type"], geoms[bb]["type"])
-            if key not in COLLISION_FUNC:
+            fn = collision_func(*key)
+            if fn is None:
                 raise MJCFError(f"no narrow phase for geom types {key} "
                                 f"({geoms[a]['name']!r}, {geoms[bb]['name']!r})")
-            func, ncon = COLLISION_FUNC[key]
+            func, ncon = fn
             ga, gb = geoms[a], geoms[bb]
-            # mixing (same priority): max friction/condim/margin/gap, solmix-weighted solref/solimp
-            mix = ga["solmix"] / (ga["solmix"] + gb["solmix"]) if (ga["solmix"] + gb["solmix"]) > 0 else 0.5
-            if ga["solref"][0] > 0 and gb["solref"][0] > 0:
-                solref = [mix * ga["solref"][k] + (1 - mix) * gb["solref"][k] for k in range(2)]
+            if ga["priority"] != gb["priority"]:  # the higher priority geom's parameters
+                gp = ga if ga["priority"] > gb["priority"] else gb
+                condim, friction = gp["condim"], gp["friction"][0]
+                solref, solimp = list(gp["solref"]), list(gp["solimp"])
             else:
-                solref = [min(ga["solref"][k], gb["solref"][k]) for k in range(2)]
-            solimp = [mix * ga["solimp"][k] + (1 - mix) * gb["solimp"][k] for k in range(5)]
-            pairs.append(dict(g1=a, g2=bb, func=func, ncon=ncon,
-                              condim=max(ga["condim"], gb["condim"]),
-                              friction=max(ga["friction"][0], gb["friction"][0]),
+                # mixing (same priority): max friction/condim, solmix-weighted solref/solimp
+                mix = ga["solmix"] / (ga["solmix"] + gb["solmix"]) if (ga["solmix"] + gb["solmix"]) > 0 else 0.5
+                if ga["solref"][0] > 0 and gb["solref"][0] > 0:
+                    solref = [mix * ga["solref"][k] + (1 - mix) * gb["solref"][k] for k in range(2)]
+                else:
+                    solref = [min(ga["solref"][k], gb["solref"][k]) for k in range(2)]
+                solimp = [mix * ga["solimp"][k] + (1 - mix) * gb["solimp"][k] for k in range(5)]
+                condim, friction = max(ga["condim"], gb["condim"]), max(ga["friction"][0], gb["friction"][0])
+            pairs.append(dict(g1=a, g2=bb, func=func, ncon=ncon, condim=condim, friction=friction,
                               solref=solref, solimp=solimp,
                               margin=max(ga["margin"], gb["margin"]),
                               gap=max(ga["gap"], gb["gap"])))
@@ -785,11 +813,20 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
                 j1 = jnames.index(a["joint1"])
                 j2 = jnames.index(a["joint2"]) if "joint2" in a else -1
                 poly = (_floats(a.get("polycoef", "0 1 0 0 0")) + [0] * 5)[:5]
-                eqs.append(dict(type=cmodel.EQ_JOINT, obj1=j1, obj2=j2, data=poly,
+                eqs.append(dict(type=cmodel.EQ_JOINT, obj1=j1, obj2=j2, data=poly + [0.0],
+                                solref=_floats(a.get("solref", "0.02 1"), 2),
+                                solimp=(_floats(a.get("solimp", "0.9 0.95 0.001 0.5 2")) + list(DEFAULT_SOLIMP))[:5]))
+            elif q.tag == "connect":
+                a = defaults.attrs(q.get("class", "main"), "equality", q)
+                bnames = [b.name for b in bodies]
+                b1 = bnames.index(a["body1"])
+                b2 = bnames.index(a["body2"]) if "body2" in a else 0
+                anchor = _floats(a.get("anchor", "0 0 0"), 3)
+                eqs.append(dict(type=cmodel.EQ_CONNECT, obj1=b1, obj2=b2, data=anchor + [0.0, 0.0, 0.0],
                                 solref=_floats(a.get("solref", "0.02 1"), 2),
                                 solimp=(_floats(a.get("solimp", "0.9 0.95 0.001 0.5 2")) + list(DEFAULT_SOLIMP))[:5]))
             else:
-                raise MJCFError(f"equality <{q.tag}> not supported yet (SURVEY §8f-4)")
+                raise MJCFError(f"equality <{q.tag}> not supported (joint, connect)")
 
     # ---- reference configuration ---------------------------------------------
     qpos0 = np.zeros(nq)
@@ -837,6 +874,10 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
     m.jnt_solref = np.array([J["solref"] for J in jnt]).reshape(-1, 2)
     m.jnt_solimp = np.array([J["solimp"] for J in jnt]).reshape(-1, 5)
     m.jnt_margin = np.array([J["margin"] for J in jnt])
+    m.jnt_stiffness = np.array([J["stiffness"] for J in jnt])
+    m.jnt_springref = np.array([J["springref"] for J in jnt])
+    m.jnt_actfrclimited = np.array([int(J["actfrclimited"]) for J in jnt], dtype=np.int64)
+    m.jnt_actfrcrange = np.array([J["actfrcrange"] for J in jnt]).reshape(-1, 2)
     m.dof_bodyid = np.array(dof_bodyid, dtype=np.int64)
     m.dof_jntid = np.array(dof_jntid, dtype=np.int64)
     m.dof_parentid = np.array(dof_parentid, dtype=np.int64)
@@ -863,6 +904,7 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
         return {0: 0.0, 2: s[0], 3: s[0] + s[1], 4: max(s), 5: math.hypot(s[0], s[1]),
                 6: float(np.linalg.norm(s))}.get(g["type"], 0.0)
     m.geom_rbound = np.array([rbound(g) for g in geoms])
+    _convex_hulls(m, geoms, pairs, meshes)
     m.nsite = len(sites)
     m.site_bodyid = np.array([s["body"] for s in sites], dtype=np.int64)
     m.site_pos = np.array([s["pos"] for s in sites]).reshape(-1, 3)
@@ -881,7 +923,7 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
     m.eq_type = np.array([e["type"] for e in eqs], dtype=np.int64)
     m.eq_obj1 = np.array([e["obj1"] for e in eqs], dtype=np.int64)
     m.eq_obj2 = np.array([e["obj2"] for e in eqs], dtype=np.int64)
-    m.eq_data = np.array([e["data"] for e in eqs]).reshape(-1, 5)
+    m.eq_data = np.array([e["data"] for e in eqs]).reshape(-1, 6)
     m.eq_solref = np.array([e["solref"] for e in eqs]).reshape(-1, 2)
     m.eq_solimp = np.array([e["solimp"] for e in eqs]).reshape(-1, 5)
 
@@ -896,6 +938,8 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
         if jt not in (2, 3) or m.jnt_qposadr[m.dof_jntid[k]] != k:
             raise MJCFError("the first num_dof dofs must be hinge/slide joints with qpos == qvel indexing")
 
+    _actuators(m, root, defaults, jnt, jnames, autolimits)
+    m.integrator = integrators[opt["integrator"]]
     m.timestep = opt["timestep"]
     m.iterations = opt["iterations"]
     m.ls_iterations = opt["ls_iterations"]
@@ -906,7 +950,148 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
     m.source = path
 
     set_const(m)
+    _connect_anchors(m)
     return m
+
+
+# ---------------------------------------------------------------------------
+# collision meshes, tendons / actuators, connect anchors
+# ---------------------------------------------------------------------------
+
+
+def convex_hull(verts):
+    """Hull vertices (recentred on their mean), the centre, and the vertex
+    graph (neighbour lists) of a point cloud: what hill-climbing support
+    queries walk (MuJoCo keeps the same graph, mesh_graph)."""
+    from scipy.spatial import ConvexHull
+    v = np.unique(np.asarray(verts, dtype=np.float64).reshape(-1, 3), axis=0)
+    h = ConvexHull(v)
+    idx = np.asarray(h.vertices)
+    remap = {int(g): k for k, g in enumerate(idx)}
+    hv = v[idx]
+    c = hv.mean(axis=0)
+    nbr = [set() for _ in idx]
+    for tri in h.simplices:
+        t = [remap[int(x)] for x in tri]
+        for a in range(3):
+            for b in range(3):
+                if a != b:
+                    nbr[t[a]].add(t[b])
+    return hv - c, c, [sorted(n) for n in nbr]
+
+
+def _convex_hulls(m, geoms, pairs, meshes):
+    """Hulls of the mesh geoms any pair uses; the geom frame is moved to the
+    hull centre (an interior point, as MuJoCo recentres meshes), which is
+    where the convex narrow phase starts its portal."""
+    ng = len(geoms)
+    m.geom_hulladr = -np.ones(ng, dtype=np.int64)
+    m.geom_hullnum = np.zeros(ng, dtype=np.int64)
+    used = {p["g1"] for p in pairs} | {p["g2"] for p in pairs}
+    cache, verts, adjadr, adjnum, adj = {}, [], [], [], []
+    for gi in sorted(used):
+        g = geoms[gi]
+        if g["type"] != 7:
+            continue
+        if g["mesh"] not in cache:
+            mpath, scale = meshes[g["mesh"]]
+            tris = load_stl(mpath) if mpath.lower().endswith(".stl") else load_obj(mpath)
+            hv, c, nbr = convex_hull(tris.reshape(-1, 3) * scale[None, :])
+            base = len(verts)
+            for k, n in enumerate(nbr):
+                adjadr.append(len(adj))
+                adjnum.append(len(n))
+                adj.extend(base + x for x in n)
+            verts.extend(hv.tolist())
+            cache[g["mesh"]] = (base, len(hv), c, float(np.max(np.linalg.norm(hv, axis=1))))
+        base, num, c, rb = cache[g["mesh"]]
+        m.geom_hulladr[gi] = base
+        m.geom_hullnum[gi] = num
+        m.geom_pos[gi] = m.geom_pos[gi] + quat2mat(m.geom_quat[gi]) @ c
+        m.geom_rbound[gi] = rb
+    m.nhullv = len(verts)
+    m.nhulla = len(adj)
+    m.hull_vert = np.array(verts, dtype=np.float64).reshape(-1, 3)
+    m.hull_adjadr = np.array(adjadr, dtype=np.int64)
+    m.hull_adjnum = np.array(adjnum, dtype=np.int64)
+    m.hull_adj = np.array(adj, dtype=np.int64)
+
+
+def _actuators(m, root, defaults, jnt, jnames, autolimits):
+    """<tendon><fixed> and <actuator> (general / motor / position) with joint
+    or fixed-tendon transmissions, flattened to (dof, qpos adr, moment)."""
+    tendons = {}
+    for t in root.findall("tendon"):
+        for f in t.findall("fixed"):
+            tendons[f.get("name")] = [(jnames.index(j.get("joint")), float(j.get("coef", 1.0)))
+                                      for j in f.findall("joint")]
+    acts = []
+    for a_el in root.findall("actuator"):
+        for el in a_el:
+            tag = el.tag
+            if tag not in ("general", "motor", "position"):
+                raise MJCFError(f"actuator <{tag}> not supported (general, motor, position)")
+            a = defaults.attrs(el.get("class", "main"), tag, el)
+            gear = _floats(a.get("gear", "1"))[0]
+            if "joint" in a:
+                j = jnames.index(a["joint"])
+                trn = [(j, gear)]
+            elif "tendon" in a:
+                trn = [(j, c * gear) for j, c in tendons[a["tendon"]]]
+            else:
+                raise MJCFError("actuators need a joint or tendon transmission")
+            if len(trn) > 2:
+                raise MJCFError("tendon transmissions of more than 2 joints are not supported")
+            if tag == "motor":
+                gaintype, biastype, gp, bp = "fixed", "none", [1.0, 0, 0], [0.0, 0, 0]
+            elif tag == "position":
+                kp = float(a.get("kp", 1.0))
+                kv = float(a.get("kv", 0.0))
+                gaintype, biastype, gp, bp = "fixed", "affine", [kp, 0, 0], [0.0, -kp, -kv]
+            else:
+                gaintype, biastype = a.get("gaintype", "fixed"), a.get("biastype", "none")
+                gp = (_floats(a.get("gainprm", "1")) + [0.0, 0.0])[:3]
+                bp = (_floats(a.get("biasprm", "0")) + [0.0, 0.0, 0.0])[:3]
+            if gaintype not in ("fixed", "affine") or biastype not in ("none", "affine"):
+                raise MJCFError(f"gaintype {gaintype!r} / biastype {biastype!r} not supported")
+
+            def lim(name):
+                rng = _floats(a[name + "range"], 2) if name + "range" in a else [0.0, 0.0]
+                flag = a.get(name + "limited", "auto")
+                on = flag == "true" or (flag == "auto" and autolimits and name + "range" in a)
+                return rng, int(on)
+            cr, cl = lim("ctrl")
+            fr, fl = lim("force")
+            acts.append(dict(trn=trn, gaintype=0 if gaintype == "fixed" else 1,
+                             biastype=0 if biastype == "none" else 1, gainprm=gp, biasprm=bp,
+                             ctrlrange=cr, ctrllimited=cl, forcerange=fr, forcelimited=fl))
+    m.nu = len(acts)
+    nu = max(m.nu, 0)
+    m.act_ntrn = np.array([len(a["trn"]) for a in acts], dtype=np.int64)
+    m.act_dof = np.array([[m.jnt_dofadr[j] for j, _ in a["trn"]] + [-1] * (2 - len(a["trn"])) for a in acts],
+                         dtype=np.int64).reshape(nu, 2)
+    m.act_qadr = np.array([[m.jnt_qposadr[j] for j, _ in a["trn"]] + [-1] * (2 - len(a["trn"])) for a in acts],
+                          dtype=np.int64).reshape(nu, 2)
+    m.act_moment = np.array([[c for _, c in a["trn"]] + [0.0] * (2 - len(a["trn"])) for a in acts]).reshape(nu, 2)
+    for k in ("gaintype", "biastype", "ctrllimited", "forcelimited"):
+        setattr(m, "act_" + k, np.array([a[k] for a in acts], dtype=np.int64))
+    for k, w in (("gainprm", 3), ("biasprm", 3), ("ctrlrange", 2), ("forcerange", 2)):
+        setattr(m, "act_" + k, np.array([a[k] for a in acts], dtype=np.float64).reshape(nu, w))
+    m.act_ctrl = np.zeros(nu)  # MjData.ctrl starts at 0 and the reference never sets it
+
+
+def _connect_anchors(m):
+    """eq_data[3:6] of connect equalities: the body1 anchor expressed in
+    body2's frame at qpos0 (MuJoCo's compiler does the same)."""
+    if not m.neq or not (m.eq_type == cmodel.EQ_CONNECT).any():
+        return
+    k = kinematics0(m, m.qpos0)
+    for e in range(m.neq):
+        if m.eq_type[e] != cmodel.EQ_CONNECT:
+            continue
+        b1, b2 = m.eq_obj1[e], m.eq_obj2[e]
+        p = k["xpos"][b1] + k["xmat"][b1] @ m.eq_data[e, :3]
+        m.eq_data[e, 3:6] = k["xmat"][b2].T @ (p - k["xpos"][b2])
 
 
 # ---------------------------------------------------------------------------

@@ -10,6 +10,10 @@ plain numeric arrays:
                       gravcomp, free target_0, static targets/obstacles
 * ``ur5e_hande_mjx``  URD/ur5e_1_robotiq_hande_mjx.xml (config C2)
 * ``scene_mjx``       URD/scene_mjx.xml = arm + object.xml box (config C3)
+* ``dual_arm``        URD/dual_arm_gripper_scene.xml (configs C4/C5): UR5e +
+                      Hand-E and UR5e + Robotiq 2F-85, implicitfast, 14
+                      actuators, fixed tendons, connect/joint equalities,
+                      convex-hull mesh collision
 """
 
 from __future__ import annotations
@@ -25,11 +29,12 @@ BUNDLES = {
     "planner_scene": "planner_scene.npz",
     "ur5e_hande_mjx": "ur5e_hande_mjx.npz",
     "scene_mjx": "scene_mjx.npz",
+    "dual_arm": "dual_arm.npz",
 }
 
 _SCALARS = ("nbody", "njnt", "nq", "nv", "ngeom", "nsite", "npair", "neq", "ncon", "nslot", "nctrl",
             "hande_body", "tcp_site", "iterations", "ls_iterations", "disableflags", "ntree", "timestep",
-            "tolerance", "ls_tolerance", "impratio", "meaninertia")
+            "tolerance", "ls_tolerance", "impratio", "meaninertia", "nu", "nhullv", "nhulla", "integrator")
 
 
 def save_bundle(m, path):
@@ -53,7 +58,7 @@ def load_bundle(path, timestep=None):
         if k != "__meta__":
             setattr(m, k, z[k])
     for k in _SCALARS:
-        setattr(m, k, meta[k])
+        setattr(m, k, meta.get(k, 0))
     m.names = meta["names"]
     m.opt = meta["opt"]
     m.source = meta.get("source", "")

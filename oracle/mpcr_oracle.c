@@ -15,7 +15,15 @@
  *     contacts, pyramidal contact / limit / joint-equality constraints with
  *     solref/solimp impedance, Newton solver (iterations=1, ls_iterations=5,
  *     warm start = better of qacc_warmstart and qacc_smooth), semi-implicit
- *     Euler (eulerdamp disabled).
+ *     Euler (eulerdamp disabled);
+ *   - the dual-arm features: joint springs, actuators
+ *     (gain/bias affine, joint and fixed-tendon transmissions, ctrl/force
+ *     clamps, joint actuator-force ranges), connect equalities, the
+ *     implicitfast integrator (M - dt*qDeriv with damping and actuator
+ *     velocity derivatives, no Coriolis) and general convex collision
+ *     (capsule / cylinder / box / sphere / mesh convex hull) by Minkowski
+ *     portal refinement (libccd's MPR, one contact per pair, the algorithm
+ *     MuJoCo's general convex path used before nativeccd) + plane-convex.
  *
  * PARITY STATUS: MuJoCo/MJX are not importable or buildable here
  * (SURVEY.md §0.2, §8c), so the physics restatement is pinned only by the
@@ -55,6 +63,7 @@ typedef struct {
   /* velocity-dependent */
   double cvel[NB][6], cdof_dot[NV][6];
   double qfrc_bias[NV], qfrc_passive[NV], qfrc_smooth[NV], qacc_smooth[NV];
+  double qfrc_actuator[NV], qfrc_constraint[NV], efc_force[MAXEFC];
   /* contacts (all slots) */
   int ncon;
   ocontact con[MAXCON];
@@ -388,6 +397,11 @@ static void passive(const mpcr_model_t* m, odata* d) {
   for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] = 0;
   if (m->disableflags & MPCR_DSBL_PASSIVE) return;
   for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] = -m->dof_damping[i] * d->qvel[i];
+  /* joint springs (hinge / slide): -stiffness (q - springref) */
+  for (int j = 0; j < m->njnt; j++) {
+    if (m->jnt_stiffness[j] == 0 || (m->jnt_type[j] != MPCR_JNT_HINGE && m->jnt_type[j] != MPCR_JNT_SLIDE)) continue;
+    d->qfrc_passive[m->jnt_dofadr[j]] -= m->jnt_stiffness[j] * (d->qpos[m->jnt_qposadr[j]] - m->jnt_springref[j]);
+  }
   /* gravity compensation: -gravity*mass*gravcomp applied at xipos */
   for (int b = 1; b < m->nbody; b++) {
     double gc = m->body_gravcomp[b];
@@ -423,6 +437,55 @@ static void rne(const mpcr_model_t* m, odata* d) {
     double v = 0;
     for (int k = 0; k < 6; k++) v += d->cdof[i][k] * cfrc[m->dof_bodyid[i]][k];
     d->qfrc_bias[i] = v;
+  }
+}
+
+/* actuation (mj_fwdActuation): force = gain ctrl + bias on the transmission
+   length / velocity, clamped, mapped through the moments; joint-level
+   actuator force ranges clamp the sum */
+static void actuation(const mpcr_model_t* m, odata* d) {
+  for (int i = 0; i < m->nv; i++) d->qfrc_actuator[i] = 0;
+  for (int a = 0; a < m->nu; a++) {
+    double len = 0, vel = 0;
+    for (int k = 0; k < m->act_ntrn[a]; k++) {
+      len += m->act_moment[a][k] * d->qpos[m->act_qadr[a][k]];
+      vel += m->act_moment[a][k] * d->qvel[m->act_dof[a][k]];
+    }
+    double ctrl = m->act_ctrl[a];
+    if (m->act_ctrllimited[a]) ctrl = clampd(ctrl, m->act_ctrlrange[a][0], m->act_ctrlrange[a][1]);
+    const double* g = m->act_gainprm[a];
+    const double* b = m->act_biasprm[a];
+    double gain = m->act_gaintype[a] == MPCR_GAIN_AFFINE ? g[0] + g[1] * len + g[2] * vel : g[0];
+    double bias = m->act_biastype[a] == MPCR_BIAS_AFFINE ? b[0] + b[1] * len + b[2] * vel : 0;
+    double f = gain * ctrl + bias;
+    if (m->act_forcelimited[a]) f = clampd(f, m->act_forcerange[a][0], m->act_forcerange[a][1]);
+    for (int k = 0; k < m->act_ntrn[a]; k++) d->qfrc_actuator[m->act_dof[a][k]] += m->act_moment[a][k] * f;
+  }
+  for (int j = 0; j < m->njnt; j++) {
+    if (!m->jnt_actfrclimited[j]) continue;
+    int v = m->jnt_dofadr[j];
+    d->qfrc_actuator[v] = clampd(d->qfrc_actuator[v], m->jnt_actfrcrange[j][0], m->jnt_actfrcrange[j][1]);
+  }
+}
+
+/* implicitfast velocity derivative of the smooth force (mjd_smooth_vel
+   without the RNE term): -damping on the diagonal + sum_a dforce/dvel m m^T */
+static void qderiv(const mpcr_model_t* m, double D[NV][NV]) {
+  for (int i = 0; i < m->nv; i++)
+    for (int j = 0; j < m->nv; j++) D[i][j] = i == j ? -m->dof_damping[i] : 0;
+  if (m->disableflags & MPCR_DSBL_PASSIVE)
+    for (int i = 0; i < m->nv; i++) D[i][i] = 0;
+  for (int a = 0; a < m->nu; a++) {
+    double dv = 0;
+    if (m->act_biastype[a] == MPCR_BIAS_AFFINE) dv += m->act_biasprm[a][2];
+    if (m->act_gaintype[a] == MPCR_GAIN_AFFINE) {
+      double ctrl = m->act_ctrl[a];
+      if (m->act_ctrllimited[a]) ctrl = clampd(ctrl, m->act_ctrlrange[a][0], m->act_ctrlrange[a][1]);
+      dv += m->act_gainprm[a][2] * ctrl;
+    }
+    for (int k = 0; k < m->act_ntrn[a]; k++)
+      for (int l = 0; l < m->act_ntrn[a]; l++)
+        D[m->act_dof[a][k]][m->act_dof[a][l]] += dv * m->act_moment[a][k] * m->act_moment[a][l];
   }
 }
 
@@ -791,6 +854,249 @@ static void col_box_box(const odata* d, int ga, int gb, const double* ha, const 
   }
 }
 
+/* ---- general convex: support functions + Minkowski portal refinement ---- */
+
+/* world support point of geom g along dir (any length) */
+static void support(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3]) {
+  const double* R = d->geom_xmat[g];
+  const double* sz = m->geom_size[g];
+  double l[3], p[3] = {0, 0, 0};
+  mulmtv(l, R, dir);
+  switch (m->geom_type[g]) {
+    case MPCR_GEOM_SPHERE: {
+      double n = norm3(l);
+      if (n > 0) for (int k = 0; k < 3; k++) p[k] = sz[0] * l[k] / n;
+      break;
+    }
+    case MPCR_GEOM_CAPSULE: {
+      double n = norm3(l);
+      if (n > 0) for (int k = 0; k < 3; k++) p[k] = sz[0] * l[k] / n;
+      p[2] += l[2] >= 0 ? sz[1] : -sz[1];
+      break;
+    }
+    case MPCR_GEOM_CYLINDER: {
+      double r = sqrt(l[0] * l[0] + l[1] * l[1]);
+      if (r > 0) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
+      p[2] = l[2] >= 0 ? sz[1] : -sz[1];
+      break;
+    }
+    case MPCR_GEOM_BOX:
+      for (int k = 0; k < 3; k++) p[k] = l[k] >= 0 ? sz[k] : -sz[k];
+      break;
+    case MPCR_GEOM_MESH: { /* steepest-ascent hill climbing on the hull graph from its first vertex */
+      int v = m->geom_hulladr[g];
+      double best = dot3(m->hull_vert[v], l);
+      for (;;) {
+        int nb = v;
+        for (int k = m->hull_adjadr[v]; k < m->hull_adjadr[v] + m->hull_adjnum[v]; k++) {
+          int u = m->hull_adj[k];
+          double du = dot3(m->hull_vert[u], l);
+          if (du > best) { best = du; nb = u; }
+        }
+        if (nb == v) break;
+        v = nb;
+      }
+      memcpy(p, m->hull_vert[v], sizeof(p));
+      break;
+    }
+    default: break;
+  }
+  mulmv(out, R, p);
+  for (int k = 0; k < 3; k++) out[k] += d->geom_xpos[g][k];
+}
+
+typedef struct { double v[3], a[3], b[3]; } mpt; /* v = a - b */
+
+#define MPR_TOL 1e-6
+#define MPR_ITER 50
+#define MPR_EPS 2.220446049250313e-16
+static int iszero(double x) { return fabs(x) < MPR_EPS; }
+
+static void msupport(const mpcr_model_t* m, const odata* d, int g1, int g2, const double dir[3], mpt* o) {
+  double nd[3] = {-dir[0], -dir[1], -dir[2]};
+  support(m, d, g1, dir, o->a);
+  support(m, d, g2, nd, o->b);
+  for (int k = 0; k < 3; k++) o->v[k] = o->a[k] - o->b[k];
+}
+static void normalize3(double v[3]) {
+  double n = norm3(v);
+  if (n > 0) for (int k = 0; k < 3; k++) v[k] /= n;
+}
+static void portal_dir(const mpt p[4], double dir[3]) {
+  double a[3], b[3];
+  for (int k = 0; k < 3; k++) { a[k] = p[2].v[k] - p[1].v[k]; b[k] = p[3].v[k] - p[1].v[k]; }
+  cross3(dir, a, b);
+  normalize3(dir);
+}
+static int reach_tol(const mpt p[4], const mpt* v4, const double dir[3]) {
+  double d4 = dot3(v4->v, dir);
+  double t = fmin(d4 - dot3(p[1].v, dir), fmin(d4 - dot3(p[2].v, dir), d4 - dot3(p[3].v, dir)));
+  return fabs(t - MPR_TOL) < MPR_EPS || t < MPR_TOL;
+}
+static void expand(mpt p[4], const mpt* v4) {
+  double x[3];
+  cross3(x, v4->v, p[0].v);
+  if (dot3(p[1].v, x) > 0) {
+    if (dot3(p[2].v, x) > 0) p[1] = *v4; else p[3] = *v4;
+  } else {
+    if (dot3(p[3].v, x) > 0) p[2] = *v4; else p[1] = *v4;
+  }
+}
+/* closest point of triangle (a, b, c) to the origin (Ericson 5.1.5) */
+static void tri_closest(const double a[3], const double b[3], const double c[3], double out[3]) {
+  double ab[3], ac[3], ap[3], bp[3], cp[3];
+  for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; ap[k] = -a[k]; bp[k] = -b[k]; cp[k] = -c[k]; }
+  double d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { memcpy(out, a, 3 * sizeof(double)); return; }
+  double d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { memcpy(out, b, 3 * sizeof(double)); return; }
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    double t = d1 / (d1 - d3);
+    for (int k = 0; k < 3; k++) out[k] = a[k] + t * ab[k];
+    return;
+  }
+  double d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0 && d5 <= d6) { memcpy(out, c, 3 * sizeof(double)); return; }
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    double t = d2 / (d2 - d6);
+    for (int k = 0; k < 3; k++) out[k] = a[k] + t * ac[k];
+    return;
+  }
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int k = 0; k < 3; k++) out[k] = b[k] + t * (c[k] - b[k]);
+    return;
+  }
+  double den = 1 / (va + vb + vc), v = vb * den, w = vc * den;
+  for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
+}
+
+/* MPR penetration of geoms g1, g2: 1 and (depth, dir from g1 to g2, pos) if
+   they overlap, else 0 */
+static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* depth, double dir[3], double pos[3]) {
+  mpt p[4], v4;
+  double va[3], vb[3], dd;
+  /* phase 1: portal discovery; v0 = interior point of the difference */
+  for (int k = 0; k < 3; k++) {
+    p[0].a[k] = d->geom_xpos[g1][k];
+    p[0].b[k] = d->geom_xpos[g2][k];
+    p[0].v[k] = p[0].a[k] - p[0].b[k];
+  }
+  if (iszero(p[0].v[0]) && iszero(p[0].v[1]) && iszero(p[0].v[2])) p[0].v[0] += 10 * MPR_EPS;
+  for (int k = 0; k < 3; k++) dir[k] = -p[0].v[k];
+  normalize3(dir);
+  msupport(m, d, g1, g2, dir, &p[1]);
+  dd = dot3(p[1].v, dir);
+  if (iszero(dd) || dd < 0) return 0;
+  cross3(dir, p[0].v, p[1].v);
+  if (iszero(dot3(dir, dir))) {
+    for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p[1].a[k] + p[1].b[k]);
+    if (iszero(p[1].v[0]) && iszero(p[1].v[1]) && iszero(p[1].v[2])) { /* touching at v1 */
+      *depth = 0;
+      dir[0] = dir[1] = dir[2] = 0;
+    } else { /* origin on the v0-v1 segment */
+      memcpy(dir, p[1].v, sizeof(double) * 3);
+      *depth = norm3(dir);
+      normalize3(dir);
+    }
+    return 1;
+  }
+  normalize3(dir);
+  msupport(m, d, g1, g2, dir, &p[2]);
+  dd = dot3(p[2].v, dir);
+  if (iszero(dd) || dd < 0) return 0;
+  for (int k = 0; k < 3; k++) { va[k] = p[1].v[k] - p[0].v[k]; vb[k] = p[2].v[k] - p[0].v[k]; }
+  cross3(dir, va, vb);
+  normalize3(dir);
+  if (dot3(dir, p[0].v) > 0) {
+    mpt t = p[1]; p[1] = p[2]; p[2] = t;
+    for (int k = 0; k < 3; k++) dir[k] = -dir[k];
+  }
+  for (int guard = 0;; guard++) {
+    if (guard > MPR_ITER) return 0;
+    msupport(m, d, g1, g2, dir, &p[3]);
+    dd = dot3(p[3].v, dir);
+    if (iszero(dd) || dd < 0) return 0;
+    int cont = 0;
+    cross3(va, p[1].v, p[3].v);
+    dd = dot3(va, p[0].v);
+    if (dd < 0 && !iszero(dd)) { p[2] = p[3]; cont = 1; }
+    if (!cont) {
+      cross3(va, p[3].v, p[2].v);
+      dd = dot3(va, p[0].v);
+      if (dd < 0 && !iszero(dd)) { p[1] = p[3]; cont = 1; }
+    }
+    if (!cont) break;
+    for (int k = 0; k < 3; k++) { va[k] = p[1].v[k] - p[0].v[k]; vb[k] = p[2].v[k] - p[0].v[k]; }
+    cross3(dir, va, vb);
+    normalize3(dir);
+  }
+  /* phase 2: refine until the portal encloses the origin */
+  for (int it = 0;; it++) {
+    portal_dir(p, dir);
+    dd = dot3(dir, p[1].v);
+    if (iszero(dd) || dd > 0) break;
+    msupport(m, d, g1, g2, dir, &v4);
+    dd = dot3(v4.v, dir);
+    if (!(iszero(dd) || dd > 0) || reach_tol(p, &v4, dir) || it > MPR_ITER) return 0;
+    expand(p, &v4);
+  }
+  /* phase 3: penetration depth / direction / position */
+  for (int it = 0;; it++) {
+    portal_dir(p, dir);
+    msupport(m, d, g1, g2, dir, &v4);
+    if (reach_tol(p, &v4, dir) || it > MPR_ITER) {
+      double w[3];
+      tri_closest(p[1].v, p[2].v, p[3].v, w);
+      *depth = norm3(w);
+      if (iszero(*depth)) dir[0] = dir[1] = dir[2] = 0;
+      else for (int k = 0; k < 3; k++) dir[k] = w[k] / *depth;
+      /* barycentric position of the origin in the tetrahedron (libccd findPos) */
+      double pd[3], b[4], x[3];
+      portal_dir(p, pd);
+      cross3(x, p[2].v, p[3].v); b[0] = dot3(x, p[1].v);
+      cross3(x, p[3].v, p[2].v); b[1] = dot3(x, p[0].v);
+      cross3(x, p[0].v, p[1].v); b[2] = dot3(x, p[3].v);
+      cross3(x, p[2].v, p[1].v); b[3] = dot3(x, p[0].v);
+      double sum = b[0] + b[1] + b[2] + b[3];
+      if (iszero(sum) || sum < 0) {
+        b[0] = 0;
+        cross3(x, p[2].v, p[3].v); b[1] = dot3(x, pd);
+        cross3(x, p[3].v, p[1].v); b[2] = dot3(x, pd);
+        cross3(x, p[1].v, p[2].v); b[3] = dot3(x, pd);
+        sum = b[1] + b[2] + b[3];
+      }
+      for (int k = 0; k < 3; k++) {
+        double pa = 0, pb = 0;
+        for (int i = 0; i < 4; i++) { pa += b[i] * p[i].a[k]; pb += b[i] * p[i].b[k]; }
+        pos[k] = 0.5 * (pa + pb) / sum;
+      }
+      return 1;
+    }
+    expand(p, &v4);
+  }
+}
+
+static void col_convex(const mpcr_model_t* m, const odata* d, int g1, int g2, ocontact* out) {
+  double depth, n[3], pos[3];
+  if (!mpr(m, d, g1, g2, &depth, n, pos)) return;
+  if (n[0] == 0 && n[1] == 0 && n[2] == 0) n[2] = 1; /* touching: any frame */
+  set_contact(out, -depth, pos, n);
+}
+
+static void col_plane_convex(const mpcr_model_t* m, const odata* d, int gp, int g, ocontact* out) {
+  const double* R = d->geom_xmat[gp];
+  double n[3] = {R[2], R[5], R[8]}, nn[3] = {-R[2], -R[5], -R[8]}, p[3], pos[3];
+  support(m, d, g, nn, p);
+  double dist = (p[0] - d->geom_xpos[gp][0]) * n[0] + (p[1] - d->geom_xpos[gp][1]) * n[1] +
+                (p[2] - d->geom_xpos[gp][2]) * n[2];
+  for (int k = 0; k < 3; k++) pos[k] = p[k] - 0.5 * dist * n[k];
+  set_contact(out, dist, pos, n);
+}
+
 static void collision(const mpcr_model_t* m, odata* d) {
   d->ncon = m->ncon;
   for (int p = 0; p < m->npair; p++) {
@@ -814,6 +1120,8 @@ static void collision(const mpcr_model_t* m, odata* d) {
       case MPCR_COL_CAPSULE_CAPSULE: col_capsule_capsule(d, g1, g2, s1, s2, out); break;
       case MPCR_COL_CAPSULE_BOX: col_capsule_box(d, g1, g2, s1, s2, out); break;
       case MPCR_COL_BOX_BOX: col_box_box(d, g1, g2, s1, s2, m->pair_margin[p] - m->pair_gap[p], out); break;
+      case MPCR_COL_CONVEX: col_convex(m, d, g1, g2, out); break;
+      case MPCR_COL_PLANE_CONVEX: col_plane_convex(m, d, g1, g2, out); break;
       default: break;
     }
     for (int s = 0; s < m->pair_ncon[p]; s++) {
@@ -858,9 +1166,27 @@ static void make_constraint(const mpcr_model_t* m, odata* d) {
   int nv = m->nv;
   d->nefc = 0;
   d->efc_trunc = 0;
-  /* joint equality: q1 - qpos0_1 = poly(q2 - qpos0_2) */
+  /* equalities in model order.  connect: 3 rows, anchor1 (body1) - anchor2
+     (body2) in world; joint: q1 - qpos0_1 = poly(q2 - qpos0_2) */
   if (!(m->disableflags & MPCR_DSBL_EQUALITY))
     for (int e = 0; e < m->neq; e++) {
+      if (m->eq_type[e] == MPCR_EQ_CONNECT) {
+        int b1 = m->eq_obj1[e], b2 = m->eq_obj2[e];
+        double p1[3], p2[3], t[3], j1[3][NV], j2[3][NV];
+        mulmv(t, d->xmat[b1], m->eq_data[e]);
+        for (int k = 0; k < 3; k++) p1[k] = d->xpos[b1][k] + t[k];
+        mulmv(t, d->xmat[b2], m->eq_data[e] + 3);
+        for (int k = 0; k < 3; k++) p2[k] = d->xpos[b2][k] + t[k];
+        jac_point(m, d, b1, p1, j1);
+        jac_point(m, d, b2, p2, j2);
+        double diag = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+        for (int k = 0; k < 3; k++) {
+          int r = add_row(m, d, 1, p1[k] - p2[k], 0, diag, m->eq_solref[e], m->eq_solimp[e]);
+          if (r < 0) continue;
+          for (int i = 0; i < nv; i++) d->efc_J[r][i] = j1[k][i] - j2[k][i];
+        }
+        continue;
+      }
       if (m->eq_type[e] != MPCR_EQ_JOINT) continue;
       int j1 = m->eq_obj1[e], j2 = m->eq_obj2[e];
       const double* c = m->eq_data[e];
@@ -999,7 +1325,11 @@ static lspt ls_eval(const odata* d, const double qg[3], const double* jar, const
 
 static void solve(const mpcr_model_t* m, odata* d) {
   int nv = m->nv, nefc = d->nefc;
-  if (nefc == 0) { memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv); return; }
+  if (nefc == 0) {
+    memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
+    for (int i = 0; i < nv; i++) d->qfrc_constraint[i] = 0;
+    return;
+  }
   double Ma[NV], jar[MAXEFC], qacc[NV];
   /* warm start: the better of qacc_warmstart and qacc_smooth */
   if (!(m->disableflags & MPCR_DSBL_WARMSTART)) {
@@ -1089,6 +1419,13 @@ static void solve(const mpcr_model_t* m, odata* d) {
     cost = solver_cost(m, d, qacc, Ma, jar);
   }
   memcpy(d->qacc, qacc, sizeof(double) * nv);
+  /* efc_force / qfrc_constraint at the final acceleration */
+  for (int i = 0; i < nv; i++) d->qfrc_constraint[i] = 0;
+  for (int r = 0; r < nefc; r++) {
+    double f = (d->efc_eq[r] || jar[r] < 0) ? -d->efc_D[r] * jar[r] : 0;
+    d->efc_force[r] = f;
+    for (int i = 0; i < nv; i++) d->qfrc_constraint[i] += d->efc_J[r][i] * f;
+  }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1102,15 +1439,29 @@ static void forward(const mpcr_model_t* m, odata* d) {
   com_vel(m, d);
   passive(m, d);
   rne(m, d);
+  actuation(m, d);
   make_constraint(m, d);
-  for (int i = 0; i < m->nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i];
+  for (int i = 0; i < m->nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
   chol_solve(d->qacc_smooth, d->L, d->qfrc_smooth, m->nv);
   solve(m, d);
 }
 
 static void euler(const mpcr_model_t* m, odata* d) {
   double dt = m->timestep;
-  for (int i = 0; i < m->nv; i++) d->qvel[i] += dt * d->qacc[i];
+  if (m->integrator == MPCR_INT_IMPLICITFAST) {
+    /* mj_implicitSkip: (M - dt qDeriv) qacc_i = qfrc_smooth + qfrc_constraint */
+    double D[NV][NV], A[NV][NV], L[NV][NV], f[NV] = {0}, acc[NV];
+    qderiv(m, D);
+    for (int i = 0; i < m->nv; i++) {
+      for (int j = 0; j < m->nv; j++) A[i][j] = d->M[i][j] - dt * D[i][j];
+      f[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
+    }
+    chol(L, A, m->nv);
+    chol_solve(acc, L, f, m->nv);
+    for (int i = 0; i < m->nv; i++) d->qvel[i] += dt * acc[i];
+  } else {
+    for (int i = 0; i < m->nv; i++) d->qvel[i] += dt * d->qacc[i];
+  }
   for (int j = 0; j < m->njnt; j++) {
     int a = m->jnt_qposadr[j], v = m->jnt_dofadr[j];
     if (m->jnt_type[j] == MPCR_JNT_FREE) {

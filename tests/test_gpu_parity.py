@@ -76,7 +76,7 @@ def test_parity_small(torch_cuda, name, layout):
         assert np.abs(g["slots"] - o["slots"]).max() < 1e-3
 
 
-@pytest.mark.parametrize("name", ["planner_scene", "scene_mjx", "ur5e_hande_mjx"])
+@pytest.mark.parametrize("name", ["planner_scene", "scene_mjx", "ur5e_hande_mjx", "dual_arm"])
 def test_parity_projected_h50(torch_cuda, name):
     """Realistic samples (projected to |thetadot| <= 0.8): arm/table/box contacts occur."""
     torch = torch_cuda
@@ -191,3 +191,30 @@ def test_compute_cem_dropin(torch_cuda):
     # the same call is deterministic (fixed key, SBP/mjx_planner.py:388)
     out2 = p.compute_cem(np.zeros(p.nvar), Q0, np.zeros(6), np.zeros(6), PT, QT)
     np.testing.assert_array_equal(out2[0], cost)
+
+
+def test_dual_arm_c4_properties(torch_cuda):
+    """C4's per-GPU shard (4096 x 100, dual arm: implicitfast, actuators,
+    connect equalities, convex-hull contacts): finite, deterministic, the
+    gripper's permanently touching linkage contacts are found (constraint rows
+    every step), no row truncation; a 32-candidate sample matches the oracle."""
+    torch = torch_cuda
+    n, H = 4096, 100
+    m = models.load("dual_arm", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
+    e = Engine(m, H, n, Pd)
+    st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    a = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, status=st).clone()
+    b = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.isfinite(a).all()
+    s_ = st.cpu().numpy()
+    assert int((s_ & 1).sum()) == 0
+    rows_per_step = (s_ >> 8) / H
+    assert rows_per_step.min() >= 8  # 8 equality rows + the linkage contacts
+    sel = np.arange(0, n, n // 32)
+    td = np.einsum("tk,njk->njt", Pd, xi.cpu().numpy()[sel].reshape(-1, 6, 11).astype(np.float64)).reshape(-1, 6 * H)
+    o = oracle.rollout(m, td, Q0, W, PT, QT, want_theta=False)["cost4"]
+    rel = np.abs(a.cpu().numpy()[sel, 0] - o[:, 0]) / np.abs(o[:, 0])
+    assert (rel < TOL).mean() >= 0.9, np.sort(rel)[-4:]

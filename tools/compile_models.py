@@ -17,6 +17,7 @@ SCENES = {
     "planner_scene": "sampling_based_planner/ur5e_hande_mjx/scene.xml",
     "ur5e_hande_mjx": "universal_robots_ur5e/ur5e_1_robotiq_hande_mjx.xml",
     "scene_mjx": "universal_robots_ur5e/scene_mjx.xml",
+    "dual_arm": "universal_robots_ur5e/dual_arm_gripper_scene.xml",
 }
 
 
