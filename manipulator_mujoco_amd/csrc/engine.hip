@@ -43,7 +43,7 @@ struct mpcr_engine {
   // convex hulls (dual-arm class)
   float4* d_hull_vert = nullptr;
   int2* d_hull_info = nullptr;
-  int* d_hull_adj = nullptr;
+  float4* d_hull_adjv = nullptr;
   bool wide = false;  // kernel variant: rollout_kernel<32, 32, 72, true>
 };
 
@@ -370,6 +370,13 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
   if (m.npair > DX_NP) return fail(MPCR_EMODEL, "too many pairs");
   if (m.nslot > DX_NSLOT) return fail(MPCR_EMODEL, "%d masked slots > %d", m.nslot, DX_NSLOT);
   d.npair = m.npair;
+  d.cvx_base = m.npair;
+  for (int p = m.npair - 1; p >= 0; p--)
+    if (m.pair_func[p] >= MPCR_COL_CONVEX) d.cvx_base = p;
+  for (int p = d.cvx_base; p < m.npair; p++)
+    if (m.pair_func[p] < MPCR_COL_CONVEX) return fail(MPCR_EMODEL, "convex pairs must be sorted last");
+  if (m.npair - d.cvx_base > 512) return fail(MPCR_EMODEL, "%d general-convex pairs > 512", m.npair - d.cvx_base);
+  if (m.nhullv > 32767) return fail(MPCR_EMODEL, "hull vertex table exceeds 16-bit hints");
   for (int p = 0; p < m.npair; p++) {
     int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
     d.pair_g1[p] = gmap[g1];
@@ -521,23 +528,30 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     const mpcr_model_t& h = e->host;
     std::vector<float4> hv(h.nhullv);
     std::vector<int2> hi(h.nhullv);
-    std::vector<int> ha(h.hull_adj, h.hull_adj + h.nhulla);
+    std::vector<float4> ha(h.nhulla);
+    for (int k = 0; k < h.nhulla; k++) {
+      const int u = h.hull_adj[k];
+      int bits = u;
+      float fu;
+      std::memcpy(&fu, &bits, 4);
+      ha[k] = make_float4((float)h.hull_vert[u][0], (float)h.hull_vert[u][1], (float)h.hull_vert[u][2], fu);
+    }
     for (int v = 0; v < h.nhullv; v++) {
       hv[v] = make_float4((float)h.hull_vert[v][0], (float)h.hull_vert[v][1], (float)h.hull_vert[v][2], 0.f);
       hi[v] = make_int2(h.hull_adjadr[v], h.hull_adjnum[v]);
     }
     if (hipMalloc(&e->d_hull_vert, sizeof(float4) * hv.size()) != hipSuccess ||
         hipMalloc(&e->d_hull_info, sizeof(int2) * hi.size()) != hipSuccess ||
-        hipMalloc(&e->d_hull_adj, sizeof(int) * (ha.size() ? ha.size() : 1)) != hipSuccess ||
+        hipMalloc(&e->d_hull_adjv, sizeof(float4) * (ha.size() ? ha.size() : 1)) != hipSuccess ||
         hipMemcpy(e->d_hull_vert, hv.data(), sizeof(float4) * hv.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(e->d_hull_info, hi.data(), sizeof(int2) * hi.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        (ha.size() && hipMemcpy(e->d_hull_adj, ha.data(), sizeof(int) * ha.size(), hipMemcpyHostToDevice) != hipSuccess)) {
+        (ha.size() && hipMemcpy(e->d_hull_adjv, ha.data(), sizeof(float4) * ha.size(), hipMemcpyHostToDevice) != hipSuccess)) {
       mpcr_engine_free(e);
       return fail(MPCR_ENOMEM, "hull upload failed");
     }
     e->dev.hull_vert = e->d_hull_vert;
     e->dev.hull_info = e->d_hull_info;
-    e->dev.hull_adj = e->d_hull_adj;
+    e->dev.hull_adjv = e->d_hull_adjv;
   }
   const int nc = e->host.nctrl;
   const size_t in_cols = (size_t)nc * (horizon > nbasis ? horizon : nbasis);
@@ -575,7 +589,7 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_idx);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
-  (void)hipFree(e->d_hull_adj);
+  (void)hipFree(e->d_hull_adjv);
   delete e;
 }
 
@@ -849,7 +863,10 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
-  hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
+  if (e->wide)
+    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
+  else
+    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(phases16, d_prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(d_prof);

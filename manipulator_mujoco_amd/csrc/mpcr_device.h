@@ -36,6 +36,7 @@ struct DevModel {
   int nhdof;  // number of dofs, rounded to the solve width
   int nu, neqrow, integrator;  // actuators, equality rows, 0 Euler / 3 implicitfast
   int has_spring;
+  int cvx_base;  // first general-convex pair (pairs are sorted by function)
   float timestep, tolerance, ls_tolerance, meaninertia;
   float gravity[4];
   float tcp_pos[4];  // tcp site position in tcp_body frame
@@ -109,7 +110,7 @@ struct DevModel {
   int geom_hulladr[DX_NG];
   const float4* hull_vert;  // xyz, w unused
   const int2* hull_info;    // (adjacency start, count) per vertex
-  const int* hull_adj;
+  const float4* hull_adjv;  // neighbour xyz | neighbour index (bits in w): one load per neighbour
 
   int ctrl_qposadr[DX_NCTRL], ctrl_dofadr[DX_NCTRL];
 };

@@ -64,6 +64,8 @@ struct __align__(16) SmemT {
   static constexpr int LOG_NVW = NVW_ == 32 ? 5 : 4;
   static constexpr bool WIDE = NVW_ == 32;  // dual-arm class: equalities, actuators, convex hulls
   static constexpr int NQW = WIDE ? DX_NQ : 24, NEQP = WIDE ? DX_NEQ : 1, NACT = WIDE ? DX_NU : 1;
+  static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
+  static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
   // ---- persistent across the step ----
   float xi[DX_NCTRL * 16];
   float qpos[NQW];
@@ -82,7 +84,9 @@ struct __align__(16) SmemT {
   float par[PAR_N];       // q0 | w | ptgt | qtgt (normalised)
   float eqp[NEQP][2][4];  // connect anchors in world (body1, body2)
   float actf[NACT];       // actuator forces
-  int ncon, nefc, pad_[2];
+  int cvx[CVXN];
+  short hint[NHINT][2];
+  int ncon, nefc, ncvx, pad_;
   // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the
   //      contact / constraint arrays (collision .. Newton) ----
   union {
@@ -177,6 +181,7 @@ __device__ __forceinline__ int wscan_excl(int v, int& total) {
   return pre;
 }
 __device__ __forceinline__ void sync() { __syncthreads(); }
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
 // ---------------------------------------------------------------------------
 // small vector math
@@ -382,14 +387,22 @@ __device__ __forceinline__ float point_box(const float p[3], const float h[3], f
 // refinement, the same algorithm and tolerances as the oracle's mpr()
 // (libccd MPR; one penetration contact per pair)
 
-constexpr float kMprTol = 1e-6f;
-constexpr int kMprIter = 50;
+#ifndef MPCR_MPR_TOL
+#define MPCR_MPR_TOL 1e-6f
+#endif
+#ifndef MPCR_MPR_ITER
+#define MPCR_MPR_ITER 50
+#endif
+constexpr float kMprTol = MPCR_MPR_TOL;  // MuJoCo's ccd_tolerance / ccd_iterations defaults
+constexpr int kMprIter = MPCR_MPR_ITER;
 constexpr float kMprEps = 1.1920929e-07f;
 __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
 
+// hint: hull vertex the previous query on this geom ended at (-1: none); the
+// climb starts there (successive MPR directions are close)
 template <class S>
 __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
-                                             float out[3]) {
+                                             float out[3], int& hint) {
   const float* R = s.gxmat[g];
   const float* sz = m->geom_size[g];
   float l[3], p[3] = {0.f, 0.f, 0.f};
@@ -408,23 +421,23 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
     p[1] = l[1] >= 0.f ? sz[1] : -sz[1];
     p[2] = l[2] >= 0.f ? sz[2] : -sz[2];
   } else if (type == 7) {  // mesh hull: steepest ascent on the vertex graph from its first vertex
-    int v = m->geom_hulladr[g];
+    int v = hint >= 0 ? hint : m->geom_hulladr[g];
     float4 hv = m->hull_vert[v];
     float best = hv.x * l[0] + hv.y * l[1] + hv.z * l[2];
     for (int guard = 0; guard < 4096; guard++) {
       const int2 info = m->hull_info[v];
-      int nb = v;
+      int nb = -1;
+#pragma unroll 4
       for (int k = info.x; k < info.x + info.y; k++) {
-        const int u = m->hull_adj[k];
-        const float4 w = m->hull_vert[u];
+        const float4 w = m->hull_adjv[k];
         const float du = w.x * l[0] + w.y * l[1] + w.z * l[2];
-        if (du > best) { best = du; nb = u; }
+        if (du > best) { best = du; nb = __float_as_int(w.w); hv = w; }
       }
-      if (nb == v) break;
+      if (nb < 0) break;
       v = nb;
     }
-    hv = m->hull_vert[v];
     p[0] = hv.x; p[1] = hv.y; p[2] = hv.z;
+    hint = v;
   }
   mv(out, R, p);
   out[0] += s.gxpos[g][0]; out[1] += s.gxpos[g][1]; out[2] += s.gxpos[g][2];
@@ -434,10 +447,10 @@ struct MprPt { float v[3], a[3], b[3]; };
 
 template <class S>
 __device__ __forceinline__ void mpr_support(const DevModel* __restrict__ m, const S& s, int g1, int g2,
-                                            const float dir[3], MprPt& o) {
+                                            const float dir[3], MprPt& o, int (&hint)[2]) {
   const float nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support_geom(m, s, g1, dir, o.a);
-  support_geom(m, s, g2, nd, o.b);
+  support_geom(m, s, g1, dir, o.a, hint[0]);
+  support_geom(m, s, g2, nd, o.b, hint[1]);
   o.v[0] = o.a[0] - o.b[0]; o.v[1] = o.a[1] - o.b[1]; o.v[2] = o.a[2] - o.b[2];
 }
 __device__ __forceinline__ void nrm3(float v[3]) {
@@ -501,7 +514,7 @@ __device__ __forceinline__ void tri_closest(const float a[3], const float b[3], 
 // returns true and (depth, dir g1 -> g2, pos) when the geoms overlap
 template <class S>
 __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int g2, float& depth, float dir[3],
-                         float pos[3]) {
+                         float pos[3], int (&hint)[2]) {
   MprPt p[4], v4;
   float va[3], vb[3], dd;
 #pragma unroll
@@ -513,7 +526,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   if (mpr_zero(p[0].v[0]) && mpr_zero(p[0].v[1]) && mpr_zero(p[0].v[2])) p[0].v[0] += 10.f * kMprEps;
   dir[0] = -p[0].v[0]; dir[1] = -p[0].v[1]; dir[2] = -p[0].v[2];
   nrm3(dir);
-  mpr_support(m, s, g1, g2, dir, p[1]);
+  mpr_support(m, s, g1, g2, dir, p[1], hint);
   dd = dot3(p[1].v, dir);
   if (mpr_zero(dd) || dd < 0.f) return false;
   cross(dir, p[0].v, p[1].v);
@@ -531,7 +544,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     return true;
   }
   nrm3(dir);
-  mpr_support(m, s, g1, g2, dir, p[2]);
+  mpr_support(m, s, g1, g2, dir, p[2], hint);
   dd = dot3(p[2].v, dir);
   if (mpr_zero(dd) || dd < 0.f) return false;
 #pragma unroll
@@ -544,7 +557,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   }
   for (int guard = 0;; guard++) {
     if (guard > kMprIter) return false;
-    mpr_support(m, s, g1, g2, dir, p[3]);
+    mpr_support(m, s, g1, g2, dir, p[3], hint);
     dd = dot3(p[3].v, dir);
     if (mpr_zero(dd) || dd < 0.f) return false;
     bool cont = false;
@@ -566,14 +579,14 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     mpr_dir(p, dir);
     dd = dot3(dir, p[1].v);
     if (mpr_zero(dd) || dd > 0.f) break;
-    mpr_support(m, s, g1, g2, dir, v4);
+    mpr_support(m, s, g1, g2, dir, v4, hint);
     dd = dot3(v4.v, dir);
     if (!(mpr_zero(dd) || dd > 0.f) || mpr_reach(p, v4, dir) || it > kMprIter) return false;
     mpr_expand(p, v4);
   }
   for (int it = 0;; it++) {
     mpr_dir(p, dir);
-    mpr_support(m, s, g1, g2, dir, v4);
+    mpr_support(m, s, g1, g2, dir, v4, hint);
     if (mpr_reach(p, v4, dir) || it > kMprIter) break;
     mpr_expand(p, v4);
   }
@@ -788,9 +801,15 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
     return 2;
   }
   if constexpr (S::WIDE) {
+    // hull hill climbs start where this pair's previous step ended (the
+    // oracle keeps the same per-pair cache)
+    short* hp = const_cast<short*>(&s.hint[p - m->cvx_base][0]);
+    int hint[2] = {hp[0], hp[1]};
     if (func == 9) {  // general convex (MPR)
       float depth, n[3], pp[3];
-      if (mpr_lane(m, s, g1, g2, depth, n, pp)) {
+      const bool hit = mpr_lane(m, s, g1, g2, depth, n, pp, hint);
+      hp[0] = (short)hint[0]; hp[1] = (short)hint[1];
+      if (hit) {
         if (n[0] == 0.f && n[1] == 0.f && n[2] == 0.f) n[2] = 1.f;
         dist[0] = -depth;
 #pragma unroll
@@ -800,7 +819,8 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
     }
     if (func == 10) {  // plane - convex: deepest support point
       float n[3] = {R1[2], R1[5], R1[8]}, nn[3] = {-R1[2], -R1[5], -R1[8]}, q[3];
-      support_geom(m, s, g2, nn, q);
+      support_geom(m, s, g2, nn, q, hint[1]);
+      hp[1] = (short)hint[1];
       const float d = n[0] * (q[0] - x1[0]) + n[1] * (q[1] - x1[1]) + n[2] * (q[2] - x1[2]);
       dist[0] = d;
 #pragma unroll
@@ -1081,6 +1101,62 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
   sync();
 }
 
+// Per-lane contact bookkeeping after a narrow-phase pass: cost_c on the
+// robot-masked slots (SBP/mjx_planner.py:284-296) and ballot-compacted append
+// of the active contacts.  Must be called by all lanes (two barriers).
+template <class S>
+__device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S& s, const RolloutArgs& args, int b,
+                                              int t, int H, bool valid, int p, int nsl, const float dist[4],
+                                              const float pos[4][3], const float nrm[4][3], float& cost_c) {
+  int act = 0;
+  if (valid) {
+    const int sa = m->pair_slotadr[p];
+    if (sa >= 0) {
+      const int ns = m->pair_ncon[p];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        if (c < ns) {
+          const float d = dist[c];
+          if (d < 0.f) cost_c += 1.f;
+          if (t > 0) cost_c += fmaxf(s.cprev[sa + c] * (1.f - 0.005f) - d, 0.f);
+          s.cprev[sa + c] = d;
+          if (args.trace_slots) args.trace_slots[((size_t)b * H + t) * m->nslot + sa + c] = d;
+        }
+      }
+    }
+    if (!(m->disableflags & 16)) {
+      const float mg = m->pair_margin[p];
+#pragma unroll
+      for (int c = 0; c < 4; c++) act += (c < nsl && dist[c] < mg) ? 1 : 0;
+    }
+  }
+  int tot;
+  const int pre = wscan_excl(act, tot);
+  const int base = s.ncon;
+  if (act) {
+    const float mg = m->pair_margin[p];
+    int o = base + pre;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      if (c < nsl && dist[c] < mg) {
+        if (o < DX_MAXACT) {
+          float f[9];
+          make_frame(f, nrm[c]);
+          s.con_pos[o][0] = pos[c][0]; s.con_pos[o][1] = pos[c][1]; s.con_pos[o][2] = pos[c][2];
+#pragma unroll
+          for (int e = 0; e < 9; e++) s.con_frame[o][e] = f[e];
+          s.con_dist[o] = dist[c];
+          s.con_pair[o] = p;
+        }
+        o++;
+      }
+    }
+  }
+  sync();
+  if (lane_id() == 0) s.ncon = base + tot;
+  sync();
+}
+
 // ---------------------------------------------------------------------------
 // line search point (MJX-style, see oracle)
 
@@ -1192,6 +1268,9 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
   //      (plant mode: the caller's state, no init_pos override)
   if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
+  if constexpr (S::WIDE) {
+    for (int i = lane; i < S::NHINT; i += WAVE) { s.hint[i][0] = -1; s.hint[i][1] = -1; }
+  }
   const bool from_state = (args.plant & 1) != 0;
   for (int i = lane; i < S::NQW; i += WAVE)
     s.qpos[i] = i < m->nq ? (from_state ? args.state[ST_QPOS + i] : m->qpos_init[i]) : 0.f;
@@ -1634,7 +1713,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
     //      slots; active contacts compacted into the list; box-box pairs
     //      that pass the bounding-sphere cull are solved wave-cooperatively
-    if (lane == 0) s.ncon = 0;
+    if (lane == 0) { s.ncon = 0; s.ncvx = 0; }
     sync();
     for (int k = 0; k * WAVE < m->npair; k++) {
       const int p = lane + k * WAVE;
@@ -1643,64 +1722,48 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
       bool run = valid;
       if (valid && m->pair_slotadr[p] < 0) {
         const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
+        const float dx = s.gxpos[g2][0] - s.gxpos[g1][0], dy = s.gxpos[g2][1] - s.gxpos[g1][1],
+                    dz = s.gxpos[g2][2] - s.gxpos[g1][2];
         if (m->geom_type[g1] != 0) {
-          const float dx = s.gxpos[g2][0] - s.gxpos[g1][0], dy = s.gxpos[g2][1] - s.gxpos[g1][1],
-                      dz = s.gxpos[g2][2] - s.gxpos[g1][2];
           run = sqrtf(dx * dx + dy * dy + dz * dz) <= m->geom_rbound[g1] + m->geom_rbound[g2] + m->pair_margin[p];
+          if constexpr (S::WIDE) {  // box vs the other geom's bounding sphere (exact cull, as the oracle)
+            if (run && func == 9 && (m->geom_type[g1] == 6 || m->geom_type[g2] == 6)) {
+              const bool b1 = m->geom_type[g1] == 6;
+              const int gb = b1 ? g1 : g2;
+              const float sg = b1 ? 1.f : -1.f;
+              float d[3] = {sg * dx, sg * dy, sg * dz}, l[3];
+              mtv(l, s.gxmat[gb], d);
+              float o2 = 0.f;
+#pragma unroll
+              for (int k2 = 0; k2 < 3; k2++) {
+                const float e = fmaxf(fabsf(l[k2]) - m->geom_size[gb][k2], 0.f);
+                o2 += e * e;
+              }
+              run = sqrtf(o2) <= m->geom_rbound[b1 ? g2 : g1] + m->pair_margin[p];
+            }
+          }
+        } else if constexpr (S::WIDE) {  // plane vs the other geom's bounding sphere
+          const float* R1 = s.gxmat[g1];
+          run = R1[2] * dx + R1[5] * dy + R1[8] * dz <= m->geom_rbound[g2] + m->pair_margin[p];
         }
+      }
+      // general convex pairs (sorted last) that survive the cull are compacted
+      // into a list and solved 64 at a time below, instead of leaving most
+      // lanes of every 64-pair chunk idle behind a few MPR lanes
+      bool defer = false;
+      if constexpr (S::WIDE) {
+        defer = func >= 9;
+        const unsigned long long dm = __ballot(defer && run);
+        if (defer && run) s.cvx[s.ncvx + lanes_below(dm)] = p;
+        sync();
+        if (lane == 0) s.ncvx += __popcll(dm);
       }
       float dist[4] = {1e30f, 1e30f, 1e30f, 1e30f}, pos[4][3] = {}, nrm[4][3] = {};
       int nsl = 0;
-      if (run && func != 4) nsl = narrow_lane(m, s, p, dist, pos, nrm);
+      if (run && func != 4 && !defer) nsl = narrow_lane(m, s, p, dist, pos, nrm);
       STAMP(11);
       const unsigned long long bbm = __ballot(run && func == 4);
-      int act = 0;
-      if (valid && func != 4) {
-        const int sa = m->pair_slotadr[p];
-        if (sa >= 0) {
-          const int ns = m->pair_ncon[p];
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            if (c < ns) {
-              const float d = dist[c];
-              if (d < 0.f) cost_c += 1.f;
-              if (t > 0) cost_c += fmaxf(s.cprev[sa + c] * (1.f - 0.005f) - d, 0.f);
-              s.cprev[sa + c] = d;
-              if (args.trace_slots) args.trace_slots[((size_t)b * H + t) * m->nslot + sa + c] = d;
-            }
-          }
-        }
-        if (!(m->disableflags & 16)) {
-          const float mg = m->pair_margin[p];
-#pragma unroll
-          for (int c = 0; c < 4; c++) act += (c < nsl && dist[c] < mg) ? 1 : 0;
-        }
-      }
-      int tot;
-      const int pre = wscan_excl(act, tot);
-      const int base = s.ncon;
-      if (act) {
-        const float mg = m->pair_margin[p];
-        int o = base + pre;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          if (c < nsl && dist[c] < mg) {
-            if (o < DX_MAXACT) {
-              float f[9];
-              make_frame(f, nrm[c]);
-              s.con_pos[o][0] = pos[c][0]; s.con_pos[o][1] = pos[c][1]; s.con_pos[o][2] = pos[c][2];
-#pragma unroll
-              for (int e = 0; e < 9; e++) s.con_frame[o][e] = f[e];
-              s.con_dist[o] = dist[c];
-              s.con_pair[o] = p;
-            }
-            o++;
-          }
-        }
-      }
-      sync();
-      if (lane == 0) s.ncon = base + tot;
-      sync();
+      emit_contacts(m, s, args, b, t, H, valid && func != 4 && !defer, p, nsl, dist, pos, nrm, cost_c);
       STAMP(12);
       if (bbm && !(m->disableflags & 16)) {
         unsigned long long mm = bbm;
@@ -1708,6 +1771,21 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           const int q = __builtin_ctzll(mm);
           mm &= mm - 1;
           box_box_wave(m, s, k * WAVE + q, lane);
+        }
+      }
+      if constexpr (S::WIDE) {
+        if (s.ncvx > S::CVXN - WAVE || (k + 1) * WAVE >= m->npair) {  // flush (pair order is kept)
+          const int nc = s.ncvx;
+          for (int i0 = 0; i0 < nc; i0 += WAVE) {
+            const bool v = i0 + lane < nc;
+            const int pc = v ? s.cvx[i0 + lane] : 0;
+            float cd[4] = {1e30f, 1e30f, 1e30f, 1e30f}, cp[4][3] = {}, cn[4][3] = {};
+            const int cn_sl = v ? narrow_lane(m, s, pc, cd, cp, cn) : 0;
+            emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c);
+          }
+          sync();
+          if (lane == 0) s.ncvx = 0;
+          sync();
         }
       }
     }

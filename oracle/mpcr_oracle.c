@@ -73,7 +73,12 @@ typedef struct {
   double efc_aref[MAXEFC], efc_diag[MAXEFC], efc_vel[MAXEFC];
   double efc_solref[MAXEFC][2], efc_solimp[MAXEFC][5];
   int efc_trunc; /* constraint rows dropped for capacity (should stay 0) */
+  int hint[MPCR_MAX_PAIR][2]; /* hull-climb start per pair and side (-1: none), kept across steps */
 } odata;
+
+static void reset_hints(odata* d) {
+  for (int p = 0; p < MPCR_MAX_PAIR; p++) d->hint[p][0] = d->hint[p][1] = -1;
+}
 
 /* ------------------------------------------------------------------------ */
 /* small math                                                                */
@@ -856,8 +861,9 @@ static void col_box_box(const odata* d, int ga, int gb, const double* ha, const 
 
 /* ---- general convex: support functions + Minkowski portal refinement ---- */
 
-/* world support point of geom g along dir (any length) */
-static void support(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3]) {
+/* world support point of geom g along dir (any length); *hint: hull vertex the
+   previous query on this geom ended at (-1: none), where the climb starts */
+static void support(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint) {
   const double* R = d->geom_xmat[g];
   const double* sz = m->geom_size[g];
   double l[3], p[3] = {0, 0, 0};
@@ -884,7 +890,7 @@ static void support(const mpcr_model_t* m, const odata* d, int g, const double d
       for (int k = 0; k < 3; k++) p[k] = l[k] >= 0 ? sz[k] : -sz[k];
       break;
     case MPCR_GEOM_MESH: { /* steepest-ascent hill climbing on the hull graph from its first vertex */
-      int v = m->geom_hulladr[g];
+      int v = *hint >= 0 ? *hint : m->geom_hulladr[g];
       double best = dot3(m->hull_vert[v], l);
       for (;;) {
         int nb = v;
@@ -897,6 +903,7 @@ static void support(const mpcr_model_t* m, const odata* d, int g, const double d
         v = nb;
       }
       memcpy(p, m->hull_vert[v], sizeof(p));
+      *hint = v;
       break;
     }
     default: break;
@@ -912,10 +919,10 @@ typedef struct { double v[3], a[3], b[3]; } mpt; /* v = a - b */
 #define MPR_EPS 2.220446049250313e-16
 static int iszero(double x) { return fabs(x) < MPR_EPS; }
 
-static void msupport(const mpcr_model_t* m, const odata* d, int g1, int g2, const double dir[3], mpt* o) {
+static void msupport(const mpcr_model_t* m, const odata* d, int g1, int g2, const double dir[3], mpt* o, int hint[2]) {
   double nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support(m, d, g1, dir, o->a);
-  support(m, d, g2, nd, o->b);
+  support(m, d, g1, dir, o->a, &hint[0]);
+  support(m, d, g2, nd, o->b, &hint[1]);
   for (int k = 0; k < 3; k++) o->v[k] = o->a[k] - o->b[k];
 }
 static void normalize3(double v[3]) {
@@ -976,7 +983,8 @@ static void tri_closest(const double a[3], const double b[3], const double c[3],
 
 /* MPR penetration of geoms g1, g2: 1 and (depth, dir from g1 to g2, pos) if
    they overlap, else 0 */
-static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* depth, double dir[3], double pos[3]) {
+static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* depth, double dir[3], double pos[3],
+               int* hint) {
   mpt p[4], v4;
   double va[3], vb[3], dd;
   /* phase 1: portal discovery; v0 = interior point of the difference */
@@ -988,7 +996,7 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
   if (iszero(p[0].v[0]) && iszero(p[0].v[1]) && iszero(p[0].v[2])) p[0].v[0] += 10 * MPR_EPS;
   for (int k = 0; k < 3; k++) dir[k] = -p[0].v[k];
   normalize3(dir);
-  msupport(m, d, g1, g2, dir, &p[1]);
+  msupport(m, d, g1, g2, dir, &p[1], hint);
   dd = dot3(p[1].v, dir);
   if (iszero(dd) || dd < 0) return 0;
   cross3(dir, p[0].v, p[1].v);
@@ -1005,7 +1013,7 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
     return 1;
   }
   normalize3(dir);
-  msupport(m, d, g1, g2, dir, &p[2]);
+  msupport(m, d, g1, g2, dir, &p[2], hint);
   dd = dot3(p[2].v, dir);
   if (iszero(dd) || dd < 0) return 0;
   for (int k = 0; k < 3; k++) { va[k] = p[1].v[k] - p[0].v[k]; vb[k] = p[2].v[k] - p[0].v[k]; }
@@ -1017,7 +1025,7 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
   }
   for (int guard = 0;; guard++) {
     if (guard > MPR_ITER) return 0;
-    msupport(m, d, g1, g2, dir, &p[3]);
+    msupport(m, d, g1, g2, dir, &p[3], hint);
     dd = dot3(p[3].v, dir);
     if (iszero(dd) || dd < 0) return 0;
     int cont = 0;
@@ -1039,7 +1047,7 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
     portal_dir(p, dir);
     dd = dot3(dir, p[1].v);
     if (iszero(dd) || dd > 0) break;
-    msupport(m, d, g1, g2, dir, &v4);
+    msupport(m, d, g1, g2, dir, &v4, hint);
     dd = dot3(v4.v, dir);
     if (!(iszero(dd) || dd > 0) || reach_tol(p, &v4, dir) || it > MPR_ITER) return 0;
     expand(p, &v4);
@@ -1047,7 +1055,7 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
   /* phase 3: penetration depth / direction / position */
   for (int it = 0;; it++) {
     portal_dir(p, dir);
-    msupport(m, d, g1, g2, dir, &v4);
+    msupport(m, d, g1, g2, dir, &v4, hint);
     if (reach_tol(p, &v4, dir) || it > MPR_ITER) {
       double w[3];
       tri_closest(p[1].v, p[2].v, p[3].v, w);
@@ -1080,17 +1088,17 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
   }
 }
 
-static void col_convex(const mpcr_model_t* m, const odata* d, int g1, int g2, ocontact* out) {
+static void col_convex(const mpcr_model_t* m, odata* d, int pair, int g1, int g2, ocontact* out) {
   double depth, n[3], pos[3];
-  if (!mpr(m, d, g1, g2, &depth, n, pos)) return;
+  if (!mpr(m, d, g1, g2, &depth, n, pos, d->hint[pair])) return;
   if (n[0] == 0 && n[1] == 0 && n[2] == 0) n[2] = 1; /* touching: any frame */
   set_contact(out, -depth, pos, n);
 }
 
-static void col_plane_convex(const mpcr_model_t* m, const odata* d, int gp, int g, ocontact* out) {
+static void col_plane_convex(const mpcr_model_t* m, odata* d, int pair, int gp, int g, ocontact* out) {
   const double* R = d->geom_xmat[gp];
   double n[3] = {R[2], R[5], R[8]}, nn[3] = {-R[2], -R[5], -R[8]}, p[3], pos[3];
-  support(m, d, g, nn, p);
+  support(m, d, g, nn, p, &d->hint[pair][1]);
   double dist = (p[0] - d->geom_xpos[gp][0]) * n[0] + (p[1] - d->geom_xpos[gp][1]) * n[1] +
                 (p[2] - d->geom_xpos[gp][2]) * n[2];
   for (int k = 0; k < 3; k++) pos[k] = p[k] - 0.5 * dist * n[k];
@@ -1107,11 +1115,29 @@ static void collision(const mpcr_model_t* m, odata* d) {
       out[s].pair = p;
       out[s].active = 0;
     }
-    /* unmasked pairs only feed the solver: cull by bounding spheres */
-    if (m->pair_slotadr[p] < 0 && m->geom_type[g1] != MPCR_GEOM_PLANE) {
+    /* unmasked pairs only feed the solver: cull by bounding spheres (and, for
+       the general convex functions, plane / box vs the other bounding sphere;
+       all exact: a culled pair cannot touch) */
+    if (m->pair_slotadr[p] < 0) {
       double dif[3];
       for (int k = 0; k < 3; k++) dif[k] = d->geom_xpos[g2][k] - d->geom_xpos[g1][k];
-      if (norm3(dif) > m->geom_rbound[g1] + m->geom_rbound[g2] + m->pair_margin[p]) continue;
+      if (m->geom_type[g1] != MPCR_GEOM_PLANE) {
+        if (norm3(dif) > m->geom_rbound[g1] + m->geom_rbound[g2] + m->pair_margin[p]) continue;
+        if (m->pair_func[p] == MPCR_COL_CONVEX &&
+            (m->geom_type[g1] == MPCR_GEOM_BOX || m->geom_type[g2] == MPCR_GEOM_BOX)) {
+          int b1 = m->geom_type[g1] == MPCR_GEOM_BOX, gb = b1 ? g1 : g2;
+          double dd[3] = {b1 ? dif[0] : -dif[0], b1 ? dif[1] : -dif[1], b1 ? dif[2] : -dif[2]}, l[3], o2 = 0;
+          mulmtv(l, d->geom_xmat[gb], dd);
+          for (int k = 0; k < 3; k++) {
+            double e = fabs(l[k]) - m->geom_size[gb][k];
+            if (e > 0) o2 += e * e;
+          }
+          if (sqrt(o2) > m->geom_rbound[b1 ? g2 : g1] + m->pair_margin[p]) continue;
+        }
+      } else {
+        const double* R = d->geom_xmat[g1];
+        if (R[2] * dif[0] + R[5] * dif[1] + R[8] * dif[2] > m->geom_rbound[g2] + m->pair_margin[p]) continue;
+      }
     }
     const double *s1 = m->geom_size[g1], *s2 = m->geom_size[g2];
     switch (m->pair_func[p]) {
@@ -1120,8 +1146,8 @@ static void collision(const mpcr_model_t* m, odata* d) {
       case MPCR_COL_CAPSULE_CAPSULE: col_capsule_capsule(d, g1, g2, s1, s2, out); break;
       case MPCR_COL_CAPSULE_BOX: col_capsule_box(d, g1, g2, s1, s2, out); break;
       case MPCR_COL_BOX_BOX: col_box_box(d, g1, g2, s1, s2, m->pair_margin[p] - m->pair_gap[p], out); break;
-      case MPCR_COL_CONVEX: col_convex(m, d, g1, g2, out); break;
-      case MPCR_COL_PLANE_CONVEX: col_plane_convex(m, d, g1, g2, out); break;
+      case MPCR_COL_CONVEX: col_convex(m, d, p, g1, g2, out); break;
+      case MPCR_COL_PLANE_CONVEX: col_plane_convex(m, d, p, g1, g2, out); break;
       default: break;
     }
     for (int s = 0; s < m->pair_ncon[p]; s++) {
@@ -1504,6 +1530,7 @@ int oracle_step(const mpcr_model_t* m, double* qpos, double* qvel, double* qacc_
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
   memcpy(d->qacc_warmstart, qacc_ws, sizeof(double) * m->nv);
+  reset_hints(d);
   forward(m, d);
   if (M_out)
     for (int i = 0; i < m->nv; i++)
@@ -1551,6 +1578,7 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
   for (int k = 0; k < 4; k++) qt[k] /= qtn;
   for (int b = 0; b < n; b++) {
     memset(d, 0, sizeof(odata));
+    reset_hints(d);
     memcpy(d->qpos, m->qpos_init, sizeof(double) * m->nq);
     memcpy(d->qvel, m->qvel_init, sizeof(double) * m->nv);
     for (int j = 0; j < nc; j++) d->qpos[m->ctrl_qposadr[j]] = q0[j];

@@ -76,7 +76,7 @@ def test_parity_small(torch_cuda, name, layout):
         assert np.abs(g["slots"] - o["slots"]).max() < 1e-3
 
 
-@pytest.mark.parametrize("name", ["planner_scene", "scene_mjx", "ur5e_hande_mjx", "dual_arm"])
+@pytest.mark.parametrize("name", ["planner_scene", "scene_mjx", "ur5e_hande_mjx"])
 def test_parity_projected_h50(torch_cuda, name):
     """Realistic samples (projected to |thetadot| <= 0.8): arm/table/box contacts occur."""
     torch = torch_cuda
@@ -193,11 +193,52 @@ def test_compute_cem_dropin(torch_cuda):
     np.testing.assert_array_equal(out2[0], cost)
 
 
+def _intrinsic(m, td, rng):
+    """The fp64 oracle against itself under 1e-7 and 1e-6 relative input
+    noise (the order of fp32 rounding): how well-conditioned each candidate's
+    cost is.  Returns the unperturbed costs and the larger miss fraction."""
+    a = oracle.rollout(m, td, Q0, W, PT, QT, want_theta=False)["cost4"]
+    miss = 0.0
+    for eps in (1e-7, 1e-6):
+        b = oracle.rollout(m, td * (1 + eps * rng.standard_normal(td.shape)), Q0, W, PT, QT, want_theta=False)["cost4"]
+        miss = max(miss, float((np.abs(a[:, 0] - b[:, 0]) / np.abs(a[:, 0]) > TOL).mean()))
+    return a, miss
+
+
+@pytest.mark.parametrize("H", [50, 100])
+def test_dual_arm_parity_to_conditioning(torch_cuda, H):
+    """Dual arm (C4/C5 scene) on realistic projected samples.  Its costs are
+    chaotic even in fp64 (the 2F-85 linkage sits in permanent mesh contact and
+    the Newton line search couples it to arm 1): 1e-7 input noise moves a
+    share of the candidates by more than 1e-4 (~3% at H = 50, ~30% at
+    H = 100, about independent of the noise level once chaotic).  The bar is
+    therefore the problem's own conditioning: the GPU may not miss 1e-4 on
+    more candidates than the perturbed oracle does, up to 3 binomial standard
+    deviations of the 128-sample fractions + 2%; the median error stays at
+    fp32 level and the GPU's selected candidate is among the oracle's best 3."""
+    torch = torch_cuda
+    n = 128
+    m = models.load("dual_arm", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
+    xi_h = xi.cpu().numpy()
+    e = Engine(m, H, n, Pd)
+    g = e.rollout_cost(xi_h, MPCR_LAYOUT_XI, Q0, W, PT, QT).astype(np.float64)
+    td = np.einsum("tk,njk->njt", Pd, xi_h.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
+    o, miss = _intrinsic(m, td, np.random.default_rng(H))
+    rel = np.abs(g[:, 0] - o[:, 0]) / np.abs(o[:, 0])
+    slack = 3 * np.sqrt(max(miss, 0.01) * (1 - miss) / n) + 0.02
+    assert (rel > TOL).mean() <= miss + slack, ((rel > TOL).mean(), miss, slack)
+    assert np.median(rel) < 1e-5
+    i = int(np.argmin(g[:, 0]))
+    assert int((o[:, 0] < o[i, 0]).sum()) < 3
+
+
 def test_dual_arm_c4_properties(torch_cuda):
     """C4's per-GPU shard (4096 x 100, dual arm: implicitfast, actuators,
-    connect equalities, convex-hull contacts): finite, deterministic, the
-    gripper's permanently touching linkage contacts are found (constraint rows
-    every step), no row truncation; a 32-candidate sample matches the oracle."""
+    connect equalities, convex-hull contacts): finite, deterministic,
+    shard-invariant, the gripper's permanently touching linkage contacts are
+    found (constraint rows every step), no row truncation."""
     torch = torch_cuda
     n, H = 4096, 100
     m = models.load("dual_arm", 0.05)
@@ -207,14 +248,11 @@ def test_dual_arm_c4_properties(torch_cuda):
     st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
     a = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, status=st).clone()
     b = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT).clone()
+    half = n // 2
+    c2 = e.rollout_cost(xi[half:].contiguous(), MPCR_LAYOUT_XI, Q0, W, PT, QT, index_base=half).clone()
     torch.cuda.synchronize()
-    assert torch.equal(a, b) and torch.isfinite(a).all()
+    assert torch.equal(a, b) and torch.isfinite(a).all() and torch.equal(c2, a[half:])
     s_ = st.cpu().numpy()
     assert int((s_ & 1).sum()) == 0
     rows_per_step = (s_ >> 8) / H
     assert rows_per_step.min() >= 8  # 8 equality rows + the linkage contacts
-    sel = np.arange(0, n, n // 32)
-    td = np.einsum("tk,njk->njt", Pd, xi.cpu().numpy()[sel].reshape(-1, 6, 11).astype(np.float64)).reshape(-1, 6 * H)
-    o = oracle.rollout(m, td, Q0, W, PT, QT, want_theta=False)["cost4"]
-    rel = np.abs(a.cpu().numpy()[sel, 0] - o[:, 0]) / np.abs(o[:, 0])
-    assert (rel < TOL).mean() >= 0.9, np.sort(rel)[-4:]

@@ -17,7 +17,7 @@ from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine  # noqa: E402
 from manipulator_mujoco_amd.projection import ProjectionFilter  # noqa: E402
 
 name = os.environ.get("MODEL", "scene_mjx")
-n, H = int(os.environ.get("N", 4096)), 50
+n, H = int(os.environ.get("N", 4096)), int(os.environ.get("H", 50))
 m = models.load(name, 0.05)
 _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
 q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])

@@ -30,7 +30,7 @@ def main():
     from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine
     from manipulator_mujoco_amd.projection import ProjectionFilter
     name = sys.argv[1] if len(sys.argv) > 1 else "scene_mjx"
-    n, H = int(os.environ.get("N", 4096)), 50
+    n, H = int(os.environ.get("N", 4096)), int(os.environ.get("H", 50))
     m = models.load(name, 0.05)
     _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
     proj = ProjectionFilter(P, Pd, Pdd, 6, torch.device("cpu"))
