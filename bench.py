@@ -36,12 +36,24 @@ QT = (0.0, 1.0, 0.0, 0.0)
 PEAK_F32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = f32-MFMA dense peak
 PEAK_HBM_GBS = 8000.0
 
+# BASELINE.json configs; c3 is the metric's workload (default)
+CONFIGS = {
+    "c2": dict(model="ur5e_hande_mjx", n=1024, H=50,
+               desc="URD/ur5e_1_robotiq_hande_mjx.xml arm alone, Newton(1 it, 5 ls)"),
+    "c3": dict(model="scene_mjx", n=4096, H=50,
+               desc="UR5e+Hand-E arm + object.xml box (URD/scene_mjx.xml), Newton(1 it, 5 ls)"),
+    "c4": dict(model="dual_arm", n=4096, H=100,
+               desc="dual-arm gripper scene (implicitfast, 14 actuators, connect equalities, convex-hull "
+                    "meshes), Newton(100 it, 50 ls); C4 = 8 GPUs x 4096"),
+}
+
 
 def flops_per_step(m, nefc_mean, ncon_pairs=None):
     fm = json.load(open(os.path.join(ROOT, "bench", "flops_model.json")))
     nb_moving = int(sum(1 for b in range(1, m.nbody) if m.body_weldid[b] != 0))
-    names = ["plane_capsule", "plane_box", "capsule_capsule", "capsule_box", "box_box"]
-    coll = sum(fm["collision_per_pair"][names[f]] for f in m.pair_func)
+    names = {0: "plane_capsule", 1: "plane_box", 2: "capsule_capsule", 3: "capsule_box", 4: "box_box", 9: "convex",
+             10: "plane_convex"}
+    coll = sum(fm["collision_per_pair"][names[int(f)]] for f in m.pair_func)
     sp = fm["solve_per_row"]
     nv = m.nv
     solve = fm["solve_base"] + nefc_mean * (sp["row_setup"] + sp["jacobian_per_dof"] * nv
@@ -88,15 +100,15 @@ def cpu_baseline(m, xi, H, Pd, workers):
         oracle.rollout(m, td, Q0, np.array(W), np.array(PT), np.array(QT), want_theta=False)
     else:
         with ProcessPoolExecutor(workers) as ex:
-            list(ex.map(_oracle_chunk, [(td[c], m.source) for c in chunks]))
+            list(ex.map(_oracle_chunk, [(td[c], m.bundle_name) for c in chunks]))
     return n / (time.perf_counter() - t0)
 
 
 def _oracle_chunk(args):
     import oracle
     from manipulator_mujoco_amd import models
-    td, _ = args
-    m = models.load("scene_mjx", 0.05)
+    td, name = args
+    m = models.load(name, 0.05)
     oracle.rollout(m, td, Q0, np.array(W), np.array(PT), np.array(QT), want_theta=False)
     return td.shape[0]
 
@@ -106,14 +118,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=4096, help="candidates per GPU")
-    ap.add_argument("--horizon", type=int, default=50)
-    ap.add_argument("--model", default="scene_mjx")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
+                    help="BASELINE.json config preset (c3 = the metric's workload, the default)")
+    ap.add_argument("--n", type=int, default=None, help="candidates per GPU (default: the config's)")
+    ap.add_argument("--horizon", type=int, default=None)
+    ap.add_argument("--model", default=None)
     ap.add_argument("--cpu-sample", type=int, default=4096)
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_rollout.csv"))
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    args.model = args.model or cfg["model"]
+    args.n = args.n or cfg["n"]
+    args.horizon = args.horizon or cfg["H"]
 
     import torch
     import torch.distributed as dist
@@ -129,6 +147,7 @@ def main():
 
     H, n = args.horizon, args.n
     m = models.load(args.model, 0.05)
+    m.bundle_name = args.model
     _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
     # synthetic inputs, generated on the host (same bytes on every run)
     rng = np.random.default_rng(20250629 + 3 + rank)
@@ -145,7 +164,8 @@ def main():
         v1 = cpu_baseline(m, sample[: max(64, args.cpu_sample // 16)], H, Pd, 1)
         vp = cpu_baseline(m, sample, H, Pd, workers)
         cpu_rec = {"value": round(vp, 1), "unit": "rollouts/s", "cores": workers, "kind": "port",
-                   "sample": f"{sample.shape[0]} of the same C3 candidates x {H} steps, fp64 scalar C oracle "
+                   "sample": f"{sample.shape[0]} of the same {args.config.upper()} candidates x {H} steps, fp64 "
+                             f"scalar C oracle "
                              f"(oracle/mpcr_oracle.c), {workers} processes; 1 core: {v1:.1f} rollouts/s",
                    "one_core": round(v1, 1)}
 
@@ -209,8 +229,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (xi ~ N(0, 10.003 I), 10-iteration ADMM projection; seed 20250629+3+rank)",
-            "config": {"workload": f"C3 {args.model}: UR5e+Hand-E arm + object.xml box, {n} candidates x {H} "
-                                   f"steps per GPU, order-10 Bernstein, Newton(1 it, 5 ls), dt 0.05",
+            "config": {"workload": f"{args.config.upper()} {args.model}: {cfg['desc']}, {n} candidates x {H} "
+                                   f"steps per GPU, order-10 Bernstein, dt 0.05",
                        "candidates_per_gpu": n, "horizon": H, "global_batch": total,
                        "parallelism": f"dp{world} (candidate shards, 8-byte RCCL MIN all-reduce)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_TFLOPS,

@@ -76,7 +76,7 @@ def run_cem_planner(num_dof=None, num_batch=None, num_steps=None, maxiter_cem=No
     cem = cem_planner(num_dof=num_dof, num_batch=num_batch, num_steps=num_steps, maxiter_cem=maxiter_cem,
                       w_pos=w_pos, w_rot=w_rot, w_col=w_col, num_elite=num_elite, timestep=timestep,
                       maxiter_projection=maxiter_projection, model_path=model_path, device=device, graph=graph,
-                      verbose=verbose, **(planner_kwargs or {}))
+                      verbose=verbose, **({"return_rollouts": False} | (planner_kwargs or {})))
     log(f"Initialized CEM Planner: {round(time.time() - start_time, 2)}s")
 
     model = cem.model

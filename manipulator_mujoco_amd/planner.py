@@ -71,12 +71,15 @@ class cem_planner:  # noqa: N801 (reference name)
                         initialised default group has more than one rank
     gather_rollouts     with ranks > 1, all-gather the full thetadot/theta
                         arrays of the 9-tuple (default: this rank's shard)
+    return_rollouts     False: the 9-tuple's thetadot/theta (iters x N x 6H,
+                        what the closed loop discards) are returned as None
+                        instead of being copied to the host every tick
     """
 
     def __init__(self, num_dof=None, num_batch=None, num_steps=None, timestep=None, maxiter_cem=None,
                  num_elite=None, w_pos=None, w_rot=None, w_col=None, maxiter_projection=None, *,
                  model_path=None, device=None, seed=0, elite_from_filtered=False, graph=False, group=None,
-                 gather_rollouts=False, verbose=True):
+                 gather_rollouts=False, return_rollouts=True, verbose=True):
         import torch
         import torch.distributed as tdist
 
@@ -95,6 +98,7 @@ class cem_planner:  # noqa: N801 (reference name)
         self.elite_from_filtered = bool(elite_from_filtered)
         self.graph = bool(graph)
         self.gather_rollouts = bool(gather_rollouts)
+        self.return_rollouts = bool(return_rollouts)
         # CEM constants (:84-97)
         self.v_max, self.a_max, self.p_max = 0.8, 1.8, np.pi
         self.alpha_mean, self.alpha_cov, self.lamda = 0.6, 0.6, 10.0
@@ -280,8 +284,10 @@ class cem_planner:  # noqa: N801 (reference name)
             import torch.distributed as tdist
             tdist.broadcast(best, src=tdist.get_global_rank(self.group, owner) if self.group is not
                             tdist.group.WORLD else owner, group=self.group)
-            if self.gather_rollouts:
+            if self.gather_rollouts and self.return_rollouts:
                 theta, thetadot = (self._gather_all(x) for x in (theta, thetadot))
+        if not self.return_rollouts:
+            theta = thetadot = None
         best_vels = best[4:4 + d * H].reshape(d, H).T
         best_traj = best[4 + d * H:].reshape(d, H).T
         out = (cost_min, best[1], best[2], best[3], best_vels, best_traj, self._mean, thetadot, theta)
