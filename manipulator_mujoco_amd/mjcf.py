@@ -930,13 +930,17 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
     # planner ids (SBP/mjx_planner.py:120-121) and controlled dofs (:254,267-270)
     m.hande_body = m.names["body"].index("hande") if "hande" in m.names["body"] else -1
     m.tcp_site = m.names["site"].index("tcp") if "tcp" in m.names["site"] else -1
-    m.nctrl = min(6, nv)
+    # the planner controls the leading hinge/slide dofs (qpos == qvel indexing),
+    # at most 6; cem_planner refuses a model whose count differs from num_dof
+    nctrl = 0
+    while nctrl < min(6, nv):
+        jt = m.jnt_type[m.dof_jntid[nctrl]]
+        if jt not in (2, 3) or m.jnt_qposadr[m.dof_jntid[nctrl]] != nctrl:
+            break
+        nctrl += 1
+    m.nctrl = nctrl
     m.ctrl_qposadr = np.arange(m.nctrl)
     m.ctrl_dofadr = np.arange(m.nctrl)
-    for k in range(m.nctrl):
-        jt = m.jnt_type[m.dof_jntid[k]]
-        if jt not in (2, 3) or m.jnt_qposadr[m.dof_jntid[k]] != k:
-            raise MJCFError("the first num_dof dofs must be hinge/slide joints with qpos == qvel indexing")
 
     _actuators(m, root, defaults, jnt, jnames, autolimits)
     m.integrator = integrators[opt["integrator"]]

@@ -1,0 +1,203 @@
+"""Dual-arm class on the CPU: the compiled
+bundle's structure, and analytic pins of the oracle's new physics
+(oracle/mpcr_oracle.c: MPR convex collision, plane-convex, actuators,
+implicitfast) on small synthetic scenes whose answers are known in closed form.
+The GPU kernel is checked against this oracle in tests/test_gpu_parity.py."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import REFERENCE, has_reference
+from manipulator_mujoco_amd import cmodel, mjcf, models
+
+
+@pytest.fixture(scope="module")
+def dual():
+    return models.load("dual_arm", 0.05)
+
+
+def test_dual_arm_structure(dual):
+    m = dual
+    assert (m.nv, m.nq, m.nu, m.neq, m.npair, m.nslot) == (22, 22, 14, 4, 662, 0)
+    assert m.integrator == cmodel.INT_IMPLICITFAST and m.iterations == 100 and m.ls_iterations == 50
+    assert sorted(m.eq_type.tolist()) == [0, 0, 2, 2]  # 2 connect, 2 joint
+    funcs = m.pair_func.tolist()
+    assert funcs.count(cmodel.COL_CONVEX) == 424 and funcs.count(cmodel.COL_PLANE_CONVEX) == 16
+    assert funcs == sorted(funcs)  # convex pairs last (the kernel compacts them in order)
+    assert int((m.body_weldid != 0).sum()) == 29
+    # arm 1 is the planner's: the first 6 dofs, hande + tcp present
+    assert m.names["body"][m.hande_body] == "hande" and m.names["site"][m.tcp_site] == "tcp"
+    # the two grippers' tendon actuators spread over their two finger / driver joints
+    tendon = [a for a in range(m.nu) if m.act_ntrn[a] == 2]
+    assert len(tendon) == 2
+    for a in tendon:
+        np.testing.assert_allclose(m.act_moment[a], [0.5, 0.5])
+
+
+def test_hull_graphs(dual):
+    """Every hull vertex graph is symmetric and hill climbing from the first
+    vertex reaches the true support point (what the kernel and oracle rely on)."""
+    m = dual
+    rng = np.random.default_rng(0)
+    adj = [set(m.hull_adj[m.hull_adjadr[v]:m.hull_adjadr[v] + m.hull_adjnum[v]].tolist()) for v in range(m.nhullv)]
+    for v, nb in enumerate(adj):
+        assert len(nb) >= 3 and v not in nb
+        for u in nb:
+            assert v in adj[u]
+    for g in np.where(m.geom_hulladr >= 0)[0]:
+        a, n = m.geom_hulladr[g], m.geom_hullnum[g]
+        V = m.hull_vert[a:a + n]
+        assert np.linalg.norm(V.mean(axis=0)) < 1e-9  # recentred: the portal starts inside
+        for d in rng.normal(size=(20, 3)):
+            v = a
+            while True:
+                best = max(adj[v], key=lambda u: m.hull_vert[u] @ d)
+                if m.hull_vert[best] @ d <= m.hull_vert[v] @ d:
+                    break
+                v = best
+            assert abs(m.hull_vert[v] @ d - (V @ d).max()) < 1e-12
+
+
+def test_connect_anchors_coincide_at_qpos0(dual):
+    m = dual
+    k = mjcf.kinematics0(m, m.qpos0)
+    for e in np.where(m.eq_type == cmodel.EQ_CONNECT)[0]:
+        b1, b2 = m.eq_obj1[e], m.eq_obj2[e]
+        p1 = k["xpos"][b1] + k["xmat"][b1] @ m.eq_data[e, :3]
+        p2 = k["xpos"][b2] + k["xmat"][b2] @ m.eq_data[e, 3:6]
+        np.testing.assert_allclose(p1, p2, atol=1e-12)
+
+
+@pytest.mark.skipif(not has_reference(), reason="needs /root/reference MJCF")
+def test_dual_bundle_is_current():
+    m = mjcf.compile_mjcf(os.path.join(REFERENCE, "universal_robots_ur5e/dual_arm_gripper_scene.xml"), 0.05)
+    assert m.to_blob() == models.load("dual_arm", 0.05).to_blob()
+
+
+def test_dual_arm_rollout_is_finite_and_holds_arm2(dual):
+    """Planner semantics on the dual arm: finite costs; arm 2 (position servos
+    at ctrl 0, its home pose) stays within a few centiradians of home."""
+    H, n = 30, 4
+    rng = np.random.default_rng(1)
+    td = rng.uniform(-0.4, 0.4, (n, 6 * H))
+    q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
+    o = oracle.rollout(dual, td, q0, np.array([20.0, 3.0, 80.0]), np.array([-0.3, -0.3, 0.5]),
+                       np.array([0.0, 1.0, 0.0, 0.0]), want_theta=True)
+    assert np.isfinite(o["cost4"]).all() and o["status"] == 0
+    qpos = dual.qpos_init[:dual.nq].copy()
+    qpos[:6] = q0
+    qvel, qws = np.zeros(dual.nv), np.zeros(dual.nv)
+    for _ in range(H):
+        r = oracle.step(dual, qpos, qvel, qws)
+        qpos, qvel, qws = r["qpos"], r["qvel"], r["qacc_warmstart"]
+    assert np.abs(qpos[8:14]).max() < 0.05
+
+
+# ---------------------------------------------------------------------------
+# analytic pins on synthetic scenes
+
+
+def _cube_stl(path, h):
+    """Binary STL of an axis-aligned cube with half size h (12 triangles)."""
+    c = np.array([[x, y, z] for x in (-h, h) for y in (-h, h) for z in (-h, h)])
+    faces = [(0, 1, 3), (0, 3, 2), (4, 6, 7), (4, 7, 5), (0, 4, 5), (0, 5, 1),
+             (2, 3, 7), (2, 7, 6), (0, 2, 6), (0, 6, 4), (1, 5, 7), (1, 7, 3)]
+    with open(path, "wb") as f:
+        f.write(b"\0" * 80 + struct.pack("<I", len(faces)))
+        for t in faces:
+            f.write(struct.pack("<3f", 0, 0, 0))
+            for i in t:
+                f.write(struct.pack("<3f", *c[i]))
+            f.write(b"\0\0")
+
+
+def _scene(tmp_path, body_xml, extra="", option='<option timestep="0.01" gravity="0 0 0"/>'):
+    _cube_stl(tmp_path / "cube.stl", 0.05)
+    xml = f"""<mujoco>
+  <compiler angle="radian" autolimits="true"/>
+  {option}
+  <asset><mesh name="cube" file="cube.stl"/></asset>
+  <worldbody>
+    <geom name="floor" type="plane" size="0 0 0.05"/>
+    {body_xml}
+  </worldbody>
+  {extra}
+</mujoco>"""
+    p = tmp_path / "s.xml"
+    p.write_text(xml)
+    return mjcf.compile_mjcf(str(p))
+
+
+def _dists(m):
+    """First contact slot of every pair, keyed by both geom-name orders."""
+    r = oracle.step(m, m.qpos_init[:m.nq].copy(), np.zeros(m.nv), np.zeros(m.nv))
+    d = {}
+    for p in range(m.npair):
+        a, b = m.names["geom"][m.pair_geom1[p]], m.names["geom"][m.pair_geom2[p]]
+        d[(a, b)] = d[(b, a)] = r["dist"][m.pair_conadr[p]]
+    return r, d
+
+
+def test_mpr_sphere_sphere_depth(tmp_path):
+    m = _scene(tmp_path, """
+    <body name="a" pos="0 0 1"><freejoint/><geom name="a" type="sphere" size="0.1"/></body>
+    <body name="b" pos="0.03 0.04 1.13"><freejoint/><geom name="b" type="sphere" size="0.1"/></body>""")
+    # sphere-sphere has no primitive function here: the general convex (MPR) path
+    assert cmodel.COL_CONVEX in m.pair_func.tolist()
+    _, d = _dists(m)
+    depth = 0.2 - np.sqrt(0.03 ** 2 + 0.04 ** 2 + 0.13 ** 2)
+    assert abs(d[("a", "b")] + depth) < 1e-6
+
+
+def test_mpr_mesh_cube_on_box_and_plane(tmp_path):
+    m = _scene(tmp_path, """
+    <body name="c" pos="0 0 0.04"><freejoint/><geom name="c" type="mesh" mesh="cube"/></body>
+    <body name="k" pos="0.3 0 0.03"><freejoint/><geom name="k" type="mesh" mesh="cube"/></body>
+    <body name="t" pos="0.3 0 -0.015"><geom name="t" type="box" size="0.2 0.2 0.01"/></body>""")
+    _, d = _dists(m)
+    assert abs(d[("floor", "c")] - (0.04 - 0.05)) < 1e-9    # plane-convex: deepest hull vertex
+    assert abs(d[("t", "k")] - ((0.03 - 0.05) - (-0.005))) < 1e-6  # box top at -0.005, cube bottom at -0.02
+
+
+def test_mpr_cylinder_and_capsule_on_box(tmp_path):
+    m = _scene(tmp_path, """
+    <body name="t" pos="0 0 -0.5"><geom name="t" type="box" size="1 1 0.5"/></body>
+    <body name="y" pos="0 0 0.097"><freejoint/><geom name="y" type="cylinder" size="0.05 0.1"/></body>
+    <body name="p" pos="0.5 0 0.015" euler="0 1.5707963267948966 0"><freejoint/>
+      <geom name="p" type="capsule" size="0.02 0.1"/></body>""")
+    _, d = _dists(m)
+    assert abs(d[("t", "y")] + 0.003) < 1e-6   # cylinder end face 3 mm into the box top (MPR)
+    assert abs(d[("t", "p")] + 0.005) < 1e-6   # capsule-box keeps its primitive function
+
+
+def test_actuator_implicitfast_slide(tmp_path):
+    """Position servo (kp, kv) on a slide joint of mass `mass`, no gravity: the
+    actuator force is -kp q - kv v, and implicitfast advances the velocity with
+    (mass + dt kv) a = -kp q - kv v."""
+    kp, kv, mass, dt, q = 100.0, 10.0, 2.0, 0.01, 0.1
+    m = _scene(tmp_path, f"""
+    <body name="s" pos="0 0 1"><joint name="x" type="slide" axis="1 0 0"/>
+      <geom name="s" type="sphere" size="0.01" mass="{mass}" contype="0" conaffinity="0"/></body>""",
+               extra=f'<actuator><position joint="x" kp="{kp}" kv="{kv}"/></actuator>',
+               option=f'<option timestep="{dt}" gravity="0 0 0" integrator="implicitfast"/>')
+    assert m.nu == 1 and m.integrator == cmodel.INT_IMPLICITFAST
+    r = oracle.step(m, np.array([q]), np.zeros(1), np.zeros(1))
+    np.testing.assert_allclose(r["qacc"], [-kp * q / mass], rtol=1e-12)   # forward (explicit) acceleration
+    a_impl = -kp * q / (mass + dt * kv)
+    np.testing.assert_allclose(r["qvel"], [dt * a_impl], rtol=1e-12)
+    np.testing.assert_allclose(r["qpos"], [q + dt * dt * a_impl], rtol=1e-12)
+
+
+def test_actuator_force_and_joint_clamps(tmp_path):
+    """General affine actuator with forcerange, on a joint with actuatorfrcrange."""
+    m = _scene(tmp_path, """
+    <body name="s" pos="0 0 1"><joint name="x" type="slide" axis="1 0 0" actuatorfrcrange="-3 3"/>
+      <geom name="s" type="sphere" size="0.01" mass="1" contype="0" conaffinity="0"/></body>""",
+               extra='<actuator><general joint="x" gaintype="fixed" biastype="affine" gainprm="2" '
+                     'biasprm="1 -50 0" ctrlrange="-1 1" forcerange="-5 5"/></actuator>')
+    for q, expect in ((0.0, 1.0), (0.05, -1.5), (0.2, -3.0), (-0.2, 3.0)):  # ctrl 0: f = 1 - 50 q
+        r = oracle.step(m, np.array([q]), np.zeros(1), np.zeros(1))
+        np.testing.assert_allclose(r["qacc"], [expect], rtol=1e-12, atol=1e-12)

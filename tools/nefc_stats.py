@@ -11,7 +11,7 @@ from manipulator_mujoco_amd import basis, models  # noqa: E402
 from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine  # noqa: E402
 from manipulator_mujoco_amd.projection import ProjectionFilter  # noqa: E402
 
-for name in ("scene_mjx", "planner_scene", "ur5e_hande_mjx"):
+for name in ("scene_mjx", "planner_scene", "ur5e_hande_mjx", "dual_arm"):
     n, H = 4096, 50
     m = models.load(name, 0.05)
     _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
