@@ -40,6 +40,7 @@ struct mpcr_engine {
   unsigned long long* d_key = nullptr;
   int* d_status = nullptr;
   int* d_idx = nullptr;
+  float* d_slot_prev = nullptr;  // max_n x nslot (variants keeping cost_c history in HBM)
   // convex hulls (dual-arm class)
   float4* d_hull_vert = nullptr;
   int2* d_hull_info = nullptr;
@@ -505,7 +506,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
 
 extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, int horizon, const float* pdot,
                                   int nbasis, mpcr_engine** out) {
-  if (!m || !out || max_n <= 0 || horizon <= 0 || !pdot || nbasis <= 0 || nbasis > 16)
+  if (!m || !out || max_n <= 0 || horizon <= 0 || !pdot || nbasis <= 0 || nbasis > 12)
     return fail(MPCR_EINVAL, "bad engine arguments");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MPCR_ENODEV, "no HIP device");
@@ -563,7 +564,9 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       hipMalloc(&e->d_thetadot, sizeof(float) * max_n * nc * horizon) != hipSuccess ||
       hipMalloc(&e->d_key, sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&e->d_status, sizeof(int) * max_n) != hipSuccess ||
-      hipMalloc(&e->d_idx, sizeof(int) * max_n) != hipSuccess) {
+      hipMalloc(&e->d_idx, sizeof(int) * max_n) != hipSuccess ||
+      hipMalloc(&e->d_slot_prev, sizeof(float) * (size_t)max_n * (e->host.nslot > 0 ? e->host.nslot : 1)) !=
+          hipSuccess) {
     mpcr_engine_free(e);
     return fail(MPCR_ENOMEM, "device allocation failed");
   }
@@ -587,6 +590,7 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_key);
   (void)hipFree(e->d_status);
   (void)hipFree(e->d_idx);
+  (void)hipFree(e->d_slot_prev);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
   (void)hipFree(e->d_hull_adjv);
@@ -627,6 +631,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.status = l.status;
   a.trace_eef = l.trace_eef;
   a.trace_slots = l.trace_slots;
+  a.slot_prev = e->d_slot_prev;
   a.dpar = l.dpar;
   a.state = l.state;
   a.plant = l.plant;
@@ -861,6 +866,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   RolloutArgs a;
   std::memset(&a, 0, sizeof(a));
   a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
+  a.slot_prev = e->d_slot_prev;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   if (e->wide)

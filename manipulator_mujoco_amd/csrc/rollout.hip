@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "mpcr_device.h"
 
 namespace mpcr {
@@ -39,6 +41,7 @@ struct RolloutArgs {
   int* status;
   float* trace_eef;    // n x H x 7 (debug)
   float* trace_slots;  // n x H x nslot (debug)
+  float* slot_prev;    // n x nslot previous slot distances (variants keeping them in HBM)
   unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs
@@ -58,16 +61,18 @@ struct RolloutArgs {
 // reading 16 different rows hit distinct bank quads (LD*r mod 64 distinct
 // multiples of 4 for LD = 20 and 36) -> conflict free, 4x fewer LDS
 // instructions than b32.
-template <int NVW_, int NBW_, int NGW_>
+template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false>
 struct __align__(16) SmemT {
   static constexpr int NVW = NVW_, NBW = NBW_, NGW = NGW_, LD = NVW_ + 4;
+  static constexpr int MAXEFC = MAXEFC_, LDJ = LDJ_;      // constraint rows kept, J row stride
+  static constexpr bool CPREV_GLOBAL = CPREV_GLOBAL_;     // previous slot distances in HBM (L2) instead of LDS
   static constexpr int LOG_NVW = NVW_ == 32 ? 5 : 4;
   static constexpr bool WIDE = NVW_ == 32;  // dual-arm class: equalities, actuators, convex hulls
   static constexpr int NQW = WIDE ? DX_NQ : 24, NEQP = WIDE ? DX_NEQ : 1, NACT = WIDE ? DX_NU : 1;
   static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
   static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
   // ---- persistent across the step ----
-  float xi[DX_NCTRL * 16];
+  float xi[DX_NCTRL * 12];  // order <= 11 Bernstein coefficients per controlled joint
   float qpos[NQW];
   alignas(16) float qvel[NVW];
   alignas(16) float qacc[NVW];
@@ -80,7 +85,7 @@ struct __align__(16) SmemT {
   alignas(16) float M[NVW][LD];
   alignas(16) float gxpos[NGW][4];   // gxpos+gxmat (dead during Newton) double as the
   float gxmat[NGW][12];  // Hessian solve's LDS scratch (NGW*16 >= NVW*LD)
-  float cprev[DX_NSLOT];  // previous-step masked slot distances (cost_c)
+  float cprev[CPREV_GLOBAL ? 1 : DX_NSLOT];  // previous-step masked slot distances (cost_c)
   float par[PAR_N];       // q0 | w | ptgt | qtgt (normalised)
   float eqp[NEQP][2][4];  // connect anchors in world (body1, body2)
   float actf[NACT];       // actuator forces
@@ -109,19 +114,28 @@ struct __align__(16) SmemT {
       int con_pair[DX_MAXACT];
       int con_row[DX_MAXACT];
       float poly[2][8][4];  // box-box clipping polygon (double buffered)
-      alignas(16) float J[DX_MAXEFC][LD];
-      float efc_D[DX_MAXEFC];
-      float efc_aref[DX_MAXEFC];
-      float efc_jar[DX_MAXEFC];
-      float efc_jv[DX_MAXEFC];
-      float efc_f[DX_MAXEFC];   // -D * jar on active rows, else 0
-      float efc_Da[DX_MAXEFC];  // D on active rows, else 0
-      int efc_src[DX_MAXEFC];  // (kind << 24) | (index << 4) | side
+      alignas(16) float J[MAXEFC][LDJ];
+      float efc_D[MAXEFC];
+      float efc_aref[MAXEFC];
+      float efc_jar[MAXEFC];
+      float efc_jv[MAXEFC];
+      float efc_f[MAXEFC];   // -D * jar on active rows, else 0
+      float efc_Da[MAXEFC];  // D on active rows, else 0
+      int efc_src[MAXEFC];  // (kind << 24) | (index << 4) | side
     };
   };
 };
 // the two variants: single-arm scenes (nv <= 16) and the dual-arm class
-using SmemN = SmemT<16, 16, 24>;
+#ifndef MPCR_N_MAXEFC
+#define MPCR_N_MAXEFC 96
+#endif
+#ifndef MPCR_N_LDJ
+#define MPCR_N_LDJ 20
+#endif
+#ifndef MPCR_N_CPREV_GLOBAL
+#define MPCR_N_CPREV_GLOBAL 0
+#endif
+using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL>;
 using SmemW = SmemT<32, 32, 72>;
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
@@ -398,6 +412,36 @@ constexpr int kMprIter = MPCR_MPR_ITER;
 constexpr float kMprEps = 1.1920929e-07f;
 __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
 
+// examine the neighbours of vertex v along l: the best strictly better one
+// (first in list order on ties) or -1.  The first 8 neighbours (90 % of hull
+// vertices have <= 8) are 8 independent loads issued together; the rest loop.
+__device__ __forceinline__ void climb_scan(const DevModel* __restrict__ m, const float4 (&w)[8], int k0, int end,
+                                           const float l[3], float& best, float4& hv, int& nb) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const float du = w[j].x * l[0] + w[j].y * l[1] + w[j].z * l[2];
+    if (k0 + j < end && du > best) { best = du; nb = __float_as_int(w[j].w); hv = w[j]; }
+  }
+}
+__device__ __forceinline__ void climb_load(const DevModel* __restrict__ m, int k0, int last, float4 (&w)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) w[j] = m->hull_adjv[min(k0 + j, last)];
+}
+__device__ __forceinline__ int climb_round(const DevModel* __restrict__ m, int v, const float l[3], float& best,
+                                           float4& hv) {
+  const int2 info = m->hull_info[v];
+  const int end = info.x + info.y;
+  int nb = -1;
+  float4 w[8];
+  climb_load(m, info.x, end - 1, w);
+  climb_scan(m, w, info.x, end, l, best, hv, nb);
+  for (int k0 = info.x + 8; k0 < end; k0 += 8) {
+    climb_load(m, k0, end - 1, w);
+    climb_scan(m, w, k0, end, l, best, hv, nb);
+  }
+  return nb;
+}
+
 // hint: hull vertex the previous query on this geom ended at (-1: none); the
 // climb starts there (successive MPR directions are close)
 template <class S>
@@ -425,14 +469,7 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
     float4 hv = m->hull_vert[v];
     float best = hv.x * l[0] + hv.y * l[1] + hv.z * l[2];
     for (int guard = 0; guard < 4096; guard++) {
-      const int2 info = m->hull_info[v];
-      int nb = -1;
-#pragma unroll 4
-      for (int k = info.x; k < info.x + info.y; k++) {
-        const float4 w = m->hull_adjv[k];
-        const float du = w.x * l[0] + w.y * l[1] + w.z * l[2];
-        if (du > best) { best = du; nb = __float_as_int(w.w); hv = w; }
-      }
+      const int nb = climb_round(m, v, l, best, hv);
       if (nb < 0) break;
       v = nb;
     }
@@ -1118,8 +1155,9 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
         if (c < ns) {
           const float d = dist[c];
           if (d < 0.f) cost_c += 1.f;
-          if (t > 0) cost_c += fmaxf(s.cprev[sa + c] * (1.f - 0.005f) - d, 0.f);
-          s.cprev[sa + c] = d;
+          float* cp = S::CPREV_GLOBAL ? args.slot_prev + (size_t)b * m->nslot : s.cprev;
+          if (t > 0) cost_c += fmaxf(cp[sa + c] * (1.f - 0.005f) - d, 0.f);
+          cp[sa + c] = d;
           if (args.trace_slots) args.trace_slots[((size_t)b * H + t) * m->nslot + sa + c] = d;
         }
       }
@@ -1255,7 +1293,8 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
 template <int NVW, int NBW, int NGW, bool WIDE>
 __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
-  using S = SmemT<NVW, NBW, NGW>;
+  using S = typename std::conditional<WIDE, SmemW, SmemN>::type;
+  static_assert(S::NVW == NVW && S::NBW == NBW && S::NGW == NGW, "variant widths");
   __shared__ S s;
   const DevModel* __restrict__ const m0 = mptr;
   const DevModel* __restrict__ m = m0;
@@ -1817,8 +1856,8 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
       const int con_pre = wscan_excl(ncr, ncrow);
       int nefc = neq + nlim + ncrow;
       int keep_con = ncon;
-      if (nefc > DX_MAXEFC) {  // keep the longest prefix of contacts that fits
-        const int room = DX_MAXEFC - neq - nlim;
+      if (nefc > S::MAXEFC) {  // keep the longest prefix of contacts that fits
+        const int room = S::MAXEFC - neq - nlim;
         const unsigned long long fit = __ballot(lane < ncon && con_pre + ncr <= room);
         keep_con = __popcll(fit);
         nefc = neq + nlim + (keep_con > 0 ? __shfl(con_pre + ncr, keep_con - 1) : 0);
