@@ -2053,6 +2053,9 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           // the iteration cap ends the solve before anything below matters
           // (cost / gradient only feed the stop test)
           if (it >= m->iterations) break;
+#ifdef MPCR_PROFILE
+          prof_acc[15] += 1;  // Newton iterations (low half of the counter, not cycles)
+#endif
           // Ma, jar, cost at the current qacc; per-row force and active D
           const float ma = lane < nv ? dotN<NVW>(s.M[lane], s.qacc) : 0.f;
           float cc = 0.f;
@@ -2078,7 +2081,13 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           for (int o = NVW; o < WAVE; o <<= 1) qc += __shfl_xor(qc, o);
           const float grad = lane < nv ? ma - s.qfs[lane] - qc : 0.f;
           const float gn = sqrtf(wsum(grad * grad));
-          if (scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance) break;
+          // MuJoCo's stop test, plus its fp32 floor: an improvement within ~8 ulp
+          // of the cost is rounding noise (without it fp32 iterates on noise
+          // where the fp64 solve has converged: 3.9 vs 1.9 iterations per
+          // dual-arm step)
+          if (scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance ||
+              prev_cost - cost <= 1e-6f * fabsf(cost))
+            break;
           // Hessian H = M + J^T D_active J: lane (row i, column quads q, q + RPW,
           // ...) builds QPL float4s of row i; rows are gathered to lanes
           // 0..NVW-1 through LDS
@@ -2133,8 +2142,15 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           bool swap = true;
           for (int ls = 0; ls < m->ls_iterations; ls++) {
             if (!swap) break;
+#ifdef MPCR_PROFILE
+            prof_acc[15] += 1ull << 32;  // line-search passes (high half of the counter)
+#endif
             if (lo.d0 < 0.f && lo.d0 > -gtol) break;
             if (hi.d0 > 0.f && hi.d0 < gtol) break;
+            // bracket closed to fp32 resolution: further passes only move alpha
+            // by rounding noise (gtol sits below fp32 resolution; without this the
+            // dual arm ran ~20 passes per Newton iteration against ~2.4 in fp64)
+            if (fabsf(hi.alpha - lo.alpha) <= 1e-6f * fmaxf(fabsf(lo.alpha), fabsf(hi.alpha))) break;
             LsPt lo_next, hi_next, mid;
             ls_eval3(s, lane, qg, lo.alpha - lo.d0 / lo.d1, hi.alpha - hi.d0 / hi.d1, 0.5f * (lo.alpha + hi.alpha),
                      lo_next, hi_next, mid);

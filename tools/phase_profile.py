@@ -49,6 +49,8 @@ def main():
     print(f"{name}: n={n} H={H} cycles/wave-step {tot / n / H:.0f}")
     for i, p in enumerate(PHASES):
         print(f"  {p:16s} {ph[i] / n / H:10.0f} cyc  {100 * ph[i] / tot:5.1f}%")
+    print(f"  Newton iterations per step: {(ph[15] & 0xFFFFFFFF) / n / H:.2f}, line-search passes per step: "
+          f"{(ph[15] >> 32) / n / H:.2f} (steps with constraints only)")
 
 
 if __name__ == "__main__":
