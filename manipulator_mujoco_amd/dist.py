@@ -47,15 +47,52 @@ def decode_key(key: int):
     return idx, float(np.uint32(u).view(np.float32))
 
 
+def _host_staged(group):
+    """gloo moves CPU tensors (used by the CPU tests and for ranks sharing one
+    GPU); RCCL moves device tensors."""
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"
+
+
 def allreduce_min_key(key_tensor, group=None):
     """In-place global MIN of a 1-element int64 tensor holding an unsigned
     packed key (sign bit flipped around the signed reduction)."""
     import torch.distributed as dist
 
-    key_tensor ^= SIGN
-    dist.all_reduce(key_tensor, op=dist.ReduceOp.MIN, group=group)
-    key_tensor ^= SIGN
+    t = key_tensor.cpu() if _host_staged(group) and key_tensor.is_cuda else key_tensor
+    t ^= SIGN
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    t ^= SIGN
+    if t is not key_tensor:
+        key_tensor.copy_(t)
     return key_tensor
+
+
+def all_gather(x, group=None):
+    """(world, *x.shape) all-gather of a contiguous tensor, on x's device."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    src = x.contiguous()
+    if _host_staged(group) and src.is_cuda:
+        src = src.cpu()
+    shape = tuple(src.shape)
+    out = torch.empty((world * shape[0],) + shape[1:], dtype=src.dtype, device=src.device)  # dim-0 concat
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out.view((world,) + shape).to(x.device)
+
+
+def broadcast(x, src, group=None):
+    """In-place broadcast from group rank src."""
+    import torch.distributed as dist
+
+    g_src = dist.get_global_rank(group, src) if group is not None and group is not dist.group.WORLD else src
+    t = x.cpu() if _host_staged(group) and x.is_cuda else x
+    dist.broadcast(t, src=g_src, group=group)
+    if t is not x:
+        x.copy_(t)
+    return x
 
 
 def shard(n_total: int, rank: int, world: int):
@@ -91,8 +128,7 @@ def gather_elites(cost, xi, k, topk_fn, group=None):
     pack = torch.empty((kl, nv + 1), dtype=xi.dtype, device=xi.device)
     pack[:, :nv] = xi.index_select(0, lidx)
     pack[:, nv] = cost.index_select(0, lidx)
-    out = torch.empty((world * kl, nv + 1), dtype=xi.dtype, device=xi.device)
-    dist.all_gather_into_tensor(out, pack, group=group)
+    out = all_gather(pack, group).reshape(world * kl, nv + 1)
     g_cost = out[:, nv].contiguous()
     g_xi = out[:, :nv].contiguous()
     sel = topk_fn(g_cost, int(k))
@@ -105,9 +141,6 @@ def allgather_min(values, group=None):
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size(group)
-    out = torch.empty((world,) + tuple(values.shape), dtype=values.dtype, device=values.device)
-    dist.all_gather_into_tensor(out, values.contiguous(), group=group)
-    a = out.cpu().numpy()
+    a = all_gather(values, group).cpu().numpy()
     return np.where(np.isnan(a).any(axis=0), np.nan, np.nanmin(np.where(np.isnan(a), np.inf, a), axis=0)).astype(
         np.float32)

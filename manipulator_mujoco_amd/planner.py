@@ -281,9 +281,7 @@ class cem_planner:  # noqa: N801 (reference name)
             best[4:4 + d * H] = thetadot[-1, li]
             best[4 + d * H:] = theta[-1, li]
         if self.world > 1:
-            import torch.distributed as tdist
-            tdist.broadcast(best, src=tdist.get_global_rank(self.group, owner) if self.group is not
-                            tdist.group.WORLD else owner, group=self.group)
+            mdist.broadcast(best, owner, group=self.group)
             if self.gather_rollouts and self.return_rollouts:
                 theta, thetadot = (self._gather_all(x) for x in (theta, thetadot))
         if not self.return_rollouts:
@@ -294,12 +292,9 @@ class cem_planner:  # noqa: N801 (reference name)
         return tuple(o.cpu().numpy() if isinstance(o, torch.Tensor) else o for o in out)
 
     def _gather_all(self, x):
-        import torch
-        import torch.distributed as tdist
+        from .dist import all_gather
         it_n, n, c = x.shape
-        out = torch.empty((self.world, it_n, n, c), dtype=x.dtype, device=x.device)
-        tdist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
-        return out.permute(1, 0, 2, 3).reshape(it_n, self.world * n, c)
+        return all_gather(x, self.group).permute(1, 0, 2, 3).reshape(it_n, self.world * n, c)
 
 
 def main():  # SBP/mjx_planner.py:408-428 (with its unpacking bug fixed)

@@ -120,3 +120,34 @@ def test_headless_closed_loop(torch_cuda, tmp_path):
     d = np.asarray(out["eef_dist"])
     assert np.isfinite(d).all() and (d[-1] < d[0] - 0.03 or out["target"] != "target_0")
     assert (np.diff(d) < 1e-3).mean() > 0.9  # steady approach, no divergence
+
+
+def _sharded_worker(rank, world, port, args, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = _planner(group=dist.group.WORLD, num_batch=512)
+        res = [p.compute_cem(*a) for a in args]
+        out[rank] = [[np.asarray(x).tolist() for x in r[:7]] for r in res]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharded_planner_equals_one_gpu(torch_cuda):
+    """The whole sharded planner with two ranks on the one GPU
+    of the box (gloo carries the collectives; RCCL refuses two ranks on one
+    device): sampling by global index, local top-E -> all-gather -> global
+    top-E, replicated update, best-key MIN all-reduce + owner broadcast.  Both
+    ranks return the single-GPU 9-tuple (first 7 entries) bit for bit."""
+    import torch.multiprocessing as mp
+    ticks = list(_ticks())
+    single = _planner(num_batch=512)
+    ref = [single.compute_cem(*a) for a in ticks]
+    mgr = mp.get_context("spawn").Manager()
+    out = mgr.dict()
+    mp.spawn(_sharded_worker, args=(2, _port(), ticks, out), nprocs=2, join=True)
+    for r in range(2):
+        for got, want in zip(out[r], ref):
+            for x, y in zip(got, want[:7]):
+                np.testing.assert_array_equal(np.asarray(x, dtype=np.asarray(y).dtype), np.asarray(y))
