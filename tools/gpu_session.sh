@@ -18,7 +18,7 @@ run() {  # name timeout cmd...
 }
 STEPS=${STEPS:-all}
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
-  run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 fi
 if [[ $STEPS == all || $STEPS == *smoke* ]]; then
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
