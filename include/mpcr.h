@@ -117,6 +117,11 @@ int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, con
                       float* thetadot, uint64_t* best_key, int index_base, int* status, int flags,
                       void* stream);
 
+/* Diagnostic: resident workgroups (= candidates) per CU, static LDS bytes and
+   VGPRs of the two rollout kernel variants on `device`:
+   info[6] = narrow (blocks, lds, vgprs), dual-arm class (blocks, lds, vgprs). */
+int mpcr_rollout_occupancy(int device, int* info);
+
 /* Same as mpcr_rollout_cost with MPCR_F_DEVICE_PTRS, except that the
    per-call arguments are a device block read when the kernel runs:
    params[20] = init_pos[8] | (w_pos, w_rot, w_col, 0) | ptgt[3], 0 | qtgt[4]

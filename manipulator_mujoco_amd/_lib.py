@@ -27,6 +27,7 @@ EXPORTS = (
     "mpcr_rollout_cost", "mpcr_argmin", "mpcr_best_key_decode", "mpcr_topk", "mpcr_cem_create", "mpcr_cem_free",
     "mpcr_cem_factor", "mpcr_cem_sample_project", "mpcr_project", "mpcr_cem_update", "mpcr_rollout_cost_dp",
     "mpcr_plant_create", "mpcr_plant_free", "mpcr_plant_set_state", "mpcr_plant_get_state", "mpcr_plant_step",
+    "mpcr_rollout_occupancy",
 )
 _VOID = ("mpcr_last_error", "mpcr_model_free", "mpcr_engine_free", "mpcr_best_key_decode", "mpcr_cem_free",
          "mpcr_plant_free")
@@ -80,6 +81,7 @@ def load():
     lib.mpcr_plant_set_state.argtypes = [vp, P(d), P(d), P(d)]
     lib.mpcr_plant_get_state.argtypes = [vp, P(d), P(d), P(d), P(d)]
     lib.mpcr_plant_step.argtypes = [vp, P(d), i, vp]
+    lib.mpcr_rollout_occupancy.argtypes = [i, P(i)]
     for name in EXPORTS + ("mpcr_rollout_trace",):
         if name not in _VOID:
             getattr(lib, name).restype = i

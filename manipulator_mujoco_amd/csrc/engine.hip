@@ -18,6 +18,11 @@ struct RolloutArgs;
 
 // kernels (rollout.hip: the fused rollout; cem.hip: the CEM distribution step)
 #include "rollout.hip"
+
+// extra dynamic LDS per narrow-kernel block (occupancy experiments only)
+#ifndef MPCR_N_DYN_LDS
+#define MPCR_N_DYN_LDS 0
+#endif
 #include "cem.hip"
 
 using namespace mpcr;
@@ -41,6 +46,7 @@ struct mpcr_engine {
   int* d_status = nullptr;
   int* d_idx = nullptr;
   float* d_slot_prev = nullptr;  // max_n x nslot (variants keeping cost_c history in HBM)
+  float* d_jx = nullptr;         // max_n x (MAXEFC - JL) x LDJ: narrow variant's J rows past the LDS ones
   // convex hulls (dual-arm class)
   float4* d_hull_vert = nullptr;
   int2* d_hull_info = nullptr;
@@ -566,6 +572,8 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       hipMalloc(&e->d_status, sizeof(int) * max_n) != hipSuccess ||
       hipMalloc(&e->d_idx, sizeof(int) * max_n) != hipSuccess ||
       hipMalloc(&e->d_slot_prev, sizeof(float) * (size_t)max_n * (e->host.nslot > 0 ? e->host.nslot : 1)) !=
+          hipSuccess ||
+      hipMalloc(&e->d_jx, sizeof(float) * (size_t)max_n * (SmemN::MAXEFC - SmemN::JL + 1) * SmemN::LDJ) !=
           hipSuccess) {
     mpcr_engine_free(e);
     return fail(MPCR_ENOMEM, "device allocation failed");
@@ -591,6 +599,7 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_status);
   (void)hipFree(e->d_idx);
   (void)hipFree(e->d_slot_prev);
+  (void)hipFree(e->d_jx);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
   (void)hipFree(e->d_hull_adjv);
@@ -632,6 +641,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.trace_eef = l.trace_eef;
   a.trace_slots = l.trace_slots;
   a.slot_prev = e->d_slot_prev;
+  a.jx = e->d_jx;
   a.dpar = l.dpar;
   a.state = l.state;
   a.plant = l.plant;
@@ -645,8 +655,25 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   if (e->wide)
     hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(l.n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
   else
-    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(l.n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
+    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(l.n), dim3(WAVE), MPCR_N_DYN_LDS, st, a, (const DevModel*)e->d_model);
   HIPCHK(hipGetLastError());
+  return MPCR_OK;
+}
+
+extern "C" int mpcr_rollout_occupancy(int device, int* info) {
+  if (!info) return fail(MPCR_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(device));
+  const void* k[2] = {reinterpret_cast<const void*>(&rollout_kernel<16, 16, 24, false>),
+                      reinterpret_cast<const void*>(&rollout_kernel<32, 32, 72, true>)};
+  for (int v = 0; v < 2; v++) {
+    int blocks = 0;
+    hipFuncAttributes fa;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k[v], WAVE, v == 0 ? MPCR_N_DYN_LDS : 0));
+    HIPCHK(hipFuncGetAttributes(&fa, k[v]));
+    info[3 * v] = blocks;
+    info[3 * v + 1] = (int)fa.sharedSizeBytes;
+    info[3 * v + 2] = fa.numRegs;
+  }
   return MPCR_OK;
 }
 
@@ -867,6 +894,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   std::memset(&a, 0, sizeof(a));
   a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
   a.slot_prev = e->d_slot_prev;
+  a.jx = e->d_jx;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   if (e->wide)

@@ -42,6 +42,7 @@ struct RolloutArgs {
   float* trace_eef;    // n x H x 7 (debug)
   float* trace_slots;  // n x H x nslot (debug)
   float* slot_prev;    // n x nslot previous slot distances (variants keeping them in HBM)
+  float* jx;           // n x (MAXEFC - JL) x LDJ: J rows past the LDS ones (narrow variant)
   unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs
@@ -61,10 +62,13 @@ struct RolloutArgs {
 // reading 16 different rows hit distinct bank quads (LD*r mod 64 distinct
 // multiples of 4 for LD = 20 and 36) -> conflict free, 4x fewer LDS
 // instructions than b32.
-template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false>
+template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false,
+          int JL_ = MAXEFC_>
 struct __align__(16) SmemT {
   static constexpr int NVW = NVW_, NBW = NBW_, NGW = NGW_, LD = NVW_ + 4;
   static constexpr int MAXEFC = MAXEFC_, LDJ = LDJ_;      // constraint rows kept, J row stride
+  static constexpr int JL = JL_;  // J rows held in LDS; rows JL.. live in the block's HBM slab (RolloutArgs::jx)
+  static_assert(JL <= MAXEFC && JL % 4 == 0, "J rows in LDS");
   static constexpr bool CPREV_GLOBAL = CPREV_GLOBAL_;     // previous slot distances in HBM (L2) instead of LDS
   static constexpr int LOG_NVW = NVW_ == 32 ? 5 : 4;
   static constexpr bool WIDE = NVW_ == 32;  // dual-arm class: equalities, actuators, convex hulls
@@ -114,7 +118,7 @@ struct __align__(16) SmemT {
       int con_pair[DX_MAXACT];
       int con_row[DX_MAXACT];
       float poly[2][8][4];  // box-box clipping polygon (double buffered)
-      alignas(16) float J[MAXEFC][LDJ];
+      alignas(16) float J[JL][LDJ];
       float efc_D[MAXEFC];
       float efc_aref[MAXEFC];
       float efc_jar[MAXEFC];
@@ -125,17 +129,31 @@ struct __align__(16) SmemT {
     };
   };
 };
-// the two variants: single-arm scenes (nv <= 16) and the dual-arm class
+// The two variants: single-arm scenes (nv <= 16) and the dual-arm class.
+// Single-arm image: 96 constraint rows of which the first 56 keep their J row
+// in LDS (stride 16) and the rest in a per-candidate HBM slab (p99 of the
+// bench scenes' per-step maximum is 40-54 rows, so the slab is rarely
+// touched), previous slot distances in HBM: 12.4 KB of LDS -> 12 blocks per
+// CU = 3 waves/SIMD at 130 VGPRs (was 17.3 KB, 2 waves/SIMD).  Measured on
+// MI355X: 12 resident blocks need <= 12704 B each (12832 B runs at the
+// 11-block speed although hipOccupancy reports 12), i.e. about 150 KB of the
+// CU's LDS is allocatable to one kernel's blocks.
 #ifndef MPCR_N_MAXEFC
-#define MPCR_N_MAXEFC 96
+#define MPCR_N_MAXEFC DX_MAXEFC
+#endif
+#ifndef MPCR_N_JL
+#define MPCR_N_JL 56
 #endif
 #ifndef MPCR_N_LDJ
-#define MPCR_N_LDJ 20
+#define MPCR_N_LDJ 16
 #endif
 #ifndef MPCR_N_CPREV_GLOBAL
-#define MPCR_N_CPREV_GLOBAL 0
+#define MPCR_N_CPREV_GLOBAL 1
 #endif
-using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL>;
+using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, MPCR_N_JL>;
+#if !defined(MPCR_N_LDS_UNCHECKED)
+static_assert(sizeof(SmemN) <= 12704, "narrow LDS image must fit 12 blocks per CU (see above)");
+#endif
 using SmemW = SmemT<32, 32, 72>;
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
@@ -1268,6 +1286,16 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
     asm volatile("" : "+s"(z_));         \
     m = m0 + z_;                         \
   } while (0)
+// The lane index is laundered once per step the same way (narrow variant):
+// otherwise every lane-mask compare (lane > k in the register Cholesky,
+// lane < nv, ...) is a loop invariant the compiler hoists out of the horizon
+// loop into an SGPR pair, which then spills to VGPR lanes (two v_readlane per
+// use) and keeps lane-derived addresses live across the step: 178 -> 130
+// VGPRs, i.e. 3 waves/SIMD instead of 2 once the LDS image fits (below).
+#ifndef MPCR_LANE_LAUNDER
+#define MPCR_LANE_LAUNDER 1
+#endif
+#define LAUNDER_LANE() asm volatile("" : "+v"(lane))
 // phase-boundary launders (-DMPCR_PHASE_LAUNDER=0 keeps only the per-step one)
 #ifndef MPCR_PHASE_LAUNDER
 #define MPCR_PHASE_LAUNDER 0
@@ -1279,6 +1307,32 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
   do {                  \
   } while (0)
 #endif
+
+// ---------------------------------------------------------------------------
+// J row access: rows < JL in LDS, the rest in the block's HBM slab gx.  The
+// branches are per lane, and the HBM side is skipped (execz) unless a lane
+// has a row past JL.
+
+template <class S>
+__device__ __forceinline__ void jstore(S& s, float* gx, int r, int i, float v) {
+  if (S::JL == S::MAXEFC || r < S::JL) s.J[r][i] = v;
+  else gx[(r - S::JL) * S::LDJ + i] = v;
+}
+template <class S>
+__device__ __forceinline__ float jdot(const S& s, const float* gx, int r, const float* vec) {
+  if (S::JL == S::MAXEFC || r < S::JL) return dotN<S::NVW>(s.J[r], vec);
+  return dotN<S::NVW>(gx + (r - S::JL) * S::LDJ, vec);
+}
+// body(row pointer, r) over rows r = r0, r0 + step, ... < nefc: the LDS rows,
+// then the slab rows (two loops, no per-row address-space select)
+template <class S, class F>
+__device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int step, int nefc, F&& body) {
+  const int n1 = nefc < S::JL ? nefc : S::JL;
+  for (int r = r0; r < n1; r += step) body(&s.J[r][0], r);
+  if constexpr (S::JL < S::MAXEFC) {
+    for (int r = S::JL + r0; r < nefc; r += step) body(gx + (r - S::JL) * S::LDJ, r);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // the kernel
@@ -1298,11 +1352,12 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
   __shared__ S s;
   const DevModel* __restrict__ const m0 = mptr;
   const DevModel* __restrict__ m = m0;
-  const int lane = threadIdx.x;
+  int lane = threadIdx.x;  // laundered per step (LAUNDER_LANE)
   const int b = blockIdx.x;
   if (b >= args.n) return;
   const int H = args.H;
   const int nv = m->nv, nb = m->nbody, nc = m->nctrl;
+  float* const gx = S::JL < S::MAXEFC ? args.jx + (size_t)b * (S::MAXEFC - S::JL) * S::LDJ : nullptr;
 
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
   //      (plant mode: the caller's state, no init_pos override)
@@ -1343,6 +1398,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
     // all live across the whole step (244 VGPRs + SGPR spills).  The loads
     // stay in their phases and hit L1/L2.
     LAUNDER_MODEL();
+    if constexpr (!WIDE && MPCR_LANE_LAUNDER) LAUNDER_LANE();
     // ---- qvel[:nctrl] = thetadot_t (basis evaluated on the fly) -------------
     if (lane < nc) {
       float v;
@@ -1912,7 +1968,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         } else if (i == m->jnt_dofadr[id]) {
           v = side == 0 ? 1.f : -1.f;
         }
-        s.J[r][i] = v;
+        jstore(s, gx, r, i, v);
       }
       // contact Jacobians: (contact, dof) -> J_n +- mu J_t rows
       for (int idx = lane; idx < keep_con * NVW; idx += WAVE) {
@@ -1939,15 +1995,15 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         const float jn = f[0] * jd[0] + f[1] * jd[1] + f[2] * jd[2];
         const int off = s.con_row[c];
         if (m->pair_condim[p] == 1) {
-          s.J[off][i] = jn;
+          jstore(s, gx, off, i, jn);
         } else {
           const float mu = m->pair_friction[p];
           const float jt1 = f[3] * jd[0] + f[4] * jd[1] + f[5] * jd[2];
           const float jt2 = f[6] * jd[0] + f[7] * jd[1] + f[8] * jd[2];
-          s.J[off + 0][i] = jn + mu * jt1;
-          s.J[off + 1][i] = jn - mu * jt1;
-          s.J[off + 2][i] = jn + mu * jt2;
-          s.J[off + 3][i] = jn - mu * jt2;
+          jstore(s, gx, off + 0, i, jn + mu * jt1);
+          jstore(s, gx, off + 1, i, jn - mu * jt1);
+          jstore(s, gx, off + 2, i, jn + mu * jt2);
+          jstore(s, gx, off + 3, i, jn - mu * jt2);
         }
       }
       sync();
@@ -1993,7 +2049,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           sref = m->pair_solref[p];
           simp = m->pair_solimp[p];
         }
-        const float vel = dotN<NVW>(s.J[r], s.qvel);
+        const float vel = jdot(s, gx, r, s.qvel);
         const float imp = impedance(simp, pos, margin);
         const float R = fmaxf((1.f - imp) / imp * diag, kMinVal);
         float tc = sref[0];
@@ -2034,8 +2090,8 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           const float gs = lane < nv ? (mas - s.qfs[lane]) * (s.qas[lane] - s.qas[lane]) : 0.f;
           float cw = 0.f, cs = 0.f;
           for (int r = lane; r < nefc; r += WAVE) {
-            const float jw = dotN<NVW>(s.J[r], s.qws) - s.efc_aref[r];
-            const float js = dotN<NVW>(s.J[r], s.qas) - s.efc_aref[r];
+            const float jw = jdot(s, gx, r, s.qws) - s.efc_aref[r];
+            const float js = jdot(s, gx, r, s.qas) - s.efc_aref[r];
             const bool eq = (s.efc_src[r] >> 24) == 1;
             if (eq || jw < 0.f) cw += s.efc_D[r] * jw * jw;
             if (eq || js < 0.f) cs += s.efc_D[r] * js * js;
@@ -2060,7 +2116,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           const float ma = lane < nv ? dotN<NVW>(s.M[lane], s.qacc) : 0.f;
           float cc = 0.f;
           for (int r = lane; r < nefc; r += WAVE) {
-            const float jar = dotN<NVW>(s.J[r], s.qacc) - s.efc_aref[r];
+            const float jar = jdot(s, gx, r, s.qacc) - s.efc_aref[r];
             const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
             const float D = s.efc_D[r];
             s.efc_jar[r] = jar;
@@ -2076,7 +2132,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           constexpr int RPW = WAVE / NVW;
           const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
           float qc = 0.f;
-          for (int r = gq; r < nefc; r += RPW) qc = fmaf(s.J[r][gi], s.efc_f[r], qc);
+          jrows(s, gx, gq, RPW, nefc, [&](const float* J, int r) { qc = fmaf(J[gi], s.efc_f[r], qc); });
 #pragma unroll
           for (int o = NVW; o < WAVE; o <<= 1) qc += __shfl_xor(qc, o);
           const float grad = lane < nv ? ma - s.qfs[lane] - qc : 0.f;
@@ -2097,15 +2153,15 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
             float4 hq[QPL];
 #pragma unroll
             for (int k = 0; k < QPL; k++) hq[k] = reinterpret_cast<const float4*>(s.M[gi])[gq + RPW * k];
-            for (int r = 0; r < nefc; r++) {
-              const float c = s.efc_Da[r] * s.J[r][gi];
+            jrows(s, gx, 0, 1, nefc, [&](const float* J, int r) {
+              const float c = s.efc_Da[r] * J[gi];
 #pragma unroll
               for (int k = 0; k < QPL; k++) {
-                const float4 v = reinterpret_cast<const float4*>(s.J[r])[gq + RPW * k];
+                const float4 v = reinterpret_cast<const float4*>(J)[gq + RPW * k];
                 hq[k].x = fmaf(c, v.x, hq[k].x); hq[k].y = fmaf(c, v.y, hq[k].y);
                 hq[k].z = fmaf(c, v.z, hq[k].z); hq[k].w = fmaf(c, v.w, hq[k].w);
               }
-            }
+            });
 #pragma unroll
             for (int k = 0; k < QPL; k++) reinterpret_cast<float4*>(Hs + gi * S::LD)[gq + RPW * k] = hq[k];
           }
@@ -2127,7 +2183,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
           sync();
           // Mv, jv, quadratic coefficients
           const float mvv = lane < nv ? dotN<NVW>(s.M[lane], s.srch) : 0.f;
-          for (int r = lane; r < nefc; r += WAVE) s.efc_jv[r] = dotN<NVW>(s.J[r], s.srch);
+          for (int r = lane; r < nefc; r += WAVE) s.efc_jv[r] = jdot(s, gx, r, s.srch);
           const float sn = sqrtf(wsum(search * search));
           const float gtol = m->tolerance * m->ls_tolerance * sn * m->meaninertia * (float)(nv > 1 ? nv : 1);
           float qg[3];
@@ -2186,7 +2242,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         implicit = true;
         const int nefc = s.nefc;
         for (int r = lane; r < nefc; r += WAVE) {
-          const float jar = dotN<NVW>(s.J[r], s.qacc) - s.efc_aref[r];
+          const float jar = jdot(s, gx, r, s.qacc) - s.efc_aref[r];
           const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
           s.efc_f[r] = act ? -s.efc_D[r] * jar : 0.f;
         }
@@ -2194,7 +2250,7 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
         constexpr int RPW = WAVE / NVW;
         const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
         float qc = 0.f;
-        for (int r = gq; r < nefc; r += RPW) qc = fmaf(s.J[r][gi], s.efc_f[r], qc);
+        jrows(s, gx, gq, RPW, nefc, [&](const float* J, int r) { qc = fmaf(J[gi], s.efc_f[r], qc); });
 #pragma unroll
         for (int o = NVW; o < WAVE; o <<= 1) qc += __shfl_xor(qc, o);
         const float dt = m->timestep;

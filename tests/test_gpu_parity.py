@@ -176,6 +176,30 @@ def test_full_size_properties(torch_cuda):
     assert (rel < TOL).mean() >= 0.95, np.sort(rel)[-4:]
 
 
+def test_rows_past_lds_match_oracle(torch_cuda):
+    """The narrow kernel keeps the J rows of the first 56 constraint rows in LDS
+    and the rest in a per-candidate HBM slab: candidates of the C3 batch whose
+    busiest step needs more rows than that go through the slab path and must
+    match the oracle like the others (and the wide kernel, LDS only)."""
+    torch = torch_cuda
+    n, H = 4096, 50
+    m = models.load("scene_mjx", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
+    e = Engine(m, H, n, Pd)
+    st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    a = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, status=st).cpu().numpy()
+    rows = ((st.cpu().numpy() >> 2) & 63)
+    sel = np.where(rows > 56)[0][:12]
+    assert len(sel) >= 4, np.sort(rows)[-8:]
+    td = np.einsum("tk,njk->njt", Pd, xi.cpu().numpy()[sel].reshape(-1, 6, 11).astype(np.float64)).reshape(-1, 6 * H)
+    o = oracle.rollout(m, td, Q0, W, PT, QT, want_slots=True)
+    rel = np.abs(a[sel, 0] - o["cost4"][:, 0]) / np.abs(o["cost4"][:, 0])
+    graze = (np.abs(o["slots"]) < 1e-5).any(axis=(1, 2))
+    assert (rel[~graze] < TOL).mean() >= 0.75, np.sort(rel)[-4:]
+    assert np.median(rel) < 1e-4
+
+
 def test_compute_cem_dropin(torch_cuda):
     from manipulator_mujoco_amd.planner import cem_planner
     p = cem_planner(num_dof=6, num_batch=256, num_steps=16, timestep=0.05, maxiter_cem=3, num_elite=0.05,

@@ -41,5 +41,13 @@ for _ in range(int(os.environ.get("R", 10))):
     b.record()
     torch.cuda.synchronize()
     ts.append(a.elapsed_time(b))
-print(f"{os.path.basename(sys.argv[1])} {name} median {np.median(ts):.3f} ms min {np.min(ts):.3f} "
+occ = ""
+lib = _lib.load()
+if hasattr(lib, "mpcr_rollout_occupancy"):
+    import ctypes
+    info = (ctypes.c_int * 6)()
+    lib.mpcr_rollout_occupancy.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    if lib.mpcr_rollout_occupancy(0, info) == 0:
+        occ = f" [narrow {info[0]} blocks/CU, {info[1]} B LDS, {info[2]} VGPR]"
+print(f"{os.path.basename(sys.argv[1])}{occ} {name} median {np.median(ts):.3f} ms min {np.min(ts):.3f} "
       f"-> {n / np.median(ts) * 1e3:.0f} rollouts/s  cost0 {float(c4[:, 0].sum()):.6e}")
