@@ -76,7 +76,9 @@ struct __align__(16) SmemT {
   static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
   static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
   // ---- persistent across the step ----
-  float xi[DX_NCTRL * 12];  // order <= 11 Bernstein coefficients per controlled joint
+  // order <= 11 Bernstein coefficients per controlled joint (narrow variant:
+  // read from HBM / L2 each step instead, the LDS is the occupancy limiter)
+  float xi[WIDE ? DX_NCTRL * 12 : 1];
   float qpos[NQW];
   alignas(16) float qvel[NVW];
   alignas(16) float qacc[NVW];
@@ -112,37 +114,45 @@ struct __align__(16) SmemT {
       float fvec[NVW][8];
     };
     struct {
-      float con_pos[DX_MAXACT][4];
-      float con_frame[DX_MAXACT][12];
-      float con_dist[DX_MAXACT];
-      int con_pair[DX_MAXACT];
-      int con_row[DX_MAXACT];
-      float poly[2][8][4];  // box-box clipping polygon (double buffered)
       alignas(16) float J[JL][LDJ];
       float efc_D[MAXEFC];
       float efc_aref[MAXEFC];
-      float efc_jar[MAXEFC];
-      float efc_jv[MAXEFC];
-      float efc_f[MAXEFC];   // -D * jar on active rows, else 0
-      float efc_Da[MAXEFC];  // D on active rows, else 0
       int efc_src[MAXEFC];  // (kind << 24) | (index << 4) | side
+      union {
+        struct {  // collision .. constraint rows
+          float con_pos[DX_MAXACT][4];
+          float con_frame[DX_MAXACT][12];
+          float con_dist[DX_MAXACT];
+          int con_pair[DX_MAXACT];
+          int con_row[DX_MAXACT];
+          float poly[2][8][4];  // box-box clipping polygon (double buffered)
+        };
+        struct {  // Newton (the contacts are dead once the rows are built)
+          float efc_jar[MAXEFC];
+          float efc_jv[MAXEFC];
+          float efc_f[MAXEFC];   // -D * jar on active rows, else 0
+          float efc_Da[MAXEFC];  // D on active rows, else 0
+        };
+      };
     };
   };
 };
 // The two variants: single-arm scenes (nv <= 16) and the dual-arm class.
-// Single-arm image: 96 constraint rows of which the first 56 keep their J row
-// in LDS (stride 16) and the rest in a per-candidate HBM slab (p99 of the
-// bench scenes' per-step maximum is 40-54 rows, so the slab is rarely
-// touched), previous slot distances in HBM: 12.4 KB of LDS -> 12 blocks per
-// CU = 3 waves/SIMD at 130 VGPRs (was 17.3 KB, 2 waves/SIMD).  Measured on
-// MI355X: 12 resident blocks need <= 12704 B each (12832 B runs at the
-// 11-block speed although hipOccupancy reports 12), i.e. about 150 KB of the
-// CU's LDS is allocatable to one kernel's blocks.
+// Single-arm image: 96 constraint rows of which the first 36 keep their J row
+// in LDS (stride 16) and the rest in a per-candidate HBM slab (RolloutArgs::jx;
+// the per-step row count is ~23 on average, p50 of a candidate's busiest step
+// 39, so the slab serves a minority of the rows), the contacts overlaid with
+// the Newton-only row arrays, the cost history and the Bernstein
+// coefficients in HBM: 9.3 KB of LDS -> 16 blocks per CU = 4 waves/SIMD at 128
+// VGPRs (was 17.3 KB and 178 VGPRs: 2 waves/SIMD).  Measured on MI355X: 12
+// resident blocks need <= 12704 B each (12832 B runs at the 11-block speed
+// although hipOccupancy reports 12), i.e. about 150 KB of the CU's 160 KB LDS
+// is allocatable to one kernel's blocks; 16 blocks therefore need <= 9520 B.
 #ifndef MPCR_N_MAXEFC
 #define MPCR_N_MAXEFC DX_MAXEFC
 #endif
 #ifndef MPCR_N_JL
-#define MPCR_N_JL 56
+#define MPCR_N_JL 36
 #endif
 #ifndef MPCR_N_LDJ
 #define MPCR_N_LDJ 16
@@ -152,7 +162,7 @@ struct __align__(16) SmemT {
 #endif
 using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, MPCR_N_JL>;
 #if !defined(MPCR_N_LDS_UNCHECKED)
-static_assert(sizeof(SmemN) <= 12704, "narrow LDS image must fit 12 blocks per CU (see above)");
+static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU (see above)");
 #endif
 using SmemW = SmemT<32, 32, 72>;
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
@@ -1337,6 +1347,12 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 // ---------------------------------------------------------------------------
 // the kernel
 
+// The narrow variant is compiled for 4 waves/SIMD (<= 128 VGPRs; its LDS image
+// fits 16 blocks per CU): at the bench's 4096 candidates = 4 per SIMD every
+// candidate is resident at once (3 waves/SIMD: 3.52 ms, 4: 2.76 ms on C3).
+#ifndef MPCR_N_WAVES
+#define MPCR_N_WAVES 4
+#endif
 // occupancy experiments: -DMPCR_WAVES_PER_EU=n asks the compiler for n waves/SIMD
 #ifdef MPCR_WAVES_PER_EU
 #define MPCR_ROLLOUT_ATTR __attribute__((amdgpu_waves_per_eu(MPCR_WAVES_PER_EU, MPCR_WAVES_PER_EU)))
@@ -1345,7 +1361,7 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 #endif
 
 template <int NVW, int NBW, int NGW, bool WIDE>
-__global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
+__global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
   using S = typename std::conditional<WIDE, SmemW, SmemN>::type;
   static_assert(S::NVW == NVW && S::NBW == NBW && S::NGW == NGW, "variant widths");
@@ -1384,7 +1400,8 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
   if (lane < nc && !from_state) s.qpos[m->ctrl_qposadr[lane]] = s.par[PAR_Q0 + lane];
   if (args.layout == 0) {
     const int nx = nc * args.nbasis;
-    for (int i = lane; i < nx; i += WAVE) s.xi[i] = args.input[(size_t)b * nx + i];
+    if constexpr (S::WIDE)
+      for (int i = lane; i < nx; i += WAVE) s.xi[i] = args.input[(size_t)b * nx + i];
   }
   sync();
 
@@ -1405,7 +1422,8 @@ __global__ void __launch_bounds__(WAVE) MPCR_ROLLOUT_ATTR rollout_kernel(Rollout
       if (args.layout == 0) {
         v = 0.f;
         const float* pd = args.pdot + (size_t)t * args.nbasis;
-        for (int k = 0; k < args.nbasis; k++) v = fmaf(pd[k], s.xi[lane * args.nbasis + k], v);
+        const float* xi = S::WIDE ? s.xi : args.input + (size_t)b * nc * args.nbasis;
+        for (int k = 0; k < args.nbasis; k++) v = fmaf(pd[k], xi[lane * args.nbasis + k], v);
       } else {
         v = args.input[(size_t)b * nc * H + lane * H + t];
       }
