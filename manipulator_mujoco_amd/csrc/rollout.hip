@@ -368,6 +368,104 @@ __device__ __forceinline__ float chol_solve(const float (&l)[N], float b, int la
   return x;
 }
 
+// The same factorisation and solve for N = 16 (narrow variant) with DPP row
+// broadcasts instead of v_readlane: row_newbcast:j hands lane j's value to
+// every lane of its 16-lane row, and as the src0 modifier of v_fmac_f32 it
+// makes each (k, j) update of the right-looking factorisation ONE VALU
+// instruction (readlane + fma before, plus the SGPR hazards).  Lanes 16..63
+// run the same code on their own rows and their results are ignored.
+template <int J>
+__device__ __forceinline__ float rbc(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + J, 0xF, 0xF, true));
+}
+// acc -= bcast_J(src) * own.  NOP: src was just written by a VALU op (DPP
+// reads need 2 wait states; the compiler does not track them in inline asm)
+template <int J, bool NOP>
+__device__ __forceinline__ void fnmac_bc(float& acc, float src, float own) {
+  if constexpr (NOP)
+    asm("s_nop 1\n\tv_fmac_f32_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(src), "v"(own), "n"(J));
+  else
+    asm("v_fmac_f32_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(src), "v"(own), "n"(J));
+}
+template <int K, int J>
+struct Chol16Upd {  // a[j] -= l[j][k] * l[i][k] for j = J..15
+  static __device__ __forceinline__ void run(float (&a)[16], float lik) {
+    fnmac_bc<J, J == K + 1>(a[J], lik, lik);
+    Chol16Upd<K, J + 1>::run(a, lik);
+  }
+};
+template <int K>
+struct Chol16Upd<K, 16> {
+  static __device__ __forceinline__ void run(float (&)[16], float) {}
+};
+template <int K>
+struct Chol16 {  // column K; dinv collects 1 / l[i][i] at lane i
+  static __device__ __forceinline__ void run(float (&a)[16], float& dinv, int lane) {
+    const float dkk = sqrtf(fmaxf(rbc<K>(a[K]), kMinVal));
+    const float inv = 1.f / dkk;
+    const float lik = lane == K ? dkk : (lane > K ? a[K] * inv : 0.f);
+    a[K] = lik;
+    dinv = lane == K ? inv : dinv;
+    Chol16Upd<K, K + 1>::run(a, lik);
+    Chol16<K + 1>::run(a, dinv, lane);
+  }
+};
+template <>
+struct Chol16<16> {
+  static __device__ __forceinline__ void run(float (&)[16], float&, int) {}
+};
+// forward (L y = b) / backward (L^T x = y) sweeps: lane K finalises its value
+// t = acc / l_KK, one fused DPP FMA hands it to the other lanes' updates
+// (lanes already final see a zero coefficient: l is lower triangular)
+template <int K, int STEP>
+struct Sweep16 {
+  static __device__ __forceinline__ void run(const float (&c)[16], float& acc, float& out, float dinv, int lane) {
+    const float t = acc * dinv;
+    fnmac_bc<K, true>(acc, t, c[K]);
+    out = lane == K ? t : out;
+    Sweep16<K + STEP, STEP>::run(c, acc, out, dinv, lane);
+  }
+};
+template <int STEP>
+struct Sweep16<16, STEP> {
+  static __device__ __forceinline__ void run(const float (&)[16], float&, float&, float, int) {}
+};
+template <int STEP>
+struct Sweep16<-1, STEP> {
+  static __device__ __forceinline__ void run(const float (&)[16], float&, float&, float, int) {}
+};
+__device__ __forceinline__ void chol16(float (&a)[16], float& dinv, int lane) {
+  dinv = 0.f;
+  Chol16<0>::run(a, dinv, lane);
+}
+// x = L^-T L^-1 b (lane i: row i of L in l[]); Lt: LDS transpose scratch
+template <int LDL>
+__device__ __forceinline__ float chol16_solve(const float (&l)[16], float dinv, float b, int lane, float* Lt) {
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) Lt[j * LDL + lane] = l[j];
+  }
+  float acc = b, y = 0.f;
+  Sweep16<0, 1>::run(l, acc, y, dinv, lane);
+  sync();
+  float lt[16];
+  {
+    const float4* col = reinterpret_cast<const float4*>(Lt + (lane & 15) * LDL);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const float4 v = col[q];
+      lt[4 * q] = v.x; lt[4 * q + 1] = v.y; lt[4 * q + 2] = v.z; lt[4 * q + 3] = v.w;
+    }
+  }
+  float x = 0.f;
+  acc = y;
+  Sweep16<15, -1>::run(lt, acc, x, dinv, lane);
+  sync();
+  return x;
+}
+
 // ---------------------------------------------------------------------------
 // narrow phase (contact definitions identical to the oracle's)
 
@@ -1350,6 +1448,9 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 // The narrow variant is compiled for 4 waves/SIMD (<= 128 VGPRs; its LDS image
 // fits 16 blocks per CU): at the bench's 4096 candidates = 4 per SIMD every
 // candidate is resident at once (3 waves/SIMD: 3.52 ms, 4: 2.76 ms on C3).
+#ifndef MPCR_DPP_CHOL
+#define MPCR_DPP_CHOL 1
+#endif
 #ifndef MPCR_N_WAVES
 #define MPCR_N_WAVES 4
 #endif
@@ -1815,9 +1916,16 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
       float Lm[NVW];
 #pragma unroll
       for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? s.M[lane][j] : 0.f;
-      chol_rows(Lm, lane);
       // the dynamics region (xpos..fvec) is dead once M is assembled
-      const float x = chol_solve<NVW, S::LD>(Lm, lane < NVW ? s.qfs[lane] : 0.f, lane, &s.xpos[0][0]);
+      float x;
+      if constexpr (NVW == 16 && MPCR_DPP_CHOL) {
+        float dinv;
+        chol16(Lm, dinv, lane);
+        x = chol16_solve<S::LD>(Lm, dinv, lane < NVW ? s.qfs[lane] : 0.f, lane, &s.xpos[0][0]);
+      } else {
+        chol_rows(Lm, lane);
+        x = chol_solve<NVW, S::LD>(Lm, lane < NVW ? s.qfs[lane] : 0.f, lane, &s.xpos[0][0]);
+      }
       if (lane < NVW) s.qas[lane] = lane < nv ? x : 0.f;
     }
 
@@ -2193,8 +2301,15 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
               h[4 * q] = v.x; h[4 * q + 1] = v.y; h[4 * q + 2] = v.z; h[4 * q + 3] = v.w;
             }
           }
-          chol_rows(h, lane);
-          const float mg = chol_solve<NVW, S::LD>(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
+          float mg;
+          if constexpr (NVW == 16 && MPCR_DPP_CHOL) {
+            float dinv;
+            chol16(h, dinv, lane);
+            mg = chol16_solve<S::LD>(h, dinv, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
+          } else {
+            chol_rows(h, lane);
+            mg = chol_solve<NVW, S::LD>(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
+          }
           const float search = lane < nv ? -mg : 0.f;
           STAMP(14);
           if (lane < NVW) s.srch[lane] = search;
