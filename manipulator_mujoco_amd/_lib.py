@@ -12,7 +12,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpcr.so")
+LIB_PATH = os.environ.get("MPCR_LIB") or os.path.join(_HERE, "libmpcr.so")  # MPCR_LIB: A/B builds (tools/)
 
 MPCR_LAYOUT_XI = 0
 MPCR_LAYOUT_THETADOT = 1

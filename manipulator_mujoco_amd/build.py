@@ -11,8 +11,16 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = [os.path.join(HERE, "csrc", "engine.hip")]
-DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("rollout.hip", "cem.hip", "mpcr_device.h")] + [
+CSRC = os.path.join(HERE, "csrc")
+# translation units and their own device flags: the rollout kernel is built
+# without SLP vectorisation (packing scalar fp32 ops into v_pk_* pairs cost
+# more register-pair v_movs than it saved there: 1328 -> 649 static v_mov,
+# 126 -> 104 VGPRs, C3 2.59 -> 2.35 ms), the CEM step kernels keep it
+# (sample_project 0.38 -> 0.30 ms with it)
+UNITS = [(os.path.join(CSRC, "engine.hip"), []),
+         (os.path.join(CSRC, "rollout.hip"), ["-Xarch_device", "-fno-slp-vectorize"])]
+SRC = [u for u, _ in UNITS]
+DEPS = SRC + [os.path.join(CSRC, f) for f in ("rollout.h", "cem.hip", "mpcr_device.h")] + [
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mpcr.h", "mpcr_model.h")]
 OUT = os.path.join(HERE, "libmpcr.so")
 ARCH = os.environ.get("MPCR_OFFLOAD_ARCH", "gfx950")
@@ -24,7 +32,7 @@ ARCH = os.environ.get("MPCR_OFFLOAD_ARCH", "gfx950")
 # simplifycfg-sink-common=false: sinking the narrow phase's per-geometry-type
 # slot stores into one store with a phi'd index forced the slot arrays into
 # scratch (32 B/lane); without it they stay in registers (205 -> 179 VGPRs).
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-pass-failed",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-pass-failed",
          "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-Xarch_device", "-freciprocal-math",
          "-Xarch_device", "-fapprox-func", "-mllvm", "-simplifycfg-sink-common=false"]
 
@@ -36,18 +44,30 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+def compile_lib(out: str, extra=(), verbose: bool = False) -> str:
+    """Compile every unit (FLAGS + its own + extra) and link the shared library."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        objs = []
+        for src, unit_flags in UNITS:
+            obj = os.path.join(tmp, os.path.basename(src) + ".o")
+            cmd = [hipcc(), f"--offload-arch={ARCH}", "-c"] + FLAGS + list(unit_flags) + list(extra) + ["-o", obj, src]
+            if verbose:
+                cmd.append("-Rpass-analysis=kernel-resource-usage")
+                print(" ".join(cmd))
+            subprocess.run(cmd, check=True)
+            objs.append(obj)
+        subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(OUT):
         mt = os.path.getmtime(OUT)
         if all(os.path.getmtime(d) <= mt for d in DEPS):
             return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + ["-o", OUT + ".tmp"] + SRC
-    if verbose:
-        cmd.append("-Rpass-analysis=kernel-resource-usage")
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    return compile_lib(OUT, verbose=verbose)
 
 
 if __name__ == "__main__":

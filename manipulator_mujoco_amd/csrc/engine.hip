@@ -12,18 +12,39 @@
 #include "../../include/mpcr.h"
 #include "mpcr_device.h"
 
-namespace mpcr {
-struct RolloutArgs;
-}
-
-// kernels (rollout.hip: the fused rollout; cem.hip: the CEM distribution step)
-#include "rollout.hip"
+// kernels: the fused rollout is its own translation unit (rollout.hip, its
+// launchers declared in rollout.h); cem.hip: the CEM distribution step
+#include "rollout.h"
 
 // extra dynamic LDS per narrow-kernel block (occupancy experiments only)
 #ifndef MPCR_N_DYN_LDS
 #define MPCR_N_DYN_LDS 0
 #endif
 #include "cem.hip"
+
+namespace mpcr {
+// argmin with NaN-first / first-index semantics over cost[i*stride]
+__global__ void __launch_bounds__(256) argmin_kernel(const float* __restrict__ cost, int stride, int n, int base,
+                                                     unsigned long long* key) {
+  unsigned long long best = ~0ull;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float c = cost[(size_t)i * stride];
+    const uint32_t u = __float_as_uint(c);
+    const uint32_t k = isnan(c) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
+    const unsigned long long k64 = ((unsigned long long)k << 32) | (uint32_t)(base + i);
+    best = k64 < best ? k64 : best;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long other = __shfl_xor(best, o);
+    best = other < best ? other : best;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMin(key, best);
+}
+
+__global__ void fill_u64(unsigned long long* p, unsigned long long v) { *p = v; }
+
+}  // namespace mpcr
 
 using namespace mpcr;
 
@@ -652,10 +673,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.index_base = l.index_base;
   std::memcpy(a.par, l.par, sizeof(a.par));
   if (l.key && l.reset_key) hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, l.key, ~0ull);
-  if (e->wide)
-    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(l.n), dim3(WAVE), 0, st, a, (const DevModel*)e->d_model);
-  else
-    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(l.n), dim3(WAVE), MPCR_N_DYN_LDS, st, a, (const DevModel*)e->d_model);
+  rollout_launch(e->wide, a, (const DevModel*)e->d_model, l.n, MPCR_N_DYN_LDS, st);
   HIPCHK(hipGetLastError());
   return MPCR_OK;
 }
@@ -663,17 +681,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
 extern "C" int mpcr_rollout_occupancy(int device, int* info) {
   if (!info) return fail(MPCR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(device));
-  const void* k[2] = {reinterpret_cast<const void*>(&rollout_kernel<16, 16, 24, false>),
-                      reinterpret_cast<const void*>(&rollout_kernel<32, 32, 72, true>)};
-  for (int v = 0; v < 2; v++) {
-    int blocks = 0;
-    hipFuncAttributes fa;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k[v], WAVE, v == 0 ? MPCR_N_DYN_LDS : 0));
-    HIPCHK(hipFuncGetAttributes(&fa, k[v]));
-    info[3 * v] = blocks;
-    info[3 * v + 1] = (int)fa.sharedSizeBytes;
-    info[3 * v + 2] = fa.numRegs;
-  }
+  HIPCHK(rollout_occupancy(info, MPCR_N_DYN_LDS));
   return MPCR_OK;
 }
 
@@ -897,10 +905,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   a.jx = e->d_jx;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
-  if (e->wide)
-    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
-  else
-    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(n), dim3(WAVE), 0, nullptr, a, (const DevModel*)e->d_model);
+  rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(phases16, d_prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(d_prof);

@@ -5,168 +5,18 @@
 // passive), (dof, dof) entries (CRB mass matrix), collision pairs (narrow
 // phase), (contact, dof) entries (contact Jacobians) and constraint rows
 // (impedance, Newton line search).  The two dense SPD solves per step
-// (M and the Newton Hessian, nv <= 16) are done row-per-lane in registers
-// with v_readlane broadcasts: no LDS round trips inside the factorisation.
+// (M and the Newton Hessian) are done row-per-lane in registers with DPP
+// row broadcasts (nv <= 16) or v_readlane (the 32-wide dual-arm variant): no
+// LDS round trips inside the factorisation.  Built as its own translation
+// unit (flags: manipulator_mujoco_amd/build.py); host side in engine.hip.
 //
 // Semantics restated (same definitions as oracle/mpcr_oracle.c):
 //   rollout / output timing  SBP/mjx_planner.py:251-274
 //   cost                     SBP/mjx_planner.py:276-303
 //   mjx.step                 mujoco-mjx 3.3.1 (third party)
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include <type_traits>
-
-#include "mpcr_device.h"
+#include "rollout.h"
 
 namespace mpcr {
-
-constexpr float kMinVal = 1e-15f;
-constexpr float kMinImp = 0.0001f;
-constexpr float kMaxImp = 0.9999f;
-
-// per-call parameter block (RolloutArgs::par / dpar) and plant state layout
-enum { PAR_Q0 = 0, PAR_W = 8, PAR_PT = 12, PAR_QT = 16, PAR_N = 20 };
-enum { ST_QPOS = 0, ST_QVEL = DX_NQ, ST_QWS = ST_QVEL + DX_NV, ST_QACC = ST_QWS + DX_NV, ST_EEF = ST_QACC + DX_NV,
-       ST_N = ST_EEF + 8 };
-
-struct RolloutArgs {
-  const DevModel* m;
-  const float* input;
-  const float* pdot;  // H x nbasis
-  float* cost4;
-  float* theta;
-  float* thetadot;
-  unsigned long long* best_key;
-  int* status;
-  float* trace_eef;    // n x H x 7 (debug)
-  float* trace_slots;  // n x H x nslot (debug)
-  float* slot_prev;    // n x nslot previous slot distances (variants keeping them in HBM)
-  float* jx;           // n x (MAXEFC - JL) x LDJ: J rows past the LDS ones (narrow variant)
-  unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
-  // per-call parameters: by value (par) or, for graph-captured ticks, read
-  // from device memory (dpar, same layout) when the launch runs
-  const float* dpar;
-  // plant mode (single environment, mpcr_plant_*): plant & 1 starts from
-  // state (qpos | qvel | qacc_warmstart) instead of the template,
-  // plant & 2 writes the final state back; qacc and the pre-integration eef
-  // pose of the last step always go to state when plant != 0
-  float* state;
-  int layout, n, H, nbasis, index_base, plant;
-  float par[PAR_N];  // q0[8] | w[4] | ptgt[4] | qtgt[4] (any norm)
-};
-
-// Per-block LDS image, sized by the kernel variant: NVW = dense-solve width
-// (16 or 32 dofs), NBW = moving bodies, NGW = collision geoms.  Row stride
-// LD = NVW + 4 floats: rows are 16-byte aligned for ds_read_b128 and 16 lanes
-// reading 16 different rows hit distinct bank quads (LD*r mod 64 distinct
-// multiples of 4 for LD = 20 and 36) -> conflict free, 4x fewer LDS
-// instructions than b32.
-template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false,
-          int JL_ = MAXEFC_>
-struct __align__(16) SmemT {
-  static constexpr int NVW = NVW_, NBW = NBW_, NGW = NGW_, LD = NVW_ + 4;
-  static constexpr int MAXEFC = MAXEFC_, LDJ = LDJ_;      // constraint rows kept, J row stride
-  static constexpr int JL = JL_;  // J rows held in LDS; rows JL.. live in the block's HBM slab (RolloutArgs::jx)
-  static_assert(JL <= MAXEFC && JL % 4 == 0, "J rows in LDS");
-  static constexpr bool CPREV_GLOBAL = CPREV_GLOBAL_;     // previous slot distances in HBM (L2) instead of LDS
-  static constexpr int LOG_NVW = NVW_ == 32 ? 5 : 4;
-  static constexpr bool WIDE = NVW_ == 32;  // dual-arm class: equalities, actuators, convex hulls
-  static constexpr int NQW = WIDE ? DX_NQ : 24, NEQP = WIDE ? DX_NEQ : 1, NACT = WIDE ? DX_NU : 1;
-  static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
-  static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
-  // ---- persistent across the step ----
-  // order <= 11 Bernstein coefficients per controlled joint (narrow variant:
-  // read from HBM / L2 each step instead, the LDS is the occupancy limiter)
-  float xi[WIDE ? DX_NCTRL * 12 : 1];
-  float qpos[NQW];
-  alignas(16) float qvel[NVW];
-  alignas(16) float qacc[NVW];
-  alignas(16) float qws[NVW];
-  alignas(16) float qfs[NVW];   // qfrc_smooth
-  alignas(16) float qas[NVW];   // qacc_smooth
-  alignas(16) float srch[NVW];  // Newton search direction
-  float com[DX_NTREE][4];
-  float cdof[NVW][8];
-  alignas(16) float M[NVW][LD];
-  alignas(16) float gxpos[NGW][4];   // gxpos+gxmat (dead during Newton) double as the
-  float gxmat[NGW][12];  // Hessian solve's LDS scratch (NGW*16 >= NVW*LD)
-  float cprev[CPREV_GLOBAL ? 1 : DX_NSLOT];  // previous-step masked slot distances (cost_c)
-  float par[PAR_N];       // q0 | w | ptgt | qtgt (normalised)
-  float eqp[NEQP][2][4];  // connect anchors in world (body1, body2)
-  float actf[NACT];       // actuator forces
-  int cvx[CVXN];
-  short hint[NHINT][2];
-  int ncon, nefc, ncvx, pad_;
-  // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the
-  //      contact / constraint arrays (collision .. Newton) ----
-  union {
-    struct {
-      alignas(16) float xpos[NBW][4];
-      float xquat[NBW][4];
-      float xmat[NBW][12];
-      float xipos[NBW][4];
-      float cinert[NBW][12];
-      float crb[NBW][12];
-      float cvel[NBW][8];
-      float cfrc[NBW][8];
-      float cdofdot[NVW][8];
-      float fvec[NVW][8];
-    };
-    struct {
-      alignas(16) float J[JL][LDJ];
-      float efc_D[MAXEFC];
-      float efc_aref[MAXEFC];
-      int efc_src[MAXEFC];  // (kind << 24) | (index << 4) | side
-      union {
-        struct {  // collision .. constraint rows
-          float con_pos[DX_MAXACT][4];
-          float con_frame[DX_MAXACT][12];
-          float con_dist[DX_MAXACT];
-          int con_pair[DX_MAXACT];
-          int con_row[DX_MAXACT];
-          float poly[2][8][4];  // box-box clipping polygon (double buffered)
-        };
-        struct {  // Newton (the contacts are dead once the rows are built)
-          float efc_jar[MAXEFC];
-          float efc_jv[MAXEFC];
-          float efc_f[MAXEFC];   // -D * jar on active rows, else 0
-          float efc_Da[MAXEFC];  // D on active rows, else 0
-        };
-      };
-    };
-  };
-};
-// The two variants: single-arm scenes (nv <= 16) and the dual-arm class.
-// Single-arm image: 96 constraint rows of which the first 36 keep their J row
-// in LDS (stride 16) and the rest in a per-candidate HBM slab (RolloutArgs::jx;
-// the per-step row count is ~23 on average, p50 of a candidate's busiest step
-// 39, so the slab serves a minority of the rows), the contacts overlaid with
-// the Newton-only row arrays, the cost history and the Bernstein
-// coefficients in HBM: 9.3 KB of LDS -> 16 blocks per CU = 4 waves/SIMD at 128
-// VGPRs (was 17.3 KB and 178 VGPRs: 2 waves/SIMD).  Measured on MI355X: 12
-// resident blocks need <= 12704 B each (12832 B runs at the 11-block speed
-// although hipOccupancy reports 12), i.e. about 150 KB of the CU's 160 KB LDS
-// is allocatable to one kernel's blocks; 16 blocks therefore need <= 9520 B.
-#ifndef MPCR_N_MAXEFC
-#define MPCR_N_MAXEFC DX_MAXEFC
-#endif
-#ifndef MPCR_N_JL
-#define MPCR_N_JL 36
-#endif
-#ifndef MPCR_N_LDJ
-#define MPCR_N_LDJ 16
-#endif
-#ifndef MPCR_N_CPREV_GLOBAL
-#define MPCR_N_CPREV_GLOBAL 1
-#endif
-using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, MPCR_N_JL>;
-#if !defined(MPCR_N_LDS_UNCHECKED)
-static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU (see above)");
-#endif
-using SmemW = SmemT<32, 32, 72>;
-static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
-static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 
 // ---------------------------------------------------------------------------
 // diagnostic phase stamps (separate -DMPCR_PROFILE build; never in the timed one)
@@ -2465,25 +2315,32 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
   }
 }
 
-// argmin with NaN-first / first-index semantics over cost[i*stride]
-__global__ void __launch_bounds__(256) argmin_kernel(const float* __restrict__ cost, int stride, int n, int base,
-                                                     unsigned long long* key) {
-  unsigned long long best = ~0ull;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float c = cost[(size_t)i * stride];
-    const uint32_t u = __float_as_uint(c);
-    const uint32_t k = isnan(c) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
-    const unsigned long long k64 = ((unsigned long long)k << 32) | (uint32_t)(base + i);
-    best = k64 < best ? k64 : best;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long other = __shfl_xor(best, o);
-    best = other < best ? other : best;
-  }
-  if ((threadIdx.x & 63) == 0) atomicMin(key, best);
+// ---------------------------------------------------------------------------
+// launchers (the host side lives in another translation unit)
+
+void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigned grid, size_t dyn_lds,
+                    hipStream_t st) {
+  if (wide)
+    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), 0, st, a, dm);
+  else
+    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(grid), dim3(WAVE), dyn_lds, st, a, dm);
 }
 
-__global__ void fill_u64(unsigned long long* p, unsigned long long v) { *p = v; }
+hipError_t rollout_occupancy(int* info, size_t dyn_lds) {
+  const void* k[2] = {reinterpret_cast<const void*>(&rollout_kernel<16, 16, 24, false>),
+                      reinterpret_cast<const void*>(&rollout_kernel<32, 32, 72, true>)};
+  for (int v = 0; v < 2; v++) {
+    int blocks = 0;
+    hipFuncAttributes fa;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k[v], WAVE, v == 0 ? dyn_lds : 0);
+    if (e != hipSuccess) return e;
+    e = hipFuncGetAttributes(&fa, k[v]);
+    if (e != hipSuccess) return e;
+    info[3 * v] = blocks;
+    info[3 * v + 1] = (int)fa.sharedSizeBytes;
+    info[3 * v + 2] = fa.numRegs;
+  }
+  return hipSuccess;
+}
 
 }  // namespace mpcr

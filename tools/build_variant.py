@@ -4,7 +4,6 @@
     python tools/build_variant.py NAME [extra hipcc flags...]
 """
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -14,6 +13,5 @@ from manipulator_mujoco_amd import build  # noqa: E402
 name, extra = sys.argv[1], sys.argv[2:]
 out = os.path.join(ROOT, "build_variants", name + ".so")
 os.makedirs(os.path.dirname(out), exist_ok=True)
-cmd = [build.hipcc(), f"--offload-arch={build.ARCH}"] + build.FLAGS + extra + ["-o", out] + build.SRC
-subprocess.run(cmd, check=True)
+build.compile_lib(out, extra)
 print(out)

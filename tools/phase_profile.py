@@ -2,7 +2,6 @@
 Builds a separate -DMPCR_PROFILE library; never used for timing claims."""
 import ctypes
 import os
-import subprocess
 import sys
 
 import numpy as np
@@ -18,8 +17,7 @@ PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rn
 
 def main():
     so = os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr_prof.so")
-    subprocess.run([build.hipcc(), "--offload-arch=gfx950"] + build.FLAGS + ["-DMPCR_PROFILE", "-o", so] + build.SRC,
-                   check=True)
+    build.compile_lib(so, ["-DMPCR_PROFILE"])
     _lib.LIB_PATH = so
     lib = _lib.load()
     lib.mpcr_rollout_profile.restype = ctypes.c_int
