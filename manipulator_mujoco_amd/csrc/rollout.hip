@@ -286,13 +286,20 @@ template <int STEP>
 struct Sweep16<-1, STEP> {
   static __device__ __forceinline__ void run(const float (&)[16], float&, float&, float, int) {}
 };
+// MPCR_CHOL_LANE_LAUNDER: re-derive the lane compares inside the solves (one
+// v_cmp each) instead of letting them be hoisted into spilled SGPR pairs
+#ifndef MPCR_CHOL_LANE_LAUNDER
+#define MPCR_CHOL_LANE_LAUNDER 1
+#endif
 __device__ __forceinline__ void chol16(float (&a)[16], float& dinv, int lane) {
+  if (MPCR_CHOL_LANE_LAUNDER) asm volatile("" : "+v"(lane));
   dinv = 0.f;
   Chol16<0>::run(a, dinv, lane);
 }
 // x = L^-T L^-1 b (lane i: row i of L in l[]); Lt: LDS transpose scratch
 template <int LDL>
 __device__ __forceinline__ float chol16_solve(const float (&l)[16], float dinv, float b, int lane, float* Lt) {
+  if (MPCR_CHOL_LANE_LAUNDER) asm volatile("" : "+v"(lane));
   if (lane < 16) {
 #pragma unroll
     for (int j = 0; j < 16; j++) Lt[j * LDL + lane] = l[j];
@@ -1260,6 +1267,11 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
 #endif
 #if MPCR_PHASE_LAUNDER
 #define LAUNDER_PHASE() LAUNDER_MODEL()
+#elif MPCR_LANE_LAUNDER >= 2
+#define LAUNDER_PHASE()                \
+  do {                                 \
+    if constexpr (!WIDE) LAUNDER_LANE(); \
+  } while (0)
 #else
 #define LAUNDER_PHASE() \
   do {                  \
