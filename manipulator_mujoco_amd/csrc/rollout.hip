@@ -1368,6 +1368,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
   }
   sync();
 
+  // narrow variant: lane j < nctrl keeps joint j's Bernstein coefficients in
+  // registers for the whole horizon (nbasis <= 12, checked by the engine)
+  float xir[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++)
+    xir[k] = (!S::WIDE && args.layout == 0 && lane < nc && k < args.nbasis)
+                 ? args.input[((size_t)b * nc + lane) * args.nbasis + k] : 0.f;
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
   int status = 0, nefc_sum = 0, nefc_max = 0;
   PROF_DECL
@@ -1385,8 +1392,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
       if (args.layout == 0) {
         v = 0.f;
         const float* pd = args.pdot + (size_t)t * args.nbasis;
-        const float* xi = S::WIDE ? s.xi : args.input + (size_t)b * nc * args.nbasis;
-        for (int k = 0; k < args.nbasis; k++) v = fmaf(pd[k], xi[lane * args.nbasis + k], v);
+        if constexpr (S::WIDE) {
+          for (int k = 0; k < args.nbasis; k++) v = fmaf(pd[k], s.xi[lane * args.nbasis + k], v);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 12; k++)
+            if (k < args.nbasis) v = fmaf(pd[k], xir[k], v);
+        }
       } else {
         v = args.input[(size_t)b * nc * H + lane * H + t];
       }
