@@ -126,7 +126,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=4096)
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_rollout.csv"))
+    ap.add_argument("--pmc", default=None,
+                    help="rocprofv3 --pmc CSV of this workload (default: the committed C3 one for c3, else none)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.model = args.model or cfg["model"]
@@ -223,7 +224,8 @@ def main():
         flops_launch = fps * H * n
         achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
         hbm_launch = n * (66 * 4 + 16 + 2 * 6 * H * 4 + 4)  # xi in; cost4, theta, thetadot, status out
-        traffic = pmc_traffic(args.pmc)
+        pmc = args.pmc or (os.path.join(ROOT, "profiles", "r01_pmc_rollout.csv") if args.config == "c3" else None)
+        traffic = pmc_traffic(pmc) if pmc else None
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": "rollouts/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
