@@ -67,7 +67,8 @@ struct mpcr_engine {
   int* d_status = nullptr;
   int* d_idx = nullptr;
   float* d_slot_prev = nullptr;  // max_n x nslot (variants keeping cost_c history in HBM)
-  float* d_jx = nullptr;         // max_n x (MAXEFC - JL) x LDJ: narrow variant's J rows past the LDS ones
+  float* d_jx = nullptr;         // max_n x (MAXEFC - JL) x LDJ: J rows past the LDS ones
+  short* d_hints = nullptr;      // max_n x NHINT x 2 (dual-arm class): hull-climb starts
   // convex hulls (dual-arm class)
   float4* d_hull_vert = nullptr;
   int2* d_hull_info = nullptr;
@@ -594,8 +595,11 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       hipMalloc(&e->d_idx, sizeof(int) * max_n) != hipSuccess ||
       hipMalloc(&e->d_slot_prev, sizeof(float) * (size_t)max_n * (e->host.nslot > 0 ? e->host.nslot : 1)) !=
           hipSuccess ||
-      hipMalloc(&e->d_jx, sizeof(float) * (size_t)max_n * (SmemN::MAXEFC - SmemN::JL + 1) * SmemN::LDJ) !=
-          hipSuccess) {
+      hipMalloc(&e->d_jx, sizeof(float) * (size_t)max_n *
+                              (e->wide ? (SmemW::MAXEFC - SmemW::JL + 1) * SmemW::LDJ
+                                       : (SmemN::MAXEFC - SmemN::JL + 1) * SmemN::LDJ)) !=
+          hipSuccess ||
+      hipMalloc(&e->d_hints, sizeof(short) * 2 * (size_t)max_n * (e->wide ? SmemW::NHINT : 1)) != hipSuccess) {
     mpcr_engine_free(e);
     return fail(MPCR_ENOMEM, "device allocation failed");
   }
@@ -621,6 +625,7 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_idx);
   (void)hipFree(e->d_slot_prev);
   (void)hipFree(e->d_jx);
+  (void)hipFree(e->d_hints);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
   (void)hipFree(e->d_hull_adjv);
@@ -663,6 +668,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.trace_slots = l.trace_slots;
   a.slot_prev = e->d_slot_prev;
   a.jx = e->d_jx;
+  a.hints = e->d_hints;
   a.dpar = l.dpar;
   a.state = l.state;
   a.plant = l.plant;
@@ -903,6 +909,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
   a.slot_prev = e->d_slot_prev;
   a.jx = e->d_jx;
+  a.hints = e->d_hints;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);

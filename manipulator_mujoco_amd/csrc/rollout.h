@@ -34,7 +34,8 @@ struct RolloutArgs {
   float* trace_eef;    // n x H x 7 (debug)
   float* trace_slots;  // n x H x nslot (debug)
   float* slot_prev;    // n x nslot previous slot distances (variants keeping them in HBM)
-  float* jx;           // n x (MAXEFC - JL) x LDJ: J rows past the LDS ones (narrow variant)
+  float* jx;           // n x (MAXEFC - JL) x LDJ: J rows past the LDS ones
+  short* hints;        // n x NHINT x 2: hull-climb start per convex pair and side (dual-arm class)
   unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs
@@ -68,9 +69,6 @@ struct __align__(16) SmemT {
   static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
   static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
   // ---- persistent across the step ----
-  // order <= 11 Bernstein coefficients per controlled joint (narrow variant:
-  // read from HBM / L2 each step instead, the LDS is the occupancy limiter)
-  float xi[WIDE ? DX_NCTRL * 12 : 1];
   float qpos[NQW];
   alignas(16) float qvel[NVW];
   alignas(16) float qacc[NVW];
@@ -79,7 +77,7 @@ struct __align__(16) SmemT {
   alignas(16) float qas[NVW];   // qacc_smooth
   alignas(16) float srch[NVW];  // Newton search direction
   float com[DX_NTREE][4];
-  float cdof[NVW][8];
+  float cdof[NVW][WIDE ? 6 : 8];
   alignas(16) float M[NVW][LD];
   alignas(16) float gxpos[NGW][4];   // gxpos+gxmat (dead during Newton) double as the
   float gxmat[NGW][12];  // Hessian solve's LDS scratch (NGW*16 >= NVW*LD)
@@ -87,8 +85,6 @@ struct __align__(16) SmemT {
   float par[PAR_N];       // q0 | w | ptgt | qtgt (normalised)
   float eqp[NEQP][2][4];  // connect anchors in world (body1, body2)
   float actf[NACT];       // actuator forces
-  int cvx[CVXN];
-  short hint[NHINT][2];
   int ncon, nefc, ncvx, pad_;
   // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the
   //      contact / constraint arrays (collision .. Newton) ----
@@ -106,7 +102,10 @@ struct __align__(16) SmemT {
       float fvec[NVW][8];
     };
     struct {
-      alignas(16) float J[JL][LDJ];
+      union {
+        alignas(16) float J[JL][LDJ];  // constraint rows .. Newton
+        int cvx[CVXN];                  // collision: the compacted convex-pair list
+      };
       float efc_D[MAXEFC];
       float efc_aref[MAXEFC];
       int efc_src[MAXEFC];  // (kind << 24) | (index << 4) | side
@@ -156,9 +155,17 @@ using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, 
 #if !defined(MPCR_N_LDS_UNCHECKED)
 static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU (see above)");
 #endif
-using SmemW = SmemT<32, 32, 72>;
+// Dual-arm image: J rows past 40 in the HBM slab, cost history and hull-climb
+// hints in HBM (the class has no robot-masked slots), the convex-pair list
+// inside the J rows, 6-float cdof rows: 21.6 KB -> 7 blocks per CU (was
+// 32.3 KB, 4); the kernel is compiled for 2 waves/SIMD (<= 256 VGPRs).
+#ifndef MPCR_W_JL
+#define MPCR_W_JL 40
+#endif
+using SmemW = SmemT<32, 32, 72, DX_MAXEFC, 36, true, MPCR_W_JL>;
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
+static_assert(SmemW::JL * SmemW::LDJ >= SmemW::CVXN, "convex-pair list inside the J rows");
 
 
 // launchers (defined in rollout.hip): the rollout kernel variant for the

@@ -48,14 +48,21 @@ __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 // full-wave sum, result uniform: DPP inside each 16-lane row (quad_perm
-// [1,0,3,2], [2,3,0,1], row_ror:4, row_ror:8) + 4 readlanes.  No LDS
+// [1,0,3,2], [2,3,0,1], row_ror:4, row_ror:8), then the GCN row_bcast:15 /
+// row_bcast:31 steps carry the row sums into lane 63, one readlane.  No LDS
 // traffic (a __shfl_xor butterfly is 6 dependent ds_bpermute round trips).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dppf_rows(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
 __device__ __forceinline__ float wsum(float v) {
   v += dppf<0xB1>(v);
   v += dppf<0x4E>(v);
   v += dppf<0x124>(v);
   v += dppf<0x128>(v);
-  return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
+  v += dppf_rows<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+  v += dppf_rows<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+  return rdlane(v, 63);
 }
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
@@ -642,7 +649,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
 // per-lane narrow phase for plane/capsule/box-vs-capsule pairs (box-box is
 // wave-cooperative, below).  out: dist[4], pos[4][3], nrm[4][3]
 template <class S>
-__device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const S& s, int p, float dist[4],
+__device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const S& s, short* hints, int p, float dist[4],
                             float pos[4][3], float nrm[4][3]) {
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   const int func = m->pair_func[p];
@@ -823,12 +830,13 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
   if constexpr (S::WIDE) {
     // hull hill climbs start where this pair's previous step ended (the
     // oracle keeps the same per-pair cache)
-    short* hp = const_cast<short*>(&s.hint[p - m->cvx_base][0]);
-    int hint[2] = {hp[0], hp[1]};
+    int* hp = reinterpret_cast<int*>(hints) + (p - m->cvx_base);  // (side 0, side 1) as two shorts
+    const int hv = *hp;
+    int hint[2] = {(int)(short)(hv & 0xffff), hv >> 16};
     if (func == 9) {  // general convex (MPR)
       float depth, n[3], pp[3];
       const bool hit = mpr_lane(m, s, g1, g2, depth, n, pp, hint);
-      hp[0] = (short)hint[0]; hp[1] = (short)hint[1];
+      *hp = (hint[0] & 0xffff) | (hint[1] << 16);
       if (hit) {
         if (n[0] == 0.f && n[1] == 0.f && n[2] == 0.f) n[2] = 1.f;
         dist[0] = -depth;
@@ -840,7 +848,7 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
     if (func == 10) {  // plane - convex: deepest support point
       float n[3] = {R1[2], R1[5], R1[8]}, nn[3] = {-R1[2], -R1[5], -R1[8]}, q[3];
       support_geom(m, s, g2, nn, q, hint[1]);
-      hp[1] = (short)hint[1];
+      *hp = (hint[0] & 0xffff) | (hint[1] << 16);
       const float d = n[0] * (q[0] - x1[0]) + n[1] * (q[1] - x1[1]) + n[2] * (q[2] - x1[2]);
       dist[0] = d;
 #pragma unroll
@@ -1313,6 +1321,12 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 #ifndef MPCR_DPP_CHOL
 #define MPCR_DPP_CHOL 1
 #endif
+// The dual-arm variant is compiled for 2 waves/SIMD (<= 256 registers incl.
+// AGPRs; uncapped it took 274 and ran 1 wave/SIMD): with its 21.6 KB image,
+// 7 blocks per CU instead of 4 (dual arm 4096 x 50: 47.5 -> 35.8 ms).
+#ifndef MPCR_W_WAVES
+#define MPCR_W_WAVES 2
+#endif
 #ifndef MPCR_N_WAVES
 #define MPCR_N_WAVES 4
 #endif
@@ -1324,7 +1338,7 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 #endif
 
 template <int NVW, int NBW, int NGW, bool WIDE>
-__global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
+__global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
   using S = typename std::conditional<WIDE, SmemW, SmemN>::type;
   static_assert(S::NVW == NVW && S::NBW == NBW && S::NGW == NGW, "variant widths");
@@ -1337,12 +1351,14 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
   const int H = args.H;
   const int nv = m->nv, nb = m->nbody, nc = m->nctrl;
   float* const gx = S::JL < S::MAXEFC ? args.jx + (size_t)b * (S::MAXEFC - S::JL) * S::LDJ : nullptr;
+  short* const hx = S::WIDE ? args.hints + (size_t)b * S::NHINT * 2 : nullptr;
 
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
   //      (plant mode: the caller's state, no init_pos override)
   if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
   if constexpr (S::WIDE) {
-    for (int i = lane; i < S::NHINT; i += WAVE) { s.hint[i][0] = -1; s.hint[i][1] = -1; }
+    int* h = reinterpret_cast<int*>(args.hints + (size_t)b * S::NHINT * 2);
+    for (int i = lane; i < S::NHINT; i += WAVE) h[i] = -1;  // both sides -1
   }
   const bool from_state = (args.plant & 1) != 0;
   for (int i = lane; i < S::NQW; i += WAVE)
@@ -1361,19 +1377,14 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
     s.par[PAR_QT + 3] = q[3] / qn;
   }
   if (lane < nc && !from_state) s.qpos[m->ctrl_qposadr[lane]] = s.par[PAR_Q0 + lane];
-  if (args.layout == 0) {
-    const int nx = nc * args.nbasis;
-    if constexpr (S::WIDE)
-      for (int i = lane; i < nx; i += WAVE) s.xi[i] = args.input[(size_t)b * nx + i];
-  }
   sync();
 
-  // narrow variant: lane j < nctrl keeps joint j's Bernstein coefficients in
-  // registers for the whole horizon (nbasis <= 12, checked by the engine)
+  // lane j < nctrl keeps joint j's Bernstein coefficients in registers for
+  // the whole horizon (nbasis <= 12, checked by the engine)
   float xir[12];
 #pragma unroll
   for (int k = 0; k < 12; k++)
-    xir[k] = (!S::WIDE && args.layout == 0 && lane < nc && k < args.nbasis)
+    xir[k] = (args.layout == 0 && lane < nc && k < args.nbasis)
                  ? args.input[((size_t)b * nc + lane) * args.nbasis + k] : 0.f;
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
   int status = 0, nefc_sum = 0, nefc_max = 0;
@@ -1392,13 +1403,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
       if (args.layout == 0) {
         v = 0.f;
         const float* pd = args.pdot + (size_t)t * args.nbasis;
-        if constexpr (S::WIDE) {
-          for (int k = 0; k < args.nbasis; k++) v = fmaf(pd[k], s.xi[lane * args.nbasis + k], v);
-        } else {
 #pragma unroll
-          for (int k = 0; k < 12; k++)
-            if (k < args.nbasis) v = fmaf(pd[k], xir[k], v);
-        }
+        for (int k = 0; k < 12; k++)
+          if (k < args.nbasis) v = fmaf(pd[k], xir[k], v);
       } else {
         v = args.input[(size_t)b * nc * H + lane * H + t];
       }
@@ -1855,7 +1862,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
       }
       float dist[4] = {1e30f, 1e30f, 1e30f, 1e30f}, pos[4][3] = {}, nrm[4][3] = {};
       int nsl = 0;
-      if (run && func != 4 && !defer) nsl = narrow_lane(m, s, p, dist, pos, nrm);
+      if (run && func != 4 && !defer) nsl = narrow_lane(m, s, hx, p, dist, pos, nrm);
       STAMP(11);
       const unsigned long long bbm = __ballot(run && func == 4);
       emit_contacts(m, s, args, b, t, H, valid && func != 4 && !defer, p, nsl, dist, pos, nrm, cost_c);
@@ -1875,7 +1882,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? 1 : MPCR_N_WAVES) MPCR_ROLLOUT_AT
             const bool v = i0 + lane < nc;
             const int pc = v ? s.cvx[i0 + lane] : 0;
             float cd[4] = {1e30f, 1e30f, 1e30f, 1e30f}, cp[4][3] = {}, cn[4][3] = {};
-            const int cn_sl = v ? narrow_lane(m, s, pc, cd, cp, cn) : 0;
+            const int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn) : 0;
             emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c);
           }
           sync();

@@ -25,6 +25,7 @@ proj = ProjectionFilter(P, Pd, Pdd, 6, torch.device("cpu"))
 xi = proj(torch.tensor(np.random.default_rng(20250632).normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32)),
           proj.boundary(q0, np.zeros(6), np.zeros(6), n), 10).cuda()
 e = Engine(m, H, n, Pd)
+st = torch.zeros(n, dtype=torch.int32, device="cuda")
 c4 = torch.empty((n, 4), device="cuda")
 th = torch.empty((n, 6 * H), device="cuda")
 td = torch.empty((n, 6 * H), device="cuda")
@@ -48,6 +49,11 @@ if hasattr(lib, "mpcr_rollout_occupancy"):
     info = (ctypes.c_int * 6)()
     lib.mpcr_rollout_occupancy.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     if lib.mpcr_rollout_occupancy(0, info) == 0:
-        occ = f" [narrow {info[0]} blocks/CU, {info[1]} B LDS, {info[2]} VGPR]"
-print(f"{os.path.basename(sys.argv[1])}{occ} {name} median {np.median(ts):.3f} ms min {np.min(ts):.3f} "
+        occ = (f" [narrow {info[0]} blocks/CU, {info[1]} B LDS, {info[2]} VGPR;"
+               f" wide {info[3]} blocks/CU, {info[4]} B LDS, {info[5]} VGPR]")
+e.rollout_cost(*args, cost4=c4, theta=th, thetadot=td, best_key=key, status=st)
+sv = st.cpu().numpy()
+rows = f" rows/step {float((sv >> 8).mean()) / H:.1f} max-rows p50/p90/p99 " + "/".join(
+    str(int(np.percentile((sv >> 2) & 63, q))) for q in (50, 90, 99))
+print(f"{os.path.basename(sys.argv[1])}{occ}{rows} {name} median {np.median(ts):.3f} ms min {np.min(ts):.3f} "
       f"-> {n / np.median(ts) * 1e3:.0f} rollouts/s  cost0 {float(c4[:, 0].sum()):.6e}")
