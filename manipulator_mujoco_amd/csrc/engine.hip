@@ -593,9 +593,11 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       hipMalloc(&e->d_key, sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&e->d_status, sizeof(int) * max_n) != hipSuccess ||
       hipMalloc(&e->d_idx, sizeof(int) * max_n) != hipSuccess ||
-      hipMalloc(&e->d_slot_prev, sizeof(float) * (size_t)max_n * (e->host.nslot > 0 ? e->host.nslot : 1)) !=
+      // per-candidate scratch slabs: one spare row for the empty group of a
+      // two-candidate wave (narrow kernel, odd n)
+      hipMalloc(&e->d_slot_prev, sizeof(float) * ((size_t)max_n + 1) * (e->host.nslot > 0 ? e->host.nslot : 1)) !=
           hipSuccess ||
-      hipMalloc(&e->d_jx, sizeof(float) * (size_t)max_n *
+      hipMalloc(&e->d_jx, sizeof(float) * ((size_t)max_n + 1) *
                               (e->wide ? (SmemW::MAXEFC - SmemW::JL + 1) * SmemW::LDJ
                                        : (SmemN::MAXEFC - SmemN::JL + 1) * SmemN::LDJ)) !=
           hipSuccess ||

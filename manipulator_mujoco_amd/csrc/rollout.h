@@ -56,9 +56,11 @@ struct RolloutArgs {
 // multiples of 4 for LD = 20 and 36) -> conflict free, 4x fewer LDS
 // instructions than b32.
 template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false,
-          int JL_ = MAXEFC_>
+          int JL_ = MAXEFC_, int CPW_ = 1>
 struct __align__(16) SmemT {
   static constexpr int NVW = NVW_, NBW = NBW_, NGW = NGW_, LD = NVW_ + 4;
+  // candidates per wave: CPW images per workgroup, HL = 64 / CPW lanes each
+  static constexpr int CPW = CPW_, HL = WAVE / CPW_;
   static constexpr int MAXEFC = MAXEFC_, LDJ = LDJ_;      // constraint rows kept, J row stride
   static constexpr int JL = JL_;  // J rows held in LDS; rows JL.. live in the block's HBM slab (RolloutArgs::jx)
   static_assert(JL <= MAXEFC && JL % 4 == 0, "J rows in LDS");
@@ -151,7 +153,10 @@ struct __align__(16) SmemT {
 #ifndef MPCR_N_CPREV_GLOBAL
 #define MPCR_N_CPREV_GLOBAL 1
 #endif
-using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, MPCR_N_JL>;
+#ifndef MPCR_N_CPW
+#define MPCR_N_CPW 1
+#endif
+using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, MPCR_N_JL, MPCR_N_CPW>;
 #if !defined(MPCR_N_LDS_UNCHECKED)
 static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU (see above)");
 #endif

@@ -80,7 +80,54 @@ __device__ __forceinline__ int wscan_excl(int v, int& total) {
   return pre;
 }
 __device__ __forceinline__ void sync() { __syncthreads(); }
-__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+
+// Candidate groups: a wave may carry CPW candidates of HL = 64 / CPW lanes
+// (lanes [32 h, 32 h + 32) for candidate h when CPW = 2).  These are the
+// group-local forms of the wave primitives above; ballots keep their bits in
+// place, restricted to the own group, so lanes_below / __popcll apply as is.
+template <int CPW>
+__device__ __forceinline__ int hlane() { return threadIdx.x & (WAVE / CPW - 1); }
+template <int CPW>
+__device__ __forceinline__ int hbase() { return threadIdx.x & (WAVE - WAVE / CPW); }
+template <int CPW>
+__device__ __forceinline__ unsigned long long hmask() {
+  if constexpr (CPW == 1) return ~0ull;
+  else return threadIdx.x >= 32 ? 0xffffffff00000000ull : 0xffffffffull;
+}
+template <int CPW>
+__device__ __forceinline__ unsigned long long hballot(bool p) { return __ballot(p) & hmask<CPW>(); }
+template <int CPW>
+__device__ __forceinline__ float hrdlane(float v, int l) {
+  if constexpr (CPW == 1) return rdlane(v, l);
+  else return threadIdx.x >= 32 ? rdlane(v, 32 + l) : rdlane(v, l);
+}
+template <int CPW>
+__device__ __forceinline__ float hsum(float v) {
+  if constexpr (CPW == 1) {
+    return wsum(v);
+  } else {
+    v += dppf<0xB1>(v);
+    v += dppf<0x4E>(v);
+    v += dppf<0x124>(v);
+    v += dppf<0x128>(v);
+    v += dppf_rows<0x142, 0xA>(v);  // rows 1, 3 += rows 0, 2: group sums in lanes 31, 63
+    return threadIdx.x >= 32 ? rdlane(v, 63) : rdlane(v, 31);
+  }
+}
+template <int CPW, class T>
+__device__ __forceinline__ T hshfl(T x, int src) { return __shfl(x, src + hbase<CPW>()); }
+template <int CPW>
+__device__ __forceinline__ int hscan_excl(int v, int& total) {
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int bit = 0; bit < 3; bit++) {
+    const unsigned long long mk = hballot<CPW>((v >> bit) & 1);
+    pre += lanes_below(mk) << bit;
+    tot += __popcll(mk) << bit;
+  }
+  total = tot;
+  return pre;
+}
 
 // ---------------------------------------------------------------------------
 // small vector math
@@ -943,19 +990,19 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
   int face_id = -1, edge_lane = -1;
 #pragma unroll
   for (int a = 0; a < 6; a++) {
-    const float v = rdlane(sep, a);
+    const float v = hrdlane<S::CPW>(sep, a);
     if (v > best_face) { best_face = v; face_id = a; }
   }
 #pragma unroll
   for (int a = 6; a < 15; a++) {
-    const float v = rdlane(sep, a);
+    const float v = hrdlane<S::CPW>(sep, a);
     if (v > -1e30f && v > best_edge) { best_edge = v; edge_lane = a; }
   }
   const float best = fmaxf(best_face, best_edge);
   if (!(best < margin)) return;
   const bool use_edge = edge_lane >= 0 && best_edge > 0.95f * best_face + 1e-5f;
   const int src = use_edge ? edge_lane : face_id;
-  float n[3] = {rdlane(L[0], src), rdlane(L[1], src), rdlane(L[2], src)};
+  float n[3] = {hrdlane<S::CPW>(L[0], src), hrdlane<S::CPW>(L[1], src), hrdlane<S::CPW>(L[2], src)};
   const float sg = dot3(t, n) >= 0.f ? 1.f : -1.f;
   n[0] *= sg; n[1] *= sg; n[2] *= sg;
   const int base = s.ncon;
@@ -1067,7 +1114,7 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
       e1 = (dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f);
     }
     int tot;
-    const int o = wscan_excl(e0 + e1, tot);
+    const int o = hscan_excl<S::CPW>(e0 + e1, tot);
     if (e0) {
 #pragma unroll
       for (int k = 0; k < 3; k++) s.poly[cur ^ 1][o][k] = P[k];
@@ -1090,7 +1137,7 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
     depth = hrf - dot3(rel, nf);
     keep = -depth < margin;
   }
-  const unsigned long long km = __ballot(keep);
+  const unsigned long long km = hballot<S::CPW>(keep);
   const int nkeep = __popcll(km);
   if (nkeep == 0) return;
   const int rank = lanes_below(km);  // position of this lane among the kept points
@@ -1102,9 +1149,10 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
     float dbest = -3e38f;
 #pragma unroll
     for (int c = 0; c < 8; c++) {
-      const float dc = rdlane(depth, c);
-      const bool kc = (km >> c) & 1ull;
-      const int rc = __popcll(km & ((1ull << c) - 1ull));
+      const int cb = c + hbase<S::CPW>();  // lane c of this group
+      const float dc = hrdlane<S::CPW>(depth, c);
+      const bool kc = (km >> cb) & 1ull;
+      const int rc = __popcll(km & ((1ull << cb) - 1ull));
       if (kc && dc > dbest) { dbest = dc; d0 = rc; }
     }
     slot = -1;
@@ -1149,7 +1197,7 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
           float* cp = S::CPREV_GLOBAL ? args.slot_prev + (size_t)b * m->nslot : s.cprev;
           if (t > 0) cost_c += fmaxf(cp[sa + c] * (1.f - 0.005f) - d, 0.f);
           cp[sa + c] = d;
-          if (args.trace_slots) args.trace_slots[((size_t)b * H + t) * m->nslot + sa + c] = d;
+          if (args.trace_slots && b < args.n) args.trace_slots[((size_t)b * H + t) * m->nslot + sa + c] = d;
         }
       }
     }
@@ -1160,7 +1208,7 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
     }
   }
   int tot;
-  const int pre = wscan_excl(act, tot);
+  const int pre = hscan_excl<S::CPW>(act, tot);
   const int base = s.ncon;
   if (act) {
     const float mg = m->pair_margin[p];
@@ -1182,7 +1230,7 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
     }
   }
   sync();
-  if (lane_id() == 0) s.ncon = base + tot;
+  if (hlane<S::CPW>() == 0) s.ncon = base + tot;
   sync();
 }
 
@@ -1194,7 +1242,7 @@ struct LsPt { float alpha, cost, d0, d1; };
 template <class S>
 __device__ __forceinline__ void ls_rows(const S& s, int lane, float alpha, float& q0, float& q1, float& q2) {
   q0 = q1 = q2 = 0.f;
-  for (int r = lane; r < s.nefc; r += WAVE) {
+  for (int r = lane; r < s.nefc; r += S::HL) {
     float jar = s.efc_jar[r], jv = s.efc_jv[r];
     float x = jar + alpha * jv;
     if (((s.efc_src[r] >> 24) == 1) || x < 0.f) {
@@ -1219,9 +1267,9 @@ template <class S>
 __device__ __forceinline__ LsPt ls_eval(const S& s, int lane, const float qg[3], float alpha) {
   float q0, q1, q2;
   ls_rows(s, lane, alpha, q0, q1, q2);
-  q0 = wsum(q0) + qg[0];
-  q1 = wsum(q1) + qg[1];
-  q2 = wsum(q2) + qg[2];
+  q0 = hsum<S::CPW>(q0) + qg[0];
+  q1 = hsum<S::CPW>(q1) + qg[1];
+  q2 = hsum<S::CPW>(q2) + qg[2];
   return ls_make(alpha, q0, q1, q2);
 }
 
@@ -1232,7 +1280,7 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
                                          LsPt& p0, LsPt& p1, LsPt& p2) {
   float q[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const float al[3] = {a0, a1, a2};
-  for (int r = lane; r < s.nefc; r += WAVE) {
+  for (int r = lane; r < s.nefc; r += S::HL) {
     const float jar = s.efc_jar[r], jv = s.efc_jv[r], D = s.efc_D[r];
     const bool eq = (s.efc_src[r] >> 24) == 1;
     const float c0 = 0.5f * D * jar * jar, c1 = D * jv * jar, c2 = 0.5f * D * jv * jv;
@@ -1242,7 +1290,7 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
     }
   }
 #pragma unroll
-  for (int k = 0; k < 9; k++) q[k] = wsum(q[k]) + qg[k % 3];
+  for (int k = 0; k < 9; k++) q[k] = hsum<S::CPW>(q[k]) + qg[k % 3];
   p0 = ls_make(a0, q[0], q[1], q[2]);
   p1 = ls_make(a1, q[3], q[4], q[5]);
   p2 = ls_make(a2, q[6], q[7], q[8]);
@@ -1338,16 +1386,19 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 #endif
 
 template <int NVW, int NBW, int NGW, bool WIDE>
-__global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
+__global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / SmemN::CPW) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
   using S = typename std::conditional<WIDE, SmemW, SmemN>::type;
   static_assert(S::NVW == NVW && S::NBW == NBW && S::NGW == NGW, "variant widths");
-  __shared__ S s;
+  __shared__ S sm[S::CPW];  // one LDS image per candidate of the wave
+  S& s = sm[S::CPW == 1 ? 0 : (int)(threadIdx.x >> 5)];
   const DevModel* __restrict__ const m0 = mptr;
   const DevModel* __restrict__ m = m0;
-  int lane = threadIdx.x;  // laundered per step (LAUNDER_LANE)
-  const int b = blockIdx.x;
-  if (b >= args.n) return;
+  int lane = hlane<S::CPW>();  // lane within the candidate's group; laundered per step (LAUNDER_LANE)
+  const int b = blockIdx.x * S::CPW + (S::CPW == 1 ? 0 : (int)(threadIdx.x >> 5));
+  const bool live = b < args.n;  // the last wave's second group may be empty
+  if (S::CPW == 1 && !live) return;
+  const int bi = live ? b : args.n - 1;  // an empty group replays a real candidate, writes nothing
   const int H = args.H;
   const int nv = m->nv, nb = m->nbody, nc = m->nctrl;
   float* const gx = S::JL < S::MAXEFC ? args.jx + (size_t)b * (S::MAXEFC - S::JL) * S::LDJ : nullptr;
@@ -1358,10 +1409,10 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
   if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
   if constexpr (S::WIDE) {
     int* h = reinterpret_cast<int*>(args.hints + (size_t)b * S::NHINT * 2);
-    for (int i = lane; i < S::NHINT; i += WAVE) h[i] = -1;  // both sides -1
+    for (int i = lane; i < S::NHINT; i += S::HL) h[i] = -1;  // both sides -1
   }
   const bool from_state = (args.plant & 1) != 0;
-  for (int i = lane; i < S::NQW; i += WAVE)
+  for (int i = lane; i < S::NQW; i += S::HL)
     s.qpos[i] = i < m->nq ? (from_state ? args.state[ST_QPOS + i] : m->qpos_init[i]) : 0.f;
   if (lane < NVW) {
     const bool v = lane < nv;
@@ -1385,7 +1436,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
 #pragma unroll
   for (int k = 0; k < 12; k++)
     xir[k] = (args.layout == 0 && lane < nc && k < args.nbasis)
-                 ? args.input[((size_t)b * nc + lane) * args.nbasis + k] : 0.f;
+                 ? args.input[((size_t)bi * nc + lane) * args.nbasis + k] : 0.f;
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
   int status = 0, nefc_sum = 0, nefc_max = 0;
   PROF_DECL
@@ -1407,10 +1458,10 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
         for (int k = 0; k < 12; k++)
           if (k < args.nbasis) v = fmaf(pd[k], xir[k], v);
       } else {
-        v = args.input[(size_t)b * nc * H + lane * H + t];
+        v = args.input[(size_t)bi * nc * H + lane * H + t];
       }
       s.qvel[m->ctrl_dofadr[lane]] = v;
-      if (args.thetadot) args.thetadot[(size_t)b * nc * H + lane * H + t] = v;
+      if (args.thetadot && live) args.thetadot[(size_t)b * nc * H + lane * H + t] = v;
     }
     sync();
 
@@ -1461,9 +1512,10 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
       for (int r = 0; r < m->jump_rounds; r++) {
         const int src = anc >= 0 ? anc : lane;
         float aq[4], ap[3];
-        aq[0] = __shfl(q[0], src); aq[1] = __shfl(q[1], src); aq[2] = __shfl(q[2], src); aq[3] = __shfl(q[3], src);
-        ap[0] = __shfl(p[0], src); ap[1] = __shfl(p[1], src); ap[2] = __shfl(p[2], src);
-        const int aanc = __shfl(anc, src);
+        aq[0] = hshfl<S::CPW>(q[0], src); aq[1] = hshfl<S::CPW>(q[1], src);
+        aq[2] = hshfl<S::CPW>(q[2], src); aq[3] = hshfl<S::CPW>(q[3], src);
+        ap[0] = hshfl<S::CPW>(p[0], src); ap[1] = hshfl<S::CPW>(p[1], src); ap[2] = hshfl<S::CPW>(p[2], src);
+        const int aanc = hshfl<S::CPW>(anc, src);
         if (anc >= 0) {
           float R[9], w[3];
           q2m(R, aq);
@@ -1535,9 +1587,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
     }
     for (int tr = 0; tr < m->ntree; tr++) {
       float mm = (lane < nb && m->body_tree[lane] == tr) ? m->body_mass[lane] : 0.f;
-      float cx = wsum(mm * (lane < nb ? s.xipos[lane][0] : 0.f));
-      float cy = wsum(mm * (lane < nb ? s.xipos[lane][1] : 0.f));
-      float cz = wsum(mm * (lane < nb ? s.xipos[lane][2] : 0.f));
+      float cx = hsum<S::CPW>(mm * (lane < nb ? s.xipos[lane][0] : 0.f));
+      float cy = hsum<S::CPW>(mm * (lane < nb ? s.xipos[lane][1] : 0.f));
+      float cz = hsum<S::CPW>(mm * (lane < nb ? s.xipos[lane][2] : 0.f));
       if (lane == 0) {
         float tm = m->tree_mass[tr];
         s.com[tr][0] = cx / tm; s.com[tr][1] = cy / tm; s.com[tr][2] = cz / tm;
@@ -1567,11 +1619,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
       float qn = sqrtf(eq[0] * eq[0] + eq[1] * eq[1] + eq[2] * eq[2] + eq[3] * eq[3]);
       float dq = fabsf((eq[0] * qt[0] + eq[1] * qt[1] + eq[2] * qt[2] + eq[3] * qt[3]) / qn);
       cost_r += 2.f * acosf(clampf(dq, -1.f, 1.f));
-      if (args.trace_eef) {
+      if (args.trace_eef && live) {
         float* e = args.trace_eef + ((size_t)b * H + t) * 7;
         e[0] = ep[0]; e[1] = ep[1]; e[2] = ep[2]; e[3] = eq[0]; e[4] = eq[1]; e[5] = eq[2]; e[6] = eq[3];
       }
-      if (args.plant && t == H - 1) {
+      if (args.plant && t == H - 1 && live) {
         float* e = args.state + ST_EEF;
         e[0] = ep[0]; e[1] = ep[1]; e[2] = ep[2]; e[3] = eq[0]; e[4] = eq[1]; e[5] = eq[2]; e[6] = eq[3];
       }
@@ -1669,7 +1721,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
     STAMP(3);
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- CRB, velocity, RNE + gravcomp (subtree sums by bitmask) -----------
-    for (int idx = lane; idx < nb * 10; idx += WAVE) {
+    for (int idx = lane; idx < nb * 10; idx += S::HL) {
       const int bb = idx / 10, k = idx - bb * 10;
       uint32_t sm = m->body_submask[bb];
       float acc = 0.f;
@@ -1748,7 +1800,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
     STAMP(4);
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // mass matrix entries (chain-masked) + bias forces
-    for (int idx = lane; idx < NVW * NVW; idx += WAVE) {
+    for (int idx = lane; idx < NVW * NVW; idx += S::HL) {
       const int i = idx >> S::LOG_NVW, j = idx & (NVW - 1);
       float v = 0.f;
       if (i < nv && j < nv) {
@@ -1817,8 +1869,8 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
     //      that pass the bounding-sphere cull are solved wave-cooperatively
     if (lane == 0) { s.ncon = 0; s.ncvx = 0; }
     sync();
-    for (int k = 0; k * WAVE < m->npair; k++) {
-      const int p = lane + k * WAVE;
+    for (int k = 0; k * S::HL < m->npair; k++) {
+      const int p = lane + k * S::HL;
       const bool valid = p < m->npair;
       const int func = valid ? m->pair_func[p] : -1;
       bool run = valid;
@@ -1864,7 +1916,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
       int nsl = 0;
       if (run && func != 4 && !defer) nsl = narrow_lane(m, s, hx, p, dist, pos, nrm);
       STAMP(11);
-      const unsigned long long bbm = __ballot(run && func == 4);
+      const unsigned long long bbm = hballot<S::CPW>(run && func == 4);
       emit_contacts(m, s, args, b, t, H, valid && func != 4 && !defer, p, nsl, dist, pos, nrm, cost_c);
       STAMP(12);
       if (bbm && !(m->disableflags & 16)) {
@@ -1872,13 +1924,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
         while (mm) {
           const int q = __builtin_ctzll(mm);
           mm &= mm - 1;
-          box_box_wave(m, s, k * WAVE + q, lane);
+          box_box_wave(m, s, k * S::HL + q - hbase<S::CPW>(), lane);
         }
       }
       if constexpr (S::WIDE) {
-        if (s.ncvx > S::CVXN - WAVE || (k + 1) * WAVE >= m->npair) {  // flush (pair order is kept)
+        if (s.ncvx > S::CVXN - WAVE || (k + 1) * S::HL >= m->npair) {  // flush (pair order is kept)
           const int nc = s.ncvx;
-          for (int i0 = 0; i0 < nc; i0 += WAVE) {
+          for (int i0 = 0; i0 < nc; i0 += S::HL) {
             const bool v = i0 + lane < nc;
             const int pc = v ? s.cvx[i0 + lane] : 0;
             float cd[4] = {1e30f, 1e30f, 1e30f, 1e30f}, cp[4][3] = {}, cn[4][3] = {};
@@ -1912,18 +1964,18 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
         if (m->jnt_range[lane][1] - q < m->jnt_margin[lane]) { nlim_l++; lsides |= 2; }
       }
       int nlim;
-      const int lim_pre = wscan_excl(nlim_l, nlim);
+      const int lim_pre = hscan_excl<S::CPW>(nlim_l, nlim);
       int ncr = 0;
       if (lane < ncon) ncr = m->pair_condim[s.con_pair[lane]] == 1 ? 1 : 4;
       int ncrow;
-      const int con_pre = wscan_excl(ncr, ncrow);
+      const int con_pre = hscan_excl<S::CPW>(ncr, ncrow);
       int nefc = neq + nlim + ncrow;
       int keep_con = ncon;
       if (nefc > S::MAXEFC) {  // keep the longest prefix of contacts that fits
         const int room = S::MAXEFC - neq - nlim;
-        const unsigned long long fit = __ballot(lane < ncon && con_pre + ncr <= room);
+        const unsigned long long fit = hballot<S::CPW>(lane < ncon && con_pre + ncr <= room);
         keep_con = __popcll(fit);
-        nefc = neq + nlim + (keep_con > 0 ? __shfl(con_pre + ncr, keep_con - 1) : 0);
+        nefc = neq + nlim + (keep_con > 0 ? hshfl<S::CPW>(con_pre + ncr, keep_con - 1) : 0);
         status |= 1;
       }
       // equality rows: joint (side 0) or connect component side - 1
@@ -1943,7 +1995,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
       sync();
       // Jacobian entries of equality/limit rows: (row, dof)
       const int nsimple = neq + nlim;
-      for (int idx = lane; idx < nsimple * NVW; idx += WAVE) {
+      for (int idx = lane; idx < nsimple * NVW; idx += S::HL) {
         const int r = idx >> S::LOG_NVW, i = idx & (NVW - 1);
         const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
         float v = 0.f;
@@ -1978,7 +2030,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
         jstore(s, gx, r, i, v);
       }
       // contact Jacobians: (contact, dof) -> J_n +- mu J_t rows
-      for (int idx = lane; idx < keep_con * NVW; idx += WAVE) {
+      for (int idx = lane; idx < keep_con * NVW; idx += S::HL) {
         const int c = idx >> S::LOG_NVW, i = idx & (NVW - 1);
         const int p = s.con_pair[c];
         const int b1 = m->geom_body[m->pair_g1[p]], b2 = m->geom_body[m->pair_g2[p]];
@@ -2015,7 +2067,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
       }
       sync();
       // row parameters: vel, impedance, D, aref
-      for (int r = lane; r < nefc; r += WAVE) {
+      for (int r = lane; r < nefc; r += S::HL) {
         const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
         float pos, margin, diag;
         const float* sref;
@@ -2096,15 +2148,15 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
           const float gw = lane < nv ? (maw - s.qfs[lane]) * (s.qws[lane] - s.qas[lane]) : 0.f;
           const float gs = lane < nv ? (mas - s.qfs[lane]) * (s.qas[lane] - s.qas[lane]) : 0.f;
           float cw = 0.f, cs = 0.f;
-          for (int r = lane; r < nefc; r += WAVE) {
+          for (int r = lane; r < nefc; r += S::HL) {
             const float jw = jdot(s, gx, r, s.qws) - s.efc_aref[r];
             const float js = jdot(s, gx, r, s.qas) - s.efc_aref[r];
             const bool eq = (s.efc_src[r] >> 24) == 1;
             if (eq || jw < 0.f) cw += s.efc_D[r] * jw * jw;
             if (eq || js < 0.f) cs += s.efc_D[r] * js * js;
           }
-          const float costw = 0.5f * wsum(gw) + 0.5f * wsum(cw);
-          const float costs = 0.5f * wsum(gs) + 0.5f * wsum(cs);
+          const float costw = 0.5f * hsum<S::CPW>(gw) + 0.5f * hsum<S::CPW>(cw);
+          const float costs = 0.5f * hsum<S::CPW>(gs) + 0.5f * hsum<S::CPW>(cs);
           if (costw < costs && lane < NVW) qacc_l = s.qws[lane];
         }
         if (lane < NVW) s.qacc[lane] = qacc_l;
@@ -2122,7 +2174,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
           // Ma, jar, cost at the current qacc; per-row force and active D
           const float ma = lane < nv ? dotN<NVW>(s.M[lane], s.qacc) : 0.f;
           float cc = 0.f;
-          for (int r = lane; r < nefc; r += WAVE) {
+          for (int r = lane; r < nefc; r += S::HL) {
             const float jar = jdot(s, gx, r, s.qacc) - s.efc_aref[r];
             const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
             const float D = s.efc_D[r];
@@ -2131,19 +2183,19 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
             s.efc_Da[r] = act ? D : 0.f;
             cc += act ? D * jar * jar : 0.f;
           }
-          const float gauss = wsum(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
-          const float cost = 0.5f * gauss + 0.5f * wsum(cc);
+          const float gauss = hsum<S::CPW>(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
+          const float cost = 0.5f * gauss + 0.5f * hsum<S::CPW>(cc);
           sync();
           // grad = Ma - qfrc_smooth - J^T f: lane (dof i, row group q); RPW
           // lanes share a dof (4 at NVW 16, 2 at NVW 32)
-          constexpr int RPW = WAVE / NVW;
+          constexpr int RPW = S::HL / NVW;
           const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
           float qc = 0.f;
           jrows(s, gx, gq, RPW, nefc, [&](const float* J, int r) { qc = fmaf(J[gi], s.efc_f[r], qc); });
 #pragma unroll
-          for (int o = NVW; o < WAVE; o <<= 1) qc += __shfl_xor(qc, o);
+          for (int o = NVW; o < S::HL; o <<= 1) qc += __shfl_xor(qc, o);
           const float grad = lane < nv ? ma - s.qfs[lane] - qc : 0.f;
-          const float gn = sqrtf(wsum(grad * grad));
+          const float gn = sqrtf(hsum<S::CPW>(grad * grad));
           // MuJoCo's stop test, plus its fp32 floor: an improvement within ~8 ulp
           // of the cost is rounding noise (without it fp32 iterates on noise
           // where the fp64 solve has converged: 3.9 vs 1.9 iterations per
@@ -2197,13 +2249,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
           sync();
           // Mv, jv, quadratic coefficients
           const float mvv = lane < nv ? dotN<NVW>(s.M[lane], s.srch) : 0.f;
-          for (int r = lane; r < nefc; r += WAVE) s.efc_jv[r] = jdot(s, gx, r, s.srch);
-          const float sn = sqrtf(wsum(search * search));
+          for (int r = lane; r < nefc; r += S::HL) s.efc_jv[r] = jdot(s, gx, r, s.srch);
+          const float sn = sqrtf(hsum<S::CPW>(search * search));
           const float gtol = m->tolerance * m->ls_tolerance * sn * m->meaninertia * (float)(nv > 1 ? nv : 1);
           float qg[3];
           qg[0] = 0.5f * gauss;
-          qg[1] = wsum(lane < nv ? search * (ma - s.qfs[lane]) : 0.f);
-          qg[2] = 0.5f * wsum(search * mvv);
+          qg[1] = hsum<S::CPW>(lane < nv ? search * (ma - s.qfs[lane]) : 0.f);
+          qg[2] = 0.5f * hsum<S::CPW>(search * mvv);
           sync();
           LsPt p0 = ls_eval(s, lane, qg, 0.f);
           LsPt lo = ls_eval(s, lane, qg, p0.alpha - p0.d0 / p0.d1);
@@ -2255,18 +2307,18 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
       if (m->integrator == 3) {
         implicit = true;
         const int nefc = s.nefc;
-        for (int r = lane; r < nefc; r += WAVE) {
+        for (int r = lane; r < nefc; r += S::HL) {
           const float jar = jdot(s, gx, r, s.qacc) - s.efc_aref[r];
           const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
           s.efc_f[r] = act ? -s.efc_D[r] * jar : 0.f;
         }
         sync();
-        constexpr int RPW = WAVE / NVW;
+        constexpr int RPW = S::HL / NVW;
         const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
         float qc = 0.f;
         jrows(s, gx, gq, RPW, nefc, [&](const float* J, int r) { qc = fmaf(J[gi], s.efc_f[r], qc); });
 #pragma unroll
-        for (int o = NVW; o < WAVE; o <<= 1) qc += __shfl_xor(qc, o);
+        for (int o = NVW; o < S::HL; o <<= 1) qc += __shfl_xor(qc, o);
         const float dt = m->timestep;
         float Lm[NVW];
 #pragma unroll
@@ -2308,13 +2360,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
         }
       }
       sync();
-      if (lane < nc && args.theta) args.theta[(size_t)b * nc * H + lane * H + t] = s.qpos[m->ctrl_qposadr[lane]];
+      if (lane < nc && args.theta && live) args.theta[(size_t)b * nc * H + lane * H + t] = s.qpos[m->ctrl_qposadr[lane]];
     }
   }
 
   STAMP(10);
   PROF_FLUSH
-  if (args.plant) {  // single-environment plant: qacc of the last step, state back
+  if (args.plant && live) {  // single-environment plant: qacc of the last step, state back
     if (lane < nv) args.state[ST_QACC + lane] = s.qacc[lane];
     if (args.plant & 2) {
       if (lane < m->nq) args.state[ST_QPOS + lane] = s.qpos[lane];
@@ -2325,12 +2377,12 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES) MPCR
     }
   }
   // ---- final reductions, outputs ----------------------------------------------
-  cost_c = wsum(cost_c);
+  cost_c = hsum<S::CPW>(cost_c);
   bool finite = true;
   if (lane < m->nq) finite = isfinite(s.qpos[lane]);
-  finite = __all(finite);
+  finite = hballot<S::CPW>(!finite) == 0;
   if (!finite) status |= 2;
-  if (lane == 0) {
+  if (lane == 0 && live) {
     const float cost = s.par[PAR_W] * cost_g + s.par[PAR_W + 1] * cost_r + s.par[PAR_W + 2] * cost_c;
     args.cost4[4 * (size_t)b + 0] = cost;
     args.cost4[4 * (size_t)b + 1] = cost_g;
@@ -2354,7 +2406,8 @@ void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigne
   if (wide)
     hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), 0, st, a, dm);
   else
-    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3(grid), dim3(WAVE), dyn_lds, st, a, dm);
+    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3((grid + SmemN::CPW - 1) / SmemN::CPW), dim3(WAVE),
+                       dyn_lds, st, a, dm);
 }
 
 hipError_t rollout_occupancy(int* info, size_t dyn_lds) {
