@@ -171,6 +171,9 @@ using SmemW = SmemT<32, 32, 72, DX_MAXEFC, 36, true, MPCR_W_JL>;
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 static_assert(SmemW::JL * SmemW::LDJ >= SmemW::CVXN, "convex-pair list inside the J rows");
+#if !defined(MPCR_N_LDS_UNCHECKED)
+static_assert(sizeof(SmemW) <= 152448 / 7, "dual-arm LDS image must fit 7 blocks per CU");
+#endif
 
 
 // launchers (defined in rollout.hip): the rollout kernel variant for the

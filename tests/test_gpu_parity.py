@@ -280,3 +280,17 @@ def test_dual_arm_c4_properties(torch_cuda):
     assert int((s_ & 1).sum()) == 0
     rows_per_step = (s_ >> 8) / H
     assert rows_per_step.min() >= 8  # 8 equality rows + the linkage contacts
+
+
+def test_kernel_occupancy_budget(torch_cuda):
+    """The LDS images and register budgets the performance rests on (DESIGN.md
+    §LDS capacity): 16 narrow blocks per CU (<= 9520 B each, 4 waves/SIMD),
+    the dual-arm image at <= 21778 B with a 2-waves/SIMD register budget."""
+    import ctypes
+
+    from manipulator_mujoco_amd import _lib
+    info = (ctypes.c_int * 6)()
+    _lib.check(_lib.load().mpcr_rollout_occupancy(0, info))
+    nb, nlds, nreg, wb, wlds, wreg = list(info)
+    assert nlds <= 9520 and nreg <= 128 and nb >= 16, list(info)
+    assert wlds <= 152448 // 7 and wreg <= 256 and wb >= 7, list(info)
