@@ -215,26 +215,37 @@ class cem_planner:  # noqa: N801 (reference name)
             torch.cuda.current_stream(self.device).wait_stream(s)
             torch.cuda.synchronize(self.device)
             graphs = []
-            if not self.exchange:  # the whole tick in one graph
+            if not self.exchange or self._exchange_capturable():
+                # the whole tick in one graph; with an RCCL group the elite
+                # all-gathers are captured too (device buffers, stream-ordered)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     for it in range(it_n):
                         self._seg_sample_rollout(it)
-                        self._seg_local_update(it)
+                        if not self.exchange:
+                            self._seg_local_update(it)
+                        else:
+                            self._exchange_update(it)
                 graphs.append(g)
-            else:  # device segments in graphs, the RCCL exchange between them eager
+            else:  # gloo (host-staged) exchange: device segments in graphs, the exchange between them eager
                 for it in range(it_n):
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g):
                         self._seg_sample_rollout(it)
                     graphs.append(g)
             self._graphs = graphs
-        if not self.exchange:
+        if len(self._graphs) == 1:
             self._graphs[0].replay()
         else:
             for it in range(it_n):
                 self._graphs[it].replay()
                 self._exchange_update(it)
+
+    def _exchange_capturable(self):
+        """RCCL collectives on device tensors can be captured into the tick's
+        graph; host-staged (gloo) ones cannot."""
+        import torch.distributed as dist
+        return dist.get_backend(self.group) == "nccl"
 
     def _run_eager_once(self):
         graph, self.graph = self.graph, False

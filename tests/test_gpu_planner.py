@@ -90,7 +90,8 @@ def _port():
 @pytest.mark.parametrize("graph", [False, True])
 def test_exchange_path_equals_single_gpu(torch_cuda, graph):
     """The sharded update (local top-E -> RCCL all-gather -> global top-E ->
-    replicated update) forced on a one-rank group equals the local update."""
+    replicated update) forced on a one-rank group equals the local update;
+    with graph=True the RCCL all-gathers are captured in the tick's graph."""
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch_cuda.device("cuda", 0))
@@ -100,6 +101,8 @@ def test_exchange_path_equals_single_gpu(torch_cuda, graph):
         sharded.exchange = True
         for args in _ticks():
             _same(single.compute_cem(*args), sharded.compute_cem(*args))
+        if graph:
+            assert len(sharded._graphs) == 1  # exchange inside the captured tick
     finally:
         dist.destroy_process_group()
 
