@@ -1051,26 +1051,26 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
     sync();
     return;
   }
-  // ---- face contact: reference box owns the face axis.  All indices below
-  // are uniform but run-time; select explicitly so nothing lives in scratch.
+  // ---- face contact: reference box owns the face axis.  The run-time axis
+  // indices address the boxes' LDS frames and model sizes directly (no
+  // select chains, nothing in scratch); same values as the registers above.
   const bool refA = face_id < 3;
   const int fi = refA ? face_id : face_id - 3;
-  float cr[3], ci[3], nf[3], R0[3], R1[3], R2[3], I0[3], I1[3], I2[3];
+  const int gr = refA ? g1 : g2, gn = refA ? g2 : g1;
+  const float* Rr = s.gxmat[gr];  // axis k of a box: (R[k], R[3 + k], R[6 + k])
+  const float* Ri = s.gxmat[gn];
+  const float* hr = m->geom_size[gr];
+  const float* hi = m->geom_size[gn];
+  float cr[3], ci[3], nf[3];
 #pragma unroll
   for (int c = 0; c < 3; c++) {
-    cr[c] = refA ? x1[c] : x2[c];
-    ci[c] = refA ? x2[c] : x1[c];
+    cr[c] = s.gxpos[gr][c];
+    ci[c] = s.gxpos[gn][c];
     nf[c] = refA ? n[c] : -n[c];
-    R0[c] = refA ? axA[0][c] : axB[0][c];
-    R1[c] = refA ? axA[1][c] : axB[1][c];
-    R2[c] = refA ? axA[2][c] : axB[2][c];
-    I0[c] = refA ? axB[0][c] : axA[0][c];
-    I1[c] = refA ? axB[1][c] : axA[1][c];
-    I2[c] = refA ? axB[2][c] : axA[2][c];
   }
-  const float hr0 = refA ? ha[0] : hb[0], hr1 = refA ? ha[1] : hb[1], hr2 = refA ? ha[2] : hb[2];
-  const float hi0 = refA ? hb[0] : ha[0], hi1 = refA ? hb[1] : ha[1], hi2 = refA ? hb[2] : ha[2];
-  const float d0 = fabsf(dot3(I0, nf)), d1 = fabsf(dot3(I1, nf)), d2 = fabsf(dot3(I2, nf));
+  const float d0 = fabsf(Ri[0] * nf[0] + Ri[3] * nf[1] + Ri[6] * nf[2]);
+  const float d1 = fabsf(Ri[1] * nf[0] + Ri[4] * nf[1] + Ri[7] * nf[2]);
+  const float d2 = fabsf(Ri[2] * nf[0] + Ri[5] * nf[1] + Ri[8] * nf[2]);
   int ki = 0;
   float bestdot = d0;
   if (d1 > bestdot) { bestdot = d1; ki = 1; }
@@ -1079,13 +1079,11 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
   float Ik[3], Iu[3], Iv[3];
 #pragma unroll
   for (int c = 0; c < 3; c++) {
-    Ik[c] = ki == 0 ? I0[c] : (ki == 1 ? I1[c] : I2[c]);
-    Iu[c] = u == 0 ? I0[c] : (u == 1 ? I1[c] : I2[c]);
-    Iv[c] = v == 0 ? I0[c] : (v == 1 ? I1[c] : I2[c]);
+    Ik[c] = Ri[3 * c + ki];
+    Iu[c] = Ri[3 * c + u];
+    Iv[c] = Ri[3 * c + v];
   }
-  const float hk = ki == 0 ? hi0 : (ki == 1 ? hi1 : hi2);
-  const float hu = u == 0 ? hi0 : (u == 1 ? hi1 : hi2);
-  const float hv = v == 0 ? hi0 : (v == 1 ? hi1 : hi2);
+  const float hk = hi[ki], hu = hi[u], hv = hi[v];
   const float si = dot3(Ik, nf) > 0.f ? -1.f : 1.f;
   if (lane < 4) {
     const float su = (lane == 0 || lane == 3) ? 1.f : -1.f, sv = lane < 2 ? 1.f : -1.f;
@@ -1097,10 +1095,8 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
     sync();
     const int ax = (fi + 1 + (pl >> 1)) % 3;
     const float sgn = (pl & 1) ? -1.f : 1.f;
-    float Ra[3];
-#pragma unroll
-    for (int c = 0; c < 3; c++) Ra[c] = ax == 0 ? R0[c] : (ax == 1 ? R1[c] : R2[c]);
-    const float hax = ax == 0 ? hr0 : (ax == 1 ? hr1 : hr2);
+    const float Ra[3] = {Rr[ax], Rr[3 + ax], Rr[6 + ax]};
+    const float hax = hr[ax];
     const float cra = dot3(cr, Ra);
     float P[3] = {0.f, 0.f, 0.f}, Q[3] = {0.f, 0.f, 0.f}, dp = 0.f, dq = 0.f;
     int e0 = 0, e1 = 0;
@@ -1129,7 +1125,7 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
   }
   sync();
   if (np == 0) return;
-  const float hrf = fi == 0 ? hr0 : (fi == 1 ? hr1 : hr2);
+  const float hrf = hr[fi];
   float depth = -3e38f;
   bool keep = false;
   if (lane < np) {
@@ -2140,13 +2136,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       if (nefc > 0) {
         // warm start: the better of qacc_warmstart and qacc_smooth
         if (!(m->disableflags & 4)) {
-          float maw = 0.f, mas = 0.f;
-          if (lane < nv) {
-            maw = dotN<NVW>(s.M[lane], s.qws);
-            mas = dotN<NVW>(s.M[lane], s.qas);
-          }
+          // (the Gauss term of qacc_smooth itself is (M a_s - f_s)'(a_s - a_s) = 0)
+          const float maw = lane < nv ? dotN<NVW>(s.M[lane], s.qws) : 0.f;
           const float gw = lane < nv ? (maw - s.qfs[lane]) * (s.qws[lane] - s.qas[lane]) : 0.f;
-          const float gs = lane < nv ? (mas - s.qfs[lane]) * (s.qas[lane] - s.qas[lane]) : 0.f;
           float cw = 0.f, cs = 0.f;
           for (int r = lane; r < nefc; r += S::HL) {
             const float jw = jdot(s, gx, r, s.qws) - s.efc_aref[r];
@@ -2156,7 +2148,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             if (eq || js < 0.f) cs += s.efc_D[r] * js * js;
           }
           const float costw = 0.5f * hsum<S::CPW>(gw) + 0.5f * hsum<S::CPW>(cw);
-          const float costs = 0.5f * hsum<S::CPW>(gs) + 0.5f * hsum<S::CPW>(cs);
+          const float costs = 0.5f * hsum<S::CPW>(cs);
           if (costw < costs && lane < NVW) qacc_l = s.qws[lane];
         }
         if (lane < NVW) s.qacc[lane] = qacc_l;
