@@ -723,29 +723,50 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
     }
     return 2;
   }
-  if (func == 1) {  // plane - box: 4 deepest corners
-    float n[3] = {R1[2], R1[5], R1[8]};
-    float cd[8];
+  if (func == 1) {  // plane - box: the 4 deepest corners, ascending depth (ties: corner index)
+    // depth(c) = n.(x2 - x1) + sum_k +-w_k with w_k = h_k n.R2_k: the deepest
+    // corner takes the sign against each w_k, the next ones flip the axis of
+    // the smallest |w|, of the second smallest, and then the third axis or
+    // both of the first two -- 5 candidates instead of a 4 x 8 scan
+    const float n[3] = {R1[2], R1[5], R1[8]};
+    float w[3];
 #pragma unroll
-    for (int c = 0; c < 8; c++) {
-      float l[3] = {(c & 1) ? s2[0] : -s2[0], (c & 2) ? s2[1] : -s2[1], (c & 4) ? s2[2] : -s2[2]}, w[3];
-      mv(w, R2, l);
-      cd[c] = n[0] * (x2[0] + w[0] - x1[0]) + n[1] * (x2[1] + w[1] - x1[1]) + n[2] * (x2[2] + w[2] - x1[2]);
+    for (int k = 0; k < 3; k++) w[k] = s2[k] * (n[0] * R2[k] + n[1] * R2[3 + k] + n[2] * R2[6 + k]);
+    const int c0 = (w[0] < 0.f ? 1 : 0) | (w[1] < 0.f ? 2 : 0) | (w[2] < 0.f ? 4 : 0);
+    int ax0 = 0, ax1 = 1, ax2 = 2;  // axes by |w| ascending, index order on ties
+    if (fabsf(w[ax1]) < fabsf(w[ax0])) { const int t = ax0; ax0 = ax1; ax1 = t; }
+    if (fabsf(w[ax2]) < fabsf(w[ax1])) { const int t = ax1; ax1 = ax2; ax2 = t; }
+    if (fabsf(w[ax1]) < fabsf(w[ax0])) { const int t = ax0; ax0 = ax1; ax1 = t; }
+    auto depth = [&](int c) {  // the same expression as the oracle's corner distance
+      const float l[3] = {(c & 1) ? s2[0] : -s2[0], (c & 2) ? s2[1] : -s2[1], (c & 4) ? s2[2] : -s2[2]};
+      float v[3];
+      mv(v, R2, l);
+      return n[0] * (x2[0] + v[0] - x1[0]) + n[1] * (x2[1] + v[1] - x1[1]) + n[2] * (x2[2] + v[2] - x1[2]);
+    };
+    int cs[4] = {c0, c0 ^ (1 << ax0), c0 ^ (1 << ax1), c0 ^ (1 << ax2)};
+    float ds[4] = {depth(cs[0]), depth(cs[1]), depth(cs[2]), depth(cs[3])};
+    {
+      const int c4 = c0 ^ (1 << ax0) ^ (1 << ax1);
+      const float d4 = depth(c4);
+      if (d4 < ds[3] || (d4 == ds[3] && c4 < cs[3])) { cs[3] = c4; ds[3] = d4; }
     }
-    int used = 0;
+    // order the four by (depth, index): sorting network (0,1) (2,3) (0,2) (1,3) (1,2)
+    auto cx = [&](int i, int j) {
+      if (ds[j] < ds[i] || (ds[j] == ds[i] && cs[j] < cs[i])) {
+        const float td = ds[i]; ds[i] = ds[j]; ds[j] = td;
+        const int tc = cs[i]; cs[i] = cs[j]; cs[j] = tc;
+      }
+    };
+    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      int best = -1;
-      float bd = 0;
+      const int c = cs[k];
+      const float l[3] = {(c & 1) ? s2[0] : -s2[0], (c & 2) ? s2[1] : -s2[1], (c & 4) ? s2[2] : -s2[2]};
+      float v[3];
+      mv(v, R2, l);
+      dist[k] = ds[k];
 #pragma unroll
-      for (int c = 0; c < 8; c++)
-        if (!((used >> c) & 1) && (best < 0 || cd[c] < bd)) { best = c; bd = cd[c]; }
-      used |= 1 << best;
-      float l[3] = {(best & 1) ? s2[0] : -s2[0], (best & 2) ? s2[1] : -s2[1], (best & 4) ? s2[2] : -s2[2]}, w[3];
-      mv(w, R2, l);
-      dist[k] = bd;
-#pragma unroll
-      for (int c = 0; c < 3; c++) { pos[k][c] = x2[c] + w[c] - n[c] * 0.5f * bd; nrm[k][c] = n[c]; }
+      for (int e = 0; e < 3; e++) { pos[k][e] = x2[e] + v[e] - n[e] * 0.5f * ds[k]; nrm[k][e] = n[e]; }
     }
     return 4;
   }
@@ -958,22 +979,20 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
   // ---- separating axes, one per lane
   float L[3] = {0.f, 0.f, 1.f}, sep = -3e38f;
   bool valid = false;
+  // (per-lane axes read from the LDS frames by index: no select chains)
   if (lane < 6) {
+    const float* R = s.gxmat[lane < 3 ? g1 : g2];
     const int ia = lane < 3 ? lane : lane - 3;
 #pragma unroll
-    for (int c = 0; c < 3; c++) {
-      const float va = ia == 0 ? axA[0][c] : (ia == 1 ? axA[1][c] : axA[2][c]);
-      const float vb = ia == 0 ? axB[0][c] : (ia == 1 ? axB[1][c] : axB[2][c]);
-      L[c] = lane < 3 ? va : vb;
-    }
+    for (int c = 0; c < 3; c++) L[c] = R[3 * c + ia];
     valid = true;
   } else if (lane < 15) {
     const int i = (lane - 6) / 3, j = (lane - 6) % 3;
     float ai[3], bj[3];
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-      ai[c] = i == 0 ? axA[0][c] : (i == 1 ? axA[1][c] : axA[2][c]);
-      bj[c] = j == 0 ? axB[0][c] : (j == 1 ? axB[1][c] : axB[2][c]);
+      ai[c] = s.gxmat[g1][3 * c + i];
+      bj[c] = s.gxmat[g2][3 * c + j];
     }
     cross(L, ai, bj);
     const float l = sqrtf(dot3(L, L));
@@ -1025,12 +1044,10 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
         for (int c = 0; c < 3; c++) pb[c] += s_ * hb[k] * axB[k][c];
       }
     }
-    const float hae = ei == 0 ? ha[0] : (ei == 1 ? ha[1] : ha[2]);
-    const float hbe = ej == 0 ? hb[0] : (ej == 1 ? hb[1] : hb[2]);
+    const float hae = m->geom_size[g1][ei], hbe = m->geom_size[g2][ej];
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-      const float ae = ei == 0 ? axA[0][c] : (ei == 1 ? axA[1][c] : axA[2][c]);
-      const float be = ej == 0 ? axB[0][c] : (ej == 1 ? axB[1][c] : axB[2][c]);
+      const float ae = s.gxmat[g1][3 * c + ei], be = s.gxmat[g2][3 * c + ej];
       pa[c] -= hae * ae; da[c] = 2.f * hae * ae;
       pb[c] -= hbe * be; db[c] = 2.f * hbe * be;
     }
