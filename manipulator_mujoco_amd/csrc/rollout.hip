@@ -304,12 +304,16 @@ template <int K>
 struct Chol16Upd<K, 16> {
   static __device__ __forceinline__ void run(float (&)[16], float) {}
 };
+// The factor is kept with a ZERO diagonal: l[i][i] lives only as its inverse
+// in dinv (lane i).  The sweeps then leave lane K's accumulator alone when
+// they broadcast its value, and read every result off at the end (acc * dinv)
+// instead of capturing it with a per-step select.
 template <int K>
 struct Chol16 {  // column K; dinv collects 1 / l[i][i] at lane i
   static __device__ __forceinline__ void run(float (&a)[16], float& dinv, int lane) {
     const float dkk = sqrtf(fmaxf(rbc<K>(a[K]), kMinVal));
     const float inv = 1.f / dkk;
-    const float lik = lane == K ? dkk : (lane > K ? a[K] * inv : 0.f);
+    const float lik = lane > K ? a[K] * inv : 0.f;
     a[K] = lik;
     dinv = lane == K ? inv : dinv;
     Chol16Upd<K, K + 1>::run(a, lik);
@@ -320,25 +324,25 @@ template <>
 struct Chol16<16> {
   static __device__ __forceinline__ void run(float (&)[16], float&, int) {}
 };
-// forward (L y = b) / backward (L^T x = y) sweeps: lane K finalises its value
-// t = acc / l_KK, one fused DPP FMA hands it to the other lanes' updates
-// (lanes already final see a zero coefficient: l is lower triangular)
+// forward (L y = b) / backward (L^T x = y) sweeps: lane K's value is final
+// at step K, t = acc / l_KK, and one fused DPP FMA hands it to the other
+// lanes' updates (lanes already final and lane K see zero coefficients: l is
+// triangular with a zero diagonal); the results are acc * dinv afterwards
 template <int K, int STEP>
 struct Sweep16 {
-  static __device__ __forceinline__ void run(const float (&c)[16], float& acc, float& out, float dinv, int lane) {
+  static __device__ __forceinline__ void run(const float (&c)[16], float& acc, float dinv) {
     const float t = acc * dinv;
     fnmac_bc<K, true>(acc, t, c[K]);
-    out = lane == K ? t : out;
-    Sweep16<K + STEP, STEP>::run(c, acc, out, dinv, lane);
+    Sweep16<K + STEP, STEP>::run(c, acc, dinv);
   }
 };
 template <int STEP>
 struct Sweep16<16, STEP> {
-  static __device__ __forceinline__ void run(const float (&)[16], float&, float&, float, int) {}
+  static __device__ __forceinline__ void run(const float (&)[16], float&, float) {}
 };
 template <int STEP>
 struct Sweep16<-1, STEP> {
-  static __device__ __forceinline__ void run(const float (&)[16], float&, float&, float, int) {}
+  static __device__ __forceinline__ void run(const float (&)[16], float&, float) {}
 };
 // MPCR_CHOL_LANE_LAUNDER: re-derive the lane compares inside the solves (one
 // v_cmp each) instead of letting them be hoisted into spilled SGPR pairs
@@ -358,8 +362,9 @@ __device__ __forceinline__ float chol16_solve(const float (&l)[16], float dinv, 
 #pragma unroll
     for (int j = 0; j < 16; j++) Lt[j * LDL + lane] = l[j];
   }
-  float acc = b, y = 0.f;
-  Sweep16<0, 1>::run(l, acc, y, dinv, lane);
+  float acc = b;
+  Sweep16<0, 1>::run(l, acc, dinv);
+  const float y = acc * dinv;
   sync();
   float lt[16];
   {
@@ -370,9 +375,9 @@ __device__ __forceinline__ float chol16_solve(const float (&l)[16], float dinv, 
       lt[4 * q] = v.x; lt[4 * q + 1] = v.y; lt[4 * q + 2] = v.z; lt[4 * q + 3] = v.w;
     }
   }
-  float x = 0.f;
   acc = y;
-  Sweep16<15, -1>::run(lt, acc, x, dinv, lane);
+  Sweep16<15, -1>::run(lt, acc, dinv);
+  const float x = acc * dinv;
   sync();
   return x;
 }
