@@ -1714,7 +1714,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         float ax[3], anchor[3];
         if (kind == 3) {
           const int k = m->dof_sub[lane];
-          ax[0] = R[k]; ax[1] = R[3 + k]; ax[2] = R[6 + k];
+          ax[0] = s.xmat[bd][k]; ax[1] = s.xmat[bd][3 + k]; ax[2] = s.xmat[bd][6 + k];  // by index, no selects
           anchor[0] = s.xpos[bd][0]; anchor[1] = s.xpos[bd][1]; anchor[2] = s.xpos[bd][2];
         } else {
           const int j = m->dof_jnt[lane];
