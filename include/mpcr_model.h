@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 #define MPCR_MODEL_MAGIC   0x4d504352u /* 'MPCR' */
-#define MPCR_MODEL_VERSION 4
+#define MPCR_MODEL_VERSION 5
 
 #define MPCR_MAX_BODY   48
 #define MPCR_MAX_JNT    40
@@ -38,6 +38,7 @@ extern "C" {
 #define MPCR_MAX_ACT    16   /* actuators */
 #define MPCR_MAX_HULLV  8192 /* convex-hull vertices of all collision meshes */
 #define MPCR_MAX_HULLA  49152 /* hull-graph adjacency entries */
+#define MPCR_MAX_TEN    4    /* spatial (site-site) tendons with limits */
 
 /* joint types (MuJoCo mjtJoint) */
 enum { MPCR_JNT_FREE = 0, MPCR_JNT_BALL = 1, MPCR_JNT_SLIDE = 2, MPCR_JNT_HINGE = 3 };
@@ -65,6 +66,8 @@ enum {
 };
 /* equality types (mjtEq) */
 enum { MPCR_EQ_CONNECT = 0, MPCR_EQ_JOINT = 2 };
+/* friction cones (mjtCone) */
+enum { MPCR_CONE_PYRAMIDAL = 0, MPCR_CONE_ELLIPTIC = 1 };
 /* integrators (mjtIntegrator) */
 enum { MPCR_INT_EULER = 0, MPCR_INT_IMPLICITFAST = 3 };
 /* actuator gain / bias types (mjtGain / mjtBias) */
@@ -94,7 +97,7 @@ typedef struct mpcr_model_t {
   int32_t hande_body;  /* body whose xquat is the eef rotation (-1: none)    */
   int32_t tcp_site;    /* site whose xpos is the eef position  (-1: none)    */
   int32_t iterations, ls_iterations, disableflags;
-  int32_t integrator, cone;  /* MPCR_INT_*, 0 = pyramidal (only one built)   */
+  int32_t integrator, cone;  /* MPCR_INT_*, MPCR_CONE_*                       */
   int32_t ntree;       /* kinematic trees (roots with dofs)                  */
   int32_t nu;          /* actuators                                          */
   int32_t nhullv, nhulla; /* convex-hull vertices / adjacency entries       */
@@ -231,6 +234,21 @@ typedef struct mpcr_model_t {
   int32_t hull_adjnum[MPCR_MAX_HULLV];
   int32_t hull_adj[MPCR_MAX_HULLA];     /* global vertex indices            */
   double hull_vert[MPCR_MAX_HULLV][3];
+
+  /* v5 (scene_robotiq_hande.xml) */
+  /* fluid: mjOption viscosity / density, MuJoCo's inertia-box model per body
+     (force -3 pi d eta v, torque -pi d^3 eta w at xipos, d = mean box side) */
+  double viscosity, density;
+  /* spatial tendons through two sites (no wrapping): length |x_s2 - x_s1|,
+     length limits as constraint rows after the joint limits (mj_instantiateLimit) */
+  int32_t nten, pad5;
+  int32_t ten_site[MPCR_MAX_TEN][2];
+  int32_t ten_limited[MPCR_MAX_TEN];
+  double ten_range[MPCR_MAX_TEN][2];
+  double ten_solref[MPCR_MAX_TEN][2];
+  double ten_solimp[MPCR_MAX_TEN][5];
+  double ten_margin[MPCR_MAX_TEN];
+  double ten_invweight0[MPCR_MAX_TEN]; /* J_ten M^-1 J_ten^T at qpos0 */
 } mpcr_model_t;
 
 #ifdef __cplusplus

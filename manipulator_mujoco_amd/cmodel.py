@@ -11,18 +11,20 @@ import ctypes
 import numpy as np
 
 MAGIC = 0x4D504352
-VERSION = 4
+VERSION = 5
 
 MAX_BODY, MAX_JNT, MAX_DOF, MAX_NQ = 48, 40, 32, 48
 MAX_GEOM, MAX_SITE, MAX_PAIR, MAX_EQ = 128, 24, 768, 8
 MAX_SLOT, MAX_CTRL, MAX_ACT = 512, 8, 16
 MAX_HULLV, MAX_HULLA = 8192, 49152
+MAX_TEN = 4
 
 COL_PLANE_CAPSULE, COL_PLANE_BOX, COL_CAPSULE_CAPSULE, COL_CAPSULE_BOX, COL_BOX_BOX = 0, 1, 2, 3, 4
 COL_PLANE_SPHERE, COL_SPHERE_SPHERE, COL_SPHERE_CAPSULE, COL_SPHERE_BOX = 5, 6, 7, 8
 COL_CONVEX, COL_PLANE_CONVEX = 9, 10
 EQ_CONNECT, EQ_JOINT = 0, 2
 INT_EULER, INT_IMPLICITFAST = 0, 3
+CONE_PYRAMIDAL, CONE_ELLIPTIC = 0, 1
 GAIN_FIXED, GAIN_AFFINE = 0, 1
 BIAS_NONE, BIAS_AFFINE = 0, 1
 
@@ -96,12 +98,17 @@ class mpcr_model_t(ctypes.Structure):
         ("geom_hulladr", _a(_i, MAX_GEOM)), ("geom_hullnum", _a(_i, MAX_GEOM)),
         ("hull_adjadr", _a(_i, MAX_HULLV)), ("hull_adjnum", _a(_i, MAX_HULLV)),
         ("hull_adj", _a(_i, MAX_HULLA)), ("hull_vert", _a(_d, MAX_HULLV, 3)),
+        ("viscosity", _d), ("density", _d), ("nten", _i), ("pad5", _i),
+        ("ten_site", _a(_i, MAX_TEN, 2)), ("ten_limited", _a(_i, MAX_TEN)),
+        ("ten_range", _a(_d, MAX_TEN, 2)), ("ten_solref", _a(_d, MAX_TEN, 2)),
+        ("ten_solimp", _a(_d, MAX_TEN, 5)), ("ten_margin", _a(_d, MAX_TEN)),
+        ("ten_invweight0", _a(_d, MAX_TEN)),
     ]
 
 
 _LIMITS = dict(nbody=MAX_BODY, njnt=MAX_JNT, nv=MAX_DOF, nq=MAX_NQ, ngeom=MAX_GEOM,
                nsite=MAX_SITE, npair=MAX_PAIR, neq=MAX_EQ, nslot=MAX_SLOT, nctrl=MAX_CTRL, nu=MAX_ACT,
-               nhullv=MAX_HULLV, nhulla=MAX_HULLA)
+               nhullv=MAX_HULLV, nhulla=MAX_HULLA, nten=MAX_TEN)
 
 # struct field -> Model attribute (when the names differ)
 _ALIASES = {}
@@ -132,17 +139,18 @@ def pack(m) -> mpcr_model_t:
     scalars = ("nbody", "njnt", "nq", "nv", "ngeom", "nsite", "npair", "neq", "ncon", "nslot",
                "nctrl", "hande_body", "tcp_site", "iterations", "ls_iterations", "disableflags",
                "ntree", "timestep", "tolerance", "ls_tolerance", "impratio", "meaninertia")
-    for k in ("nu", "nhullv", "nhulla", "integrator"):
+    for k in ("nu", "nhullv", "nhulla", "integrator", "cone", "nten"):
         setattr(s, k, int(getattr(m, k, 0)))
+    for k in ("viscosity", "density"):
+        setattr(s, k, float(getattr(m, k, 0.0)))
     for k in scalars:
         setattr(s, k, getattr(m, k))
-    s.cone = 0
     for k in range(3):
         s.gravity[k] = float(m.gravity[k])
     for name, _ in mpcr_model_t._fields_:
         if name in scalars or name.startswith("pad") or name in ("magic", "version", "nbytes", "gravity",
                                                                  "integrator", "cone", "nu", "nhullv",
-                                                                 "nhulla"):
+                                                                 "nhulla", "nten", "viscosity", "density"):
             continue
         attr = _ALIASES.get(name, name)
         if hasattr(m, attr):

@@ -131,8 +131,11 @@ static int check_model(const mpcr_model_t& m) {
       m.nu > MPCR_MAX_ACT || m.nhullv > MPCR_MAX_HULLV || m.nhulla > MPCR_MAX_HULLA || m.nu < 0 || m.nhullv < 0 ||
       m.nhulla < 0)
     return fail(MPCR_EMODEL, "model exceeds blob capacity");
-  if ((m.integrator != MPCR_INT_EULER && m.integrator != MPCR_INT_IMPLICITFAST) || m.cone != 0)
+  if ((m.integrator != MPCR_INT_EULER && m.integrator != MPCR_INT_IMPLICITFAST) || m.cone != MPCR_CONE_PYRAMIDAL)
     return fail(MPCR_EMODEL, "only Euler / implicitfast with pyramidal cones supported");
+  if (m.nten < 0 || m.nten > MPCR_MAX_TEN) return fail(MPCR_EMODEL, "model exceeds blob capacity");
+  if (m.nten != 0 || m.viscosity != 0 || m.density != 0)
+    return fail(MPCR_EMODEL, "spatial tendons and fluid forces are not built on the device yet");
   for (int g = 0; g < m.ngeom; g++)
     if (m.geom_hulladr[g] >= 0 && m.geom_hulladr[g] + m.geom_hullnum[g] > m.nhullv)
       return fail(MPCR_EMODEL, "geom %d hull outside the vertex table", g);

@@ -433,7 +433,7 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
     # options
     opt = dict(timestep=0.002, iterations=100, ls_iterations=50, tolerance=1e-8,
                ls_tolerance=0.01, impratio=1.0, gravity=(0.0, 0.0, -9.81),
-               integrator="Euler", cone="pyramidal", solver="Newton")
+               integrator="Euler", cone="pyramidal", solver="Newton", viscosity=0.0, density=0.0)
     disable = 0
     flag_bits = {"eulerdamp": cmodel.DSBL_EULERDAMP, "refsafe": cmodel.DSBL_REFSAFE,
                  "warmstart": cmodel.DSBL_WARMSTART, "gravity": cmodel.DSBL_GRAVITY,
@@ -441,7 +441,7 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
                  "equality": cmodel.DSBL_EQUALITY, "passive": cmodel.DSBL_PASSIVE,
                  "filterparent": cmodel.DSBL_FILTERPARENT}
     for o in root.iter("option"):
-        for k in ("timestep", "tolerance", "ls_tolerance", "impratio"):
+        for k in ("timestep", "tolerance", "ls_tolerance", "impratio", "viscosity", "density"):
             if k in o.attrib:
                 opt[k] = float(o.get(k))
         for k in ("iterations", "ls_iterations"):
@@ -464,8 +464,9 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
     integrators = {"Euler": cmodel.INT_EULER, "implicitfast": cmodel.INT_IMPLICITFAST}
     if opt["integrator"] not in integrators:
         raise MJCFError(f"integrator {opt['integrator']!r} not supported (Euler, implicitfast)")
-    if opt["cone"] != "pyramidal":
-        raise MJCFError("only pyramidal friction cones are supported")
+    cones = {"pyramidal": cmodel.CONE_PYRAMIDAL, "elliptic": cmodel.CONE_ELLIPTIC}
+    if opt["cone"] not in cones:
+        raise MJCFError(f"cone {opt['cone']!r} not supported (pyramidal, elliptic)")
     if opt["solver"] != "Newton":
         raise MJCFError("only the Newton solver is supported")
 
@@ -950,9 +951,13 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
     m.tolerance = opt["tolerance"]
     m.ls_tolerance = opt["ls_tolerance"]
     m.impratio = opt["impratio"]
+    m.cone = cones[opt["cone"]]
+    m.viscosity = opt["viscosity"]
+    m.density = opt["density"]
     m.gravity = np.array(opt["gravity"])
     m.source = path
 
+    _spatial_tendons(m, root, defaults)
     set_const(m)
     _connect_anchors(m)
     return m
@@ -1082,6 +1087,49 @@ def _actuators(m, root, defaults, jnt, jnames, autolimits):
     for k, w in (("gainprm", 3), ("biasprm", 3), ("ctrlrange", 2), ("forcerange", 2)):
         setattr(m, "act_" + k, np.array([a[k] for a in acts], dtype=np.float64).reshape(nu, w))
     m.act_ctrl = np.zeros(nu)  # MjData.ctrl starts at 0 and the reference never sets it
+
+
+def _spatial_tendons(m, root, defaults):
+    """<tendon><spatial> through exactly two sites (no wrapping geoms, no
+    pulleys), kept for their length limits (scene_robotiq_hande.xml:34-39).
+    Limit solref/solimp/margin default as MuJoCo's tendon defaults."""
+    sites = m.names["site"]
+    ten = []
+    for t in root.findall("tendon"):
+        for sp in t.findall("spatial"):
+            a = defaults.attrs(sp.get("class", "main"), "tendon", sp)
+            kids = list(sp)
+            if len(kids) != 2 or any(k.tag != "site" for k in kids):
+                raise MJCFError("spatial tendons must run through exactly two sites")
+            s1, s2 = (sites.index(k.get("site")) for k in kids)
+            rng = _floats(a.get("range", "0 0"), 2)
+            flag = a.get("limited", "auto")
+            lim = flag == "true" or (flag == "auto" and "range" in a)
+            ten.append(dict(site=(s1, s2), limited=int(lim), range=rng,
+                            solref=(_floats(a.get("solreflimit", "0.02 1")) + [1.0])[:2],
+                            solimp=(_floats(a.get("solimplimit", "0.9 0.95 0.001 0.5 2"))
+                                    + [0.5, 2.0])[:5],
+                            margin=float(a.get("margin", 0.0))))
+    m.nten = len(ten)
+    n = m.nten
+    m.ten_site = np.array([t["site"] for t in ten], dtype=np.int64).reshape(n, 2)
+    m.ten_limited = np.array([t["limited"] for t in ten], dtype=np.int64)
+    m.ten_range = np.array([t["range"] for t in ten], dtype=np.float64).reshape(n, 2)
+    m.ten_solref = np.array([t["solref"] for t in ten], dtype=np.float64).reshape(n, 2)
+    m.ten_solimp = np.array([t["solimp"] for t in ten], dtype=np.float64).reshape(n, 5)
+    m.ten_margin = np.array([t["margin"] for t in ten], dtype=np.float64)
+    m.ten_invweight0 = np.zeros(n)
+
+
+def tendon_jac(m, k, t):
+    """Length and moment row (nv) of spatial tendon t at the kinematics k."""
+    s1, s2 = m.ten_site[t]
+    p = [k["xpos"][m.site_bodyid[s]] + k["xmat"][m.site_bodyid[s]] @ m.site_pos[s] for s in (s1, s2)]
+    dif = p[1] - p[0]
+    L = float(np.linalg.norm(dif))
+    j1, _ = body_jac(m, k, m.site_bodyid[s1], p[0])
+    j2, _ = body_jac(m, k, m.site_bodyid[s2], p[1])
+    return L, (dif / max(L, 1e-15)) @ (j2 - j1)
 
 
 def _connect_anchors(m):
@@ -1243,6 +1291,10 @@ def set_const(m):
         else:
             dw[d0] = Minv[d0, d0]
     m.dof_invweight0 = dw
+    # tendon_invweight0 = J_ten M^-1 J_ten^T (mj_setConst)
+    for t in range(getattr(m, "nten", 0)):
+        _, J = tendon_jac(m, k, t)
+        m.ten_invweight0[t] = float(J @ Minv @ J)
     return m
 
 

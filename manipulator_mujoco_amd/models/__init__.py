@@ -14,6 +14,10 @@ plain numeric arrays:
                       Hand-E and UR5e + Robotiq 2F-85, implicitfast, 14
                       actuators, fixed tendons, connect/joint equalities,
                       convex-hull mesh collision
+* ``hande_scene``     URD/scene_robotiq_hande.xml: free Hand-E
+                      gripper + a box hung from a spatial tendon; elliptic
+                      cones with impratio 10, fluid viscosity 0.1, own
+                      timestep 0.002
 """
 
 from __future__ import annotations
@@ -30,11 +34,13 @@ BUNDLES = {
     "ur5e_hande_mjx": "ur5e_hande_mjx.npz",
     "scene_mjx": "scene_mjx.npz",
     "dual_arm": "dual_arm.npz",
+    "hande_scene": "hande_scene.npz",
 }
 
 _SCALARS = ("nbody", "njnt", "nq", "nv", "ngeom", "nsite", "npair", "neq", "ncon", "nslot", "nctrl",
             "hande_body", "tcp_site", "iterations", "ls_iterations", "disableflags", "ntree", "timestep",
-            "tolerance", "ls_tolerance", "impratio", "meaninertia", "nu", "nhullv", "nhulla", "integrator")
+            "tolerance", "ls_tolerance", "impratio", "meaninertia", "nu", "nhullv", "nhulla", "integrator",
+            "cone", "nten", "viscosity", "density")
 
 
 def save_bundle(m, path):

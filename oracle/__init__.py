@@ -43,6 +43,8 @@ def lib():
                                      ctypes.POINTER(ctypes.c_int)]
         _LIB.oracle_step.restype = ctypes.c_int
         _LIB.oracle_model_size.restype = ctypes.c_int
+        _LIB.oracle_cone_eval.argtypes = [ctypes.c_double] + [dp] * 4 + [ctypes.c_double] + [dp] * 4
+        _LIB.oracle_cone_eval.restype = ctypes.c_int
     return _LIB
 
 
@@ -77,6 +79,16 @@ def rollout(model, thetadot, q0, w, ptgt, qtgt, want_theta=True, want_slots=Fals
     if want_eef:
         out["eef"] = eef
     return out
+
+
+def cone_eval(mu, fri, D, jar, jv, alpha):
+    """The oracle's elliptic cone (one condim-3 contact): cost, force, Hessian
+    at jar and the line function along jar + alpha jv."""
+    c = ctypes.c_double(0)
+    f, H, line = np.zeros(3), np.zeros(9), np.zeros(3)
+    a = [np.ascontiguousarray(x, dtype=np.float64) for x in (fri, D, jar, jv)]
+    lib().oracle_cone_eval(float(mu), *(_p(x) for x in a), float(alpha), ctypes.byref(c), _p(f), _p(H), _p(line))
+    return c.value, f, H.reshape(3, 3), line
 
 
 def step(model, qpos, qvel, qacc_ws):

@@ -23,7 +23,11 @@
  *     velocity derivatives, no Coriolis) and general convex collision
  *     (capsule / cylinder / box / sphere / mesh convex hull) by Minkowski
  *     portal refinement (libccd's MPR, one contact per pair, the algorithm
- *     MuJoCo's general convex path used before nativeccd) + plane-convex.
+ *     MuJoCo's general convex path used before nativeccd) + plane-convex;
+ *   - the scene_robotiq_hande.xml features: elliptic
+ *     friction cones with impratio (MuJoCo's three-zone primal cone cost in
+ *     the Newton gradient, Hessian and an exact per-contact line search),
+ *     inertia-box fluid viscosity, spatial (two-site) tendon length limits.
  *
  * PARITY STATUS: MuJoCo/MJX are not importable or buildable here
  * (SURVEY.md §0.2, §8c), so the physics restatement is pinned only by the
@@ -44,6 +48,7 @@
 #define MINVAL 1e-15
 #define MINIMP 0.0001
 #define MAXIMP 0.9999
+#define PI 3.14159265358979323846
 
 typedef struct {
   double dist, pos[3], frame[9];
@@ -69,6 +74,11 @@ typedef struct {
   ocontact con[MAXCON];
   /* constraints */
   int nefc, efc_eq[MAXEFC];
+  /* efc_eq: 0 inequality (quadratic when jar < 0), 1 equality (always
+     quadratic), 2 elliptic contact: the normal row owns rows r..r+efc_dim-1,
+     3 elliptic friction row (evaluated by its normal row) */
+  int efc_dim[MAXEFC];
+  double efc_mu[MAXEFC], efc_fri[MAXEFC][2];
   double efc_J[MAXEFC][NV], efc_pos[MAXEFC], efc_margin[MAXEFC], efc_D[MAXEFC];
   double efc_aref[MAXEFC], efc_diag[MAXEFC], efc_vel[MAXEFC];
   double efc_solref[MAXEFC][2], efc_solimp[MAXEFC][5];
@@ -416,6 +426,34 @@ static void passive(const mpcr_model_t* m, odata* d) {
     jac_point(m, d, b, d->xipos[b], jac);
     for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] += jac[0][i] * f[0] + jac[1][i] * f[1] + jac[2][i] * f[2];
   }
+  /* fluid viscosity, MuJoCo's inertia-box model (mj_inertiaBoxFluidModel)
+     with density 0: the body's equivalent inertia box gives the sphere
+     diameter d = mean side; force -3 pi d eta v and torque -pi d^3 eta w at
+     xipos.  Both are isotropic, so the world-frame velocities serve. */
+  if (m->viscosity > 0)
+    for (int b = 1; b < m->nbody; b++) {
+      double mass = m->body_mass[b];
+      if (mass < MINVAL) continue;
+      const double* I = m->body_inertia[b];
+      double diam = 0;
+      for (int k = 0; k < 3; k++) {
+        double x = I[(k + 1) % 3] + I[(k + 2) % 3] - I[k];
+        diam += sqrt((x > MINVAL ? x : MINVAL) / mass * 6) / 3;
+      }
+      const double* cv = d->cvel[b];
+      const double* com = d->subtree_com[m->body_rootid[b]];
+      double r[3] = {d->xipos[b][0] - com[0], d->xipos[b][1] - com[1], d->xipos[b][2] - com[2]}, wr[3];
+      cross3(wr, cv, r);
+      double fl = -3 * PI * diam * m->viscosity, fa = -PI * diam * diam * diam * m->viscosity;
+      double f[3], t[3], jac[3][NV];
+      for (int k = 0; k < 3; k++) { f[k] = fl * (cv[3 + k] + wr[k]); t[k] = fa * cv[k]; }
+      jac_point(m, d, b, d->xipos[b], jac);
+      for (int i = 0; i < m->nv; i++) {
+        double q = jac[0][i] * f[0] + jac[1][i] * f[1] + jac[2][i] * f[2];
+        if (m->body_dofmask[b] >> i & 1u) q += d->cdof[i][0] * t[0] + d->cdof[i][1] * t[1] + d->cdof[i][2] * t[2];
+        d->qfrc_passive[i] += q;
+      }
+    }
 }
 
 static void rne(const mpcr_model_t* m, odata* d) {
@@ -1182,6 +1220,7 @@ static int add_row(const mpcr_model_t* m, odata* d, int eq, double pos, double m
   d->efc_pos[r] = pos;
   d->efc_margin[r] = margin;
   d->efc_diag[r] = diag;
+  d->efc_dim[r] = 1;
   memcpy(d->efc_solref[r], solref, 2 * sizeof(double));
   memcpy(d->efc_solimp[r], solimp, 5 * sizeof(double));
   for (int i = 0; i < m->nv; i++) d->efc_J[r][i] = 0;
@@ -1246,7 +1285,33 @@ static void make_constraint(const mpcr_model_t* m, odata* d) {
         }
       }
     }
-  /* contacts: pyramidal, condim 3 -> 4 rows J_n +- mu J_t{1,2}; condim 1 -> J_n */
+  /* spatial tendon limits (after the joint limits, mj_instantiateLimit):
+     length |x_s2 - x_s1|, moment (x_s2 - x_s1)^T (J_s2 - J_s1) / length */
+  if (!(m->disableflags & MPCR_DSBL_LIMIT))
+    for (int t = 0; t < m->nten; t++) {
+      if (!m->ten_limited[t]) continue;
+      int s1 = m->ten_site[t][0], s2 = m->ten_site[t][1];
+      double dif[3], j1[3][NV], j2[3][NV], jt[NV];
+      for (int k = 0; k < 3; k++) dif[k] = d->site_xpos[s2][k] - d->site_xpos[s1][k];
+      double len = norm3(dif), il = 1 / (len > MINVAL ? len : MINVAL);
+      jac_point(m, d, m->site_bodyid[s1], d->site_xpos[s1], j1);
+      jac_point(m, d, m->site_bodyid[s2], d->site_xpos[s2], j2);
+      for (int i = 0; i < nv; i++) {
+        double v = 0;
+        for (int k = 0; k < 3; k++) v += dif[k] * il * (j2[k][i] - j1[k][i]);
+        jt[i] = v;
+      }
+      for (int side = 0; side < 2; side++) {
+        double dist = side == 0 ? len - m->ten_range[t][0] : m->ten_range[t][1] - len;
+        if (dist < m->ten_margin[t]) {
+          int r = add_row(m, d, 0, dist, m->ten_margin[t], m->ten_invweight0[t], m->ten_solref[t], m->ten_solimp[t]);
+          if (r >= 0)
+            for (int i = 0; i < nv; i++) d->efc_J[r][i] = side == 0 ? jt[i] : -jt[i];
+        }
+      }
+    }
+  /* contacts: pyramidal, condim 3 -> 4 rows J_n +- mu J_t{1,2}; condim 1 -> J_n;
+     elliptic, condim 3 -> 3 rows J_n, J_t1, J_t2 (friction rows: pos 0) */
   for (int c = 0; c < d->ncon; c++) {
     ocontact* con = &d->con[c];
     if (!con->active) continue;
@@ -1267,6 +1332,17 @@ static void make_constraint(const mpcr_model_t* m, odata* d) {
       int r = add_row(m, d, 0, con->dist, margin, tran, m->pair_solref[p], m->pair_solimp[p]);
       if (r >= 0)
         for (int i = 0; i < nv; i++) d->efc_J[r][i] = jf[0][i];
+      continue;
+    }
+    if (m->cone == MPCR_CONE_ELLIPTIC) {
+      if (d->nefc + 3 > MAXEFC) { d->efc_trunc += 3; continue; }
+      for (int k = 0; k < 3; k++) {
+        int r = add_row(m, d, k == 0 ? 2 : 3, k == 0 ? con->dist : 0, k == 0 ? margin : 0, tran,
+                        m->pair_solref[p], m->pair_solimp[p]);
+        for (int i = 0; i < nv; i++) d->efc_J[r][i] = jf[k][i];
+        d->efc_dim[r] = k == 0 ? 3 : 0;
+        d->efc_fri[r][0] = d->efc_fri[r][1] = mu;
+      }
       continue;
     }
     for (int k = 1; k < 3; k++)
@@ -1298,6 +1374,17 @@ static void make_constraint(const mpcr_model_t* m, odata* d) {
     }
     d->efc_aref[r] = -B * v - K * imp * (d->efc_pos[r] - d->efc_margin[r]);
   }
+  /* elliptic contacts: friction R = R_n fri_0^2 / (fri_j^2 impratio), and the
+     cone slope of the primal zones mu = fri_0 sqrt(R_t1 / R_n) */
+  for (int r = 0; r < d->nefc; r++) {
+    if (d->efc_eq[r] != 2) continue;
+    double Rn = 1 / d->efc_D[r];
+    for (int j = 1; j < d->efc_dim[r]; j++) {
+      double fj = d->efc_fri[r][j - 1];
+      d->efc_D[r + j] = 1 / (Rn * d->efc_fri[r][0] * d->efc_fri[r][0] / (fj * fj * m->impratio));
+    }
+    d->efc_mu[r] = d->efc_fri[r][0] * sqrt(d->efc_D[r] / d->efc_D[r + 1]);
+  }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1313,13 +1400,67 @@ static void mulM(const mpcr_model_t* m, const odata* d, const double* x, double*
   }
 }
 
+/* Elliptic contact with normal row r (condim 3), MuJoCo's primal cone cost
+   (mj_constraintUpdate): with N = mu jar_n, U_j = fri_j jar_tj, T = |U|,
+     top    N >= mu T              satisfied, no cost;
+     bottom mu N + T <= 0          0.5 sum_k D_k jar_k^2 (all rows quadratic);
+     middle otherwise              0.5 Dm (N - mu T)^2, Dm = D_n / (mu^2 (1 + mu^2)).
+   Returns the cost; f = -d cost / d jar, H = d^2 cost / d jar^2 (3 x 3). */
+static double ell_update(const odata* d, int r, const double* jar, double f[3], double H[3][3]) {
+  double mu = d->efc_mu[r], N = mu * jar[r], U[2], T = 0;
+  for (int j = 0; j < 2; j++) { U[j] = d->efc_fri[r][j] * jar[r + 1 + j]; T += U[j] * U[j]; }
+  T = sqrt(T);
+  memset(H, 0, 9 * sizeof(double));
+  if (N >= mu * T || (T <= 0 && N >= 0)) {
+    f[0] = f[1] = f[2] = 0;
+    return 0;
+  }
+  if (mu * N + T <= 0 || (T <= 0 && N < 0)) {
+    double c = 0;
+    for (int k = 0; k < 3; k++) {
+      f[k] = -d->efc_D[r + k] * jar[r + k];
+      H[k][k] = d->efc_D[r + k];
+      c += 0.5 * d->efc_D[r + k] * jar[r + k] * jar[r + k];
+    }
+    return c;
+  }
+  double Dm = d->efc_D[r] / (mu * mu * (1 + mu * mu)), phi = N - mu * T;
+  /* grad phi = (mu, -mu fri_j U_j / T); hess phi_tt = -mu fri_j fri_k (delta_jk - U_j U_k / T^2) / T */
+  double g[3] = {mu, -mu * d->efc_fri[r][0] * U[0] / T, -mu * d->efc_fri[r][1] * U[1] / T};
+  for (int a = 0; a < 3; a++) f[a] = -Dm * phi * g[a];
+  for (int a = 0; a < 3; a++)
+    for (int b = 0; b < 3; b++) H[a][b] = Dm * g[a] * g[b];
+  for (int j = 0; j < 2; j++)
+    for (int k = 0; k < 2; k++) {
+      double h = -mu * d->efc_fri[r][j] * d->efc_fri[r][k] * ((j == k) - U[j] * U[k] / (T * T)) / T;
+      H[1 + j][1 + k] += Dm * phi * h;
+    }
+  return 0.5 * Dm * phi * phi;
+}
+
+/* constraint cost and forces (f = -D jar on the quadratic rows, cone forces) */
+static double efc_cost_force(const odata* d, const double* jar, double* f) {
+  double c = 0;
+  for (int r = 0; r < d->nefc; r++) {
+    int t = d->efc_eq[r];
+    if (t == 2) {
+      double H[3][3];
+      c += ell_update(d, r, jar, f + r, H);
+    } else if (t == 1 || (t == 0 && jar[r] < 0)) {
+      f[r] = -d->efc_D[r] * jar[r];
+      c += 0.5 * d->efc_D[r] * jar[r] * jar[r];
+    } else if (t == 0) {
+      f[r] = 0;
+    }
+  }
+  return c;
+}
+
 static double solver_cost(const mpcr_model_t* m, const odata* d, const double* qacc, const double* Ma,
                           const double* jar) {
-  double gauss = 0, c = 0;
+  double gauss = 0, f[MAXEFC];
   for (int i = 0; i < m->nv; i++) gauss += (Ma[i] - d->qfrc_smooth[i]) * (qacc[i] - d->qacc_smooth[i]);
-  for (int r = 0; r < d->nefc; r++)
-    if (d->efc_eq[r] || jar[r] < 0) c += d->efc_D[r] * jar[r] * jar[r];
-  return 0.5 * gauss + 0.5 * c;
+  return 0.5 * gauss + efc_cost_force(d, jar, f);
 }
 
 static void eval_jar(const mpcr_model_t* m, const odata* d, const double* x, double* jar) {
@@ -1330,11 +1471,51 @@ static void eval_jar(const mpcr_model_t* m, const odata* d, const double* x, dou
   }
 }
 
+/* cost and its first two alpha-derivatives of the elliptic contact at row r
+   along jar + alpha jv (the zones re-evaluated at alpha) */
+static void ell_line(const odata* d, int r, const double* jar, const double* jv, double alpha, double c[3]) {
+  double x[3], v[3];
+  for (int k = 0; k < 3; k++) { x[k] = jar[r + k] + alpha * jv[r + k]; v[k] = jv[r + k]; }
+  double mu = d->efc_mu[r], N = mu * x[0], N1 = mu * v[0], U[2], W[2], T = 0, UW = 0, WW = 0;
+  for (int j = 0; j < 2; j++) {
+    U[j] = d->efc_fri[r][j] * x[1 + j];
+    W[j] = d->efc_fri[r][j] * v[1 + j];
+    T += U[j] * U[j];
+    UW += U[j] * W[j];
+    WW += W[j] * W[j];
+  }
+  T = sqrt(T);
+  c[0] = c[1] = c[2] = 0;
+  if (N >= mu * T || (T <= 0 && N >= 0)) return;
+  if (mu * N + T <= 0 || (T <= 0 && N < 0)) {
+    for (int k = 0; k < 3; k++) {
+      double D = d->efc_D[r + k];
+      c[0] += 0.5 * D * x[k] * x[k];
+      c[1] += D * x[k] * v[k];
+      c[2] += D * v[k] * v[k];
+    }
+    return;
+  }
+  double Dm = d->efc_D[r] / (mu * mu * (1 + mu * mu));
+  double T1 = UW / T, T2 = (WW - T1 * T1) / T;
+  double phi = N - mu * T, phi1 = N1 - mu * T1, phi2 = -mu * T2;
+  c[0] = 0.5 * Dm * phi * phi;
+  c[1] = Dm * phi * phi1;
+  c[2] = Dm * (phi1 * phi1 + phi * phi2);
+}
+
 static lspt ls_eval(const odata* d, const double qg[3], const double* jar, const double* jv, double alpha) {
-  double q0 = qg[0], q1 = qg[1], q2 = qg[2];
+  double q0 = qg[0], q1 = qg[1], q2 = qg[2], e[3] = {0, 0, 0};
   for (int r = 0; r < d->nefc; r++) {
     double x = jar[r] + alpha * jv[r];
-    if (d->efc_eq[r] || x < 0) {
+    if (d->efc_eq[r] == 2) {
+      double c[3];
+      ell_line(d, r, jar, jv, alpha, c);
+      for (int k = 0; k < 3; k++) e[k] += c[k];
+      continue;
+    }
+    if (d->efc_eq[r] == 3) continue;
+    if (d->efc_eq[r] == 1 || x < 0) {
       double D = d->efc_D[r];
       q0 += 0.5 * D * jar[r] * jar[r];
       q1 += D * jv[r] * jar[r];
@@ -1343,9 +1524,10 @@ static lspt ls_eval(const odata* d, const double qg[3], const double* jar, const
   }
   lspt p;
   p.alpha = alpha;
-  p.cost = alpha * alpha * q2 + alpha * q1 + q0;
-  p.d0 = 2 * alpha * q2 + q1;
-  p.d1 = 2 * q2 + (q2 == 0 ? MINVAL : 0);
+  p.cost = alpha * alpha * q2 + alpha * q1 + q0 + e[0];
+  p.d0 = 2 * alpha * q2 + q1 + e[1];
+  p.d1 = 2 * q2 + e[2];
+  if (p.d1 == 0) p.d1 = MINVAL;
   return p;
 }
 
@@ -1375,11 +1557,11 @@ static void solve(const mpcr_model_t* m, odata* d) {
   double cost = solver_cost(m, d, qacc, Ma, jar), prev_cost = 1e300;
   for (int it = 0;; it++) {
     /* gradient and Newton direction with the Hessian of the active set */
-    double grad[NV], H[NV][NV], Lh[NV][NV], Mgrad[NV], search[NV];
+    double grad[NV], H[NV][NV], Lh[NV][NV], Mgrad[NV], search[NV], f[MAXEFC];
+    efc_cost_force(d, jar, f);
     for (int i = 0; i < nv; i++) {
       double qc = 0;
-      for (int r = 0; r < nefc; r++)
-        if (d->efc_eq[r] || jar[r] < 0) qc += d->efc_J[r][i] * (-d->efc_D[r] * jar[r]);
+      for (int r = 0; r < nefc; r++) qc += d->efc_J[r][i] * f[r];
       grad[i] = Ma[i] - d->qfrc_smooth[i] - qc;
     }
     double gn = 0;
@@ -1390,9 +1572,23 @@ static void solve(const mpcr_model_t* m, odata* d) {
       for (int j = 0; j < nv; j++) {
         double h = d->M[i][j];
         for (int r = 0; r < nefc; r++)
-          if (d->efc_eq[r] || jar[r] < 0) h += d->efc_J[r][i] * d->efc_D[r] * d->efc_J[r][j];
+          if (d->efc_eq[r] == 1 || (d->efc_eq[r] == 0 && jar[r] < 0))
+            h += d->efc_J[r][i] * d->efc_D[r] * d->efc_J[r][j];
         H[i][j] = h;
       }
+    /* cone Hessian blocks J_c^T H_c J_c of the elliptic contacts */
+    for (int r = 0; r < nefc; r++) {
+      if (d->efc_eq[r] != 2) continue;
+      double fc[3], Hc[3][3];
+      ell_update(d, r, jar, fc, Hc);
+      for (int i = 0; i < nv; i++)
+        for (int j = 0; j < nv; j++) {
+          double h = 0;
+          for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) h += d->efc_J[r + a][i] * Hc[a][b] * d->efc_J[r + b][j];
+          H[i][j] += h;
+        }
+    }
     chol(Lh, H, nv);
     chol_solve(Mgrad, Lh, grad, nv);
     for (int i = 0; i < nv; i++) search[i] = -Mgrad[i];
@@ -1447,11 +1643,9 @@ static void solve(const mpcr_model_t* m, odata* d) {
   memcpy(d->qacc, qacc, sizeof(double) * nv);
   /* efc_force / qfrc_constraint at the final acceleration */
   for (int i = 0; i < nv; i++) d->qfrc_constraint[i] = 0;
-  for (int r = 0; r < nefc; r++) {
-    double f = (d->efc_eq[r] || jar[r] < 0) ? -d->efc_D[r] * jar[r] : 0;
-    d->efc_force[r] = f;
-    for (int i = 0; i < nv; i++) d->qfrc_constraint[i] += d->efc_J[r][i] * f;
-  }
+  efc_cost_force(d, jar, d->efc_force);
+  for (int r = 0; r < nefc; r++)
+    for (int i = 0; i < nv; i++) d->qfrc_constraint[i] += d->efc_J[r][i] * d->efc_force[r];
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1627,4 +1821,28 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
   free(cprev);
   free(d);
   return status;
+}
+
+/* test hook: the elliptic cone of one condim-3 contact (rows 0..2) at jar, and
+   its line function along jar + alpha jv (cost, d/dalpha, d2/dalpha2) */
+int oracle_cone_eval(double mu, const double fri[2], const double D[3], const double jar[3], const double jv[3],
+                     double alpha, double* cost, double f[3], double H[9], double line[3]) {
+  odata* d = (odata*)calloc(1, sizeof(odata));
+  if (!d) return -1;
+  d->nefc = 3;
+  for (int k = 0; k < 3; k++) {
+    d->efc_eq[k] = k == 0 ? 2 : 3;
+    d->efc_D[k] = D[k];
+  }
+  d->efc_dim[0] = 3;
+  d->efc_mu[0] = mu;
+  d->efc_fri[0][0] = fri[0];
+  d->efc_fri[0][1] = fri[1];
+  double Hc[3][3];
+  *cost = ell_update(d, 0, jar, f, Hc);
+  for (int a = 0; a < 3; a++)
+    for (int b = 0; b < 3; b++) H[3 * a + b] = Hc[a][b];
+  ell_line(d, 0, jar, jv, alpha, line);
+  free(d);
+  return 0;
 }

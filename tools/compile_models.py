@@ -18,12 +18,15 @@ SCENES = {
     "ur5e_hande_mjx": "universal_robots_ur5e/ur5e_1_robotiq_hande_mjx.xml",
     "scene_mjx": "universal_robots_ur5e/scene_mjx.xml",
     "dual_arm": "universal_robots_ur5e/dual_arm_gripper_scene.xml",
+    "hande_scene": "universal_robots_ur5e/scene_robotiq_hande.xml",
 }
+# scenes simulated at their own timestep (not planner scenes)
+NATIVE_DT = {"hande_scene"}
 
 
 def main():
     for name, rel in SCENES.items():
-        m = mjcf.compile_mjcf(os.path.join(REF, rel), timestep=0.05)
+        m = mjcf.compile_mjcf(os.path.join(REF, rel), timestep=None if name in NATIVE_DT else 0.05)
         out = os.path.join(models.HERE, models.BUNDLES[name])
         models.save_bundle(m, out)
         print(f"{name}: nbody={m.nbody} nq={m.nq} nv={m.nv} npair={m.npair} nslot={m.nslot} -> {out}")
