@@ -81,7 +81,7 @@ struct mpcr_engine {
 // wide one (dual-arm class).
 static bool needs_wide(const mpcr_model_t& m, const DevModel& d) {
   if (m.nv > 16 || d.nbody > 16 || d.ngeom > 24 || m.nq > 24 || m.nu > 0 || d.has_spring ||
-      m.integrator != MPCR_INT_EULER)
+      m.integrator != MPCR_INT_EULER || m.cone != MPCR_CONE_PYRAMIDAL || m.nten > 0 || m.viscosity != 0)
     return true;
   for (int e = 0; e < m.neq; e++)
     if (m.eq_type[e] != MPCR_EQ_JOINT) return true;
@@ -131,11 +131,12 @@ static int check_model(const mpcr_model_t& m) {
       m.nu > MPCR_MAX_ACT || m.nhullv > MPCR_MAX_HULLV || m.nhulla > MPCR_MAX_HULLA || m.nu < 0 || m.nhullv < 0 ||
       m.nhulla < 0)
     return fail(MPCR_EMODEL, "model exceeds blob capacity");
-  if ((m.integrator != MPCR_INT_EULER && m.integrator != MPCR_INT_IMPLICITFAST) || m.cone != MPCR_CONE_PYRAMIDAL)
-    return fail(MPCR_EMODEL, "only Euler / implicitfast with pyramidal cones supported");
+  if ((m.integrator != MPCR_INT_EULER && m.integrator != MPCR_INT_IMPLICITFAST) || (m.cone != MPCR_CONE_PYRAMIDAL && m.cone != MPCR_CONE_ELLIPTIC))
+    return fail(MPCR_EMODEL, "only Euler / implicitfast with pyramidal or elliptic cones supported");
   if (m.nten < 0 || m.nten > MPCR_MAX_TEN) return fail(MPCR_EMODEL, "model exceeds blob capacity");
-  if (m.nten != 0 || m.viscosity != 0 || m.density != 0)
-    return fail(MPCR_EMODEL, "spatial tendons and fluid forces are not built on the device yet");
+  if (m.density != 0) return fail(MPCR_EMODEL, "fluid density (inertia-box drag terms) not supported");
+  if (m.viscosity != 0 && m.integrator != MPCR_INT_EULER)
+    return fail(MPCR_EMODEL, "fluid viscosity with implicit integration not supported");
   for (int g = 0; g < m.ngeom; g++)
     if (m.geom_hulladr[g] >= 0 && m.geom_hulladr[g] + m.geom_hullnum[g] > m.nhullv)
       return fail(MPCR_EMODEL, "geom %d hull outside the vertex table", g);
@@ -315,6 +316,45 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.tree_mass[t] += (float)m.body_mass[b];
   }
   d.ntree = (int)roots.size();
+  // inertia-box viscosity (mj_inertiaBoxFluidModel, density 0): the body's
+  // equivalent box gives the diameter d = mean side
+  if (m.viscosity > 0 && !no_passive)
+    for (int b = 1; b < m.nbody; b++) {
+      const int i = dmap[b];
+      const double mass = m.body_mass[b];
+      if (i < 0 || mass < 1e-15) continue;
+      double diam = 0;
+      for (int k = 0; k < 3; k++) {
+        double x = m.body_inertia[b][(k + 1) % 3] + m.body_inertia[b][(k + 2) % 3] - m.body_inertia[b][k];
+        diam += std::sqrt((x > 1e-15 ? x : 1e-15) / mass * 6) / 3;
+      }
+      d.body_visc[i][0] = (float)(-3 * M_PI * diam * m.viscosity);
+      d.body_visc[i][1] = (float)(-M_PI * diam * diam * diam * m.viscosity);
+    }
+  // spatial tendons: site bodies and positions
+  if (m.nten > DX_NTEN) return fail(MPCR_EMODEL, "%d spatial tendons > %d", m.nten, DX_NTEN);
+  d.nten = m.nten;
+  for (int t = 0; t < m.nten; t++) {
+    for (int k = 0; k < 2; k++) {
+      const int st = m.ten_site[t][k], b = m.site_bodyid[st];
+      if (dmap[b] >= 0) {
+        d.ten_body[t][k] = dmap[b];
+        for (int c = 0; c < 3; c++) d.ten_pos[t][k][c] = (float)m.site_pos[st][c];
+      } else {
+        double r[3];
+        h_rot(r, &wquat[4 * b], m.site_pos[st]);
+        d.ten_body[t][k] = -1;
+        for (int c = 0; c < 3; c++) d.ten_pos[t][k][c] = (float)(wpos[3 * b + c] + r[c]);
+      }
+    }
+    d.ten_limited[t] = m.ten_limited[t];
+    for (int k = 0; k < 2; k++) { d.ten_range[t][k] = (float)m.ten_range[t][k]; d.ten_solref[t][k] = (float)m.ten_solref[t][k]; }
+    for (int k = 0; k < 5; k++) d.ten_solimp[t][k] = (float)m.ten_solimp[t][k];
+    d.ten_margin[t] = (float)m.ten_margin[t];
+    d.ten_invw[t] = (float)m.ten_invweight0[t];
+  }
+  d.cone = m.cone;
+  d.impratio = (float)m.impratio;
   for (int t = 0; t < d.ntree; t++)
     if (d.tree_mass[t] <= 0) d.tree_mass[t] = 1.f;
   int rounds = 0;
@@ -420,6 +460,8 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.pair_slotadr[p] = m.pair_slotadr[p];
     d.pair_condim[p] = m.pair_condim[p];
     d.pair_friction[p] = (float)m.pair_friction[p];
+    d.pair_cmu[p] = (float)(m.pair_friction[p] / std::sqrt(m.impratio > 0 ? m.impratio : 1.0));
+    if (m.pair_condim[p] != 1 && m.pair_condim[p] != 3) return fail(MPCR_EMODEL, "condim %d not supported", m.pair_condim[p]);
     d.pair_margin[p] = (float)(m.pair_margin[p] - m.pair_gap[p]);
     for (int k = 0; k < 2; k++) d.pair_solref[p][k] = (float)m.pair_solref[p][k];
     for (int k = 0; k < 5; k++) d.pair_solimp[p][k] = (float)m.pair_solimp[p][k];

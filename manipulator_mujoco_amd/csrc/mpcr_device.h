@@ -25,6 +25,7 @@ constexpr int DX_NTREE = 4;
 constexpr int DX_MAXACT = 20;  // active contacts kept per step
 constexpr int DX_MAXEFC = 96;  // constraint rows kept per step
 constexpr int DX_NSLOT = 192;  // robot-masked contact slots
+constexpr int DX_NTEN = 2;     // spatial (two-site) tendons with length limits
 
 // body kinds for the kinematics pass
 enum { BK_STATIC = 0, BK_FREE = 1, BK_HINGE = 2, BK_SLIDE = 3, BK_WELD = 4 };
@@ -113,6 +114,18 @@ struct DevModel {
   const float4* hull_adjv;  // neighbour xyz | neighbour index (bits in w): one load per neighbour
 
   int ctrl_qposadr[DX_NCTRL], ctrl_dofadr[DX_NCTRL];
+
+  // scene_robotiq_hande.xml features (wide variant) ----------------------------
+  int cone;        // 0 pyramidal, 1 elliptic (condim-3 contacts: rows n, t1, t2)
+  int nten;
+  float impratio;
+  float pair_cmu[DX_NP];    // elliptic cone slope: friction / sqrt(impratio)
+  float body_visc[DX_NB][2];  // inertia-box viscosity: force = [0] v, torque = [1] w (at xipos)
+  // spatial tendons: site body (device index, -1 static) and the site position
+  // in that body's frame (static: in world)
+  int ten_body[DX_NTEN][2], ten_limited[DX_NTEN];
+  float ten_pos[DX_NTEN][2][4];
+  float ten_range[DX_NTEN][2], ten_solref[DX_NTEN][2], ten_solimp[DX_NTEN][5], ten_margin[DX_NTEN], ten_invw[DX_NTEN];
 };
 
 }  // namespace mpcr

@@ -86,6 +86,7 @@ struct __align__(16) SmemT {
   float cprev[CPREV_GLOBAL ? 1 : DX_NSLOT];  // previous-step masked slot distances (cost_c)
   float par[PAR_N];       // q0 | w | ptgt | qtgt (normalised)
   float eqp[NEQP][2][4];  // connect anchors in world (body1, body2)
+  float tenp[WIDE ? DX_NTEN : 1][2][4];  // spatial-tendon sites in world
   float actf[NACT];       // actuator forces
   int ncon, nefc, ncvx, pad_;
   // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the

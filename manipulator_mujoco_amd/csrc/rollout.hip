@@ -1257,12 +1257,21 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
 
 struct LsPt { float alpha, cost, d0, d1; };
 
+// elliptic rows: efc_src = (5 << 24) | (contact << 14) | (pair << 4) | side
+__device__ __forceinline__ bool ell_row(int src) { return (src >> 24) == 5; }
+__device__ __forceinline__ bool ell_head(int src) { return (src >> 24) == 5 && (src & 15) == 0; }
+__device__ __forceinline__ int ell_pair(int src) { return (src >> 4) & 1023; }
+
+
 template <class S>
 __device__ __forceinline__ void ls_rows(const S& s, int lane, float alpha, float& q0, float& q1, float& q2) {
   q0 = q1 = q2 = 0.f;
   for (int r = lane; r < s.nefc; r += S::HL) {
     float jar = s.efc_jar[r], jv = s.efc_jv[r];
     float x = jar + alpha * jv;
+    if constexpr (S::WIDE) {
+      if (ell_row(s.efc_src[r])) continue;
+    }
     if (((s.efc_src[r] >> 24) == 1) || x < 0.f) {
       float D = s.efc_D[r];
       q0 += 0.5f * D * jar * jar;
@@ -1301,6 +1310,9 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
   for (int r = lane; r < s.nefc; r += S::HL) {
     const float jar = s.efc_jar[r], jv = s.efc_jv[r], D = s.efc_D[r];
     const bool eq = (s.efc_src[r] >> 24) == 1;
+    if constexpr (S::WIDE) {
+      if (ell_row(s.efc_src[r])) continue;
+    }
     const float c0 = 0.5f * D * jar * jar, c1 = D * jv * jar, c2 = 0.5f * D * jv * jv;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -1312,6 +1324,99 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
   p0 = ls_make(a0, q[0], q[1], q[2]);
   p1 = ls_make(a1, q[3], q[4], q[5]);
   p2 = ls_make(a2, q[6], q[7], q[8]);
+}
+
+// ---------------------------------------------------------------------------
+// elliptic friction cone of one condim-3 contact (rows n, t1, t2; equal
+// sliding frictions), MuJoCo's primal three-zone cost (oracle: ell_update /
+// ell_line).  N = mu x_n, U = fri x_t, T = |U|:
+//   top    N >= mu T        no cost
+//   bottom mu N + T <= 0    0.5 sum D_k x_k^2
+//   middle                  0.5 Dm (N - mu T)^2, Dm = D_n / (mu^2 (1 + mu^2))
+
+// cost; f = -dcost/dx; h = Hessian (h00 h01 h02 h11 h12 h22)
+__device__ __forceinline__ float cone_update(const float x[3], float mu, float fri, const float D[3], float f[3],
+                                             float h[6]) {
+  const float N = mu * x[0], U0 = fri * x[1], U1 = fri * x[2], T = sqrtf(U0 * U0 + U1 * U1);
+  if (N >= mu * T || (T <= 0.f && N >= 0.f)) {
+    f[0] = f[1] = f[2] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; k++) h[k] = 0.f;
+    return 0.f;
+  }
+  if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
+    f[0] = -D[0] * x[0]; f[1] = -D[1] * x[1]; f[2] = -D[2] * x[2];
+    h[0] = D[0]; h[1] = 0.f; h[2] = 0.f; h[3] = D[1]; h[4] = 0.f; h[5] = D[2];
+    return 0.5f * (D[0] * x[0] * x[0] + D[1] * x[1] * x[1] + D[2] * x[2] * x[2]);
+  }
+  const float Dm = D[0] / (mu * mu * (1.f + mu * mu)), phi = N - mu * T, iT = 1.f / T;
+  const float g[3] = {mu, -mu * fri * U0 * iT, -mu * fri * U1 * iT};
+  f[0] = -Dm * phi * g[0]; f[1] = -Dm * phi * g[1]; f[2] = -Dm * phi * g[2];
+  const float c = -Dm * phi * mu * fri * fri * iT, u0 = U0 * iT, u1 = U1 * iT;
+  h[0] = Dm * g[0] * g[0];
+  h[1] = Dm * g[0] * g[1];
+  h[2] = Dm * g[0] * g[2];
+  h[3] = Dm * g[1] * g[1] + c * (1.f - u0 * u0);
+  h[4] = Dm * g[1] * g[2] - c * u0 * u1;
+  h[5] = Dm * g[2] * g[2] + c * (1.f - u1 * u1);
+  return 0.5f * Dm * phi * phi;
+}
+
+// cost and its first two derivatives along x + alpha v (zones at alpha)
+__device__ __forceinline__ void cone_line(const float x0[3], const float v[3], float alpha, float mu, float fri,
+                                          const float D[3], float& c0, float& c1, float& c2) {
+  const float x[3] = {x0[0] + alpha * v[0], x0[1] + alpha * v[1], x0[2] + alpha * v[2]};
+  const float N = mu * x[0], U0 = fri * x[1], U1 = fri * x[2], W0 = fri * v[1], W1 = fri * v[2];
+  const float T = sqrtf(U0 * U0 + U1 * U1);
+  if (N >= mu * T || (T <= 0.f && N >= 0.f)) { c0 = c1 = c2 = 0.f; return; }
+  if (mu * N + T <= 0.f || (T <= 0.f && N < 0.f)) {
+    c0 = 0.5f * (D[0] * x[0] * x[0] + D[1] * x[1] * x[1] + D[2] * x[2] * x[2]);
+    c1 = D[0] * x[0] * v[0] + D[1] * x[1] * v[1] + D[2] * x[2] * v[2];
+    c2 = D[0] * v[0] * v[0] + D[1] * v[1] * v[1] + D[2] * v[2] * v[2];
+    return;
+  }
+  const float Dm = D[0] / (mu * mu * (1.f + mu * mu));
+  const float T1 = (U0 * W0 + U1 * W1) / T, T2 = (W0 * W0 + W1 * W1 - T1 * T1) / T;
+  const float phi = N - mu * T, phi1 = mu * v[0] - mu * T1, phi2 = -mu * T2;
+  c0 = 0.5f * Dm * phi * phi;
+  c1 = Dm * phi * phi1;
+  c2 = Dm * (phi1 * phi1 + phi * phi2);
+}
+
+template <class S>
+__device__ __forceinline__ const float* jrow_ptr(const S& s, const float* gx, int r) {
+  return (S::JL == S::MAXEFC || r < S::JL) ? &s.J[r][0] : gx + (r - S::JL) * S::LDJ;
+}
+
+// line-search extra terms of the elliptic contacts at three step sizes
+template <class S>
+__device__ __forceinline__ void ls_cones3(const S& s, const DevModel* __restrict__ m, int lane, const float al[3],
+                                          float e[9]) {
+#pragma unroll
+  for (int k = 0; k < 9; k++) e[k] = 0.f;
+  for (int r = lane; r < s.nefc; r += S::HL) {
+    const int src = s.efc_src[r];
+    if (!ell_head(src)) continue;
+    const int p = ell_pair(src);
+    const float x[3] = {s.efc_jar[r], s.efc_jar[r + 1], s.efc_jar[r + 2]};
+    const float v[3] = {s.efc_jv[r], s.efc_jv[r + 1], s.efc_jv[r + 2]};
+    const float D[3] = {s.efc_D[r], s.efc_D[r + 1], s.efc_D[r + 2]};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float c0, c1, c2;
+      cone_line(x, v, al[k], m->pair_cmu[p], m->pair_friction[p], D, c0, c1, c2);
+      e[3 * k] += c0; e[3 * k + 1] += c1; e[3 * k + 2] += c2;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) e[k] = hsum<S::CPW>(e[k]);
+}
+
+__device__ __forceinline__ void ls_add(LsPt& p, float c0, float c1, float c2) {
+  p.cost += c0;
+  p.d0 += c1;
+  p.d1 = p.d1 - (p.d1 == kMinVal ? kMinVal : 0.f) + c2;
+  if (p.d1 == 0.f) p.d1 = kMinVal;
 }
 
 // Re-derive the model pointer from the kernel argument through an opaque
@@ -1602,6 +1707,19 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         }
         s.eqp[e][side][0] = pw[0]; s.eqp[e][side][1] = pw[1]; s.eqp[e][side][2] = pw[2];
       }
+      if (lane < 2 * m->nten) {  // spatial-tendon sites in world
+        const int t = lane >> 1, side = lane & 1, bb = m->ten_body[t][side];
+        const float* a = m->ten_pos[t][side];
+        float pw[3] = {a[0], a[1], a[2]};
+        if (bb >= 0) {
+          float R[9], w[3];
+#pragma unroll
+          for (int k = 0; k < 9; k++) R[k] = s.xmat[bb][k];
+          mv(w, R, a);
+          pw[0] = s.xpos[bb][0] + w[0]; pw[1] = s.xpos[bb][1] + w[1]; pw[2] = s.xpos[bb][2] + w[2];
+        }
+        s.tenp[t][side][0] = pw[0]; s.tenp[t][side][1] = pw[1]; s.tenp[t][side][2] = pw[2];
+      }
     }
     for (int tr = 0; tr < m->ntree; tr++) {
       float mm = (lane < nb && m->body_tree[lane] == tr) ? m->body_mass[lane] : 0.f;
@@ -1806,7 +1924,16 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       float F[3] = {-m->gravity[0] * gc, -m->gravity[1] * gc, -m->gravity[2] * gc};
       float rr[3] = {s.xipos[lane][0] - s.com[tr][0], s.xipos[lane][1] - s.com[tr][1],
                      s.xipos[lane][2] - s.com[tr][2]}, tq[3];
+      float Tv[3] = {0.f, 0.f, 0.f};
+      if constexpr (S::WIDE) {  // inertia-box viscosity at xipos: v = v_com + w x rr
+        const float vl = m->body_visc[lane][0], va = m->body_visc[lane][1];
+        float wr[3];
+        cross(wr, cv, rr);
+#pragma unroll
+        for (int k = 0; k < 3; k++) { F[k] += vl * (cv[3 + k] + wr[k]); Tv[k] = va * cv[k]; }
+      }
       cross(tq, rr, F);
+      tq[0] += Tv[0]; tq[1] += Tv[1]; tq[2] += Tv[2];
       s.cfrc[lane][0] = f[0] + vf[0] - tq[0];
       s.cfrc[lane][1] = f[1] + vf[1] - tq[1];
       s.cfrc[lane][2] = f[2] + vf[2] - tq[2];
@@ -1983,17 +2110,31 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       }
       int nlim;
       const int lim_pre = hscan_excl<S::CPW>(nlim_l, nlim);
+      // spatial-tendon limit rows after the joint limits (wave-uniform)
+      int ntr = 0, tsides = 0;
+      if constexpr (S::WIDE) {
+        if (!(m->disableflags & 32))
+          for (int t = 0; t < m->nten; t++) {
+            if (!m->ten_limited[t]) continue;
+            const float dx = s.tenp[t][1][0] - s.tenp[t][0][0], dy = s.tenp[t][1][1] - s.tenp[t][0][1],
+                        dz = s.tenp[t][1][2] - s.tenp[t][0][2];
+            const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+            if (len - m->ten_range[t][0] < m->ten_margin[t]) { tsides |= 1 << (2 * t); ntr++; }
+            if (m->ten_range[t][1] - len < m->ten_margin[t]) { tsides |= 2 << (2 * t); ntr++; }
+          }
+      }
+      const bool ell = S::WIDE && m->cone == 1;
       int ncr = 0;
-      if (lane < ncon) ncr = m->pair_condim[s.con_pair[lane]] == 1 ? 1 : 4;
+      if (lane < ncon) ncr = m->pair_condim[s.con_pair[lane]] == 1 ? 1 : (ell ? 3 : 4);
       int ncrow;
       const int con_pre = hscan_excl<S::CPW>(ncr, ncrow);
-      int nefc = neq + nlim + ncrow;
+      int nefc = neq + nlim + ntr + ncrow;
       int keep_con = ncon;
       if (nefc > S::MAXEFC) {  // keep the longest prefix of contacts that fits
-        const int room = S::MAXEFC - neq - nlim;
+        const int room = S::MAXEFC - neq - nlim - ntr;
         const unsigned long long fit = hballot<S::CPW>(lane < ncon && con_pre + ncr <= room);
         keep_con = __popcll(fit);
-        nefc = neq + nlim + (keep_con > 0 ? hshfl<S::CPW>(con_pre + ncr, keep_con - 1) : 0);
+        nefc = neq + nlim + ntr + (keep_con > 0 ? hshfl<S::CPW>(con_pre + ncr, keep_con - 1) : 0);
         status |= 1;
       }
       // equality rows: joint (side 0) or connect component side - 1
@@ -2004,15 +2145,28 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         if (lsides & 1) s.efc_src[o++] = (2 << 24) | (lane << 4) | 0;
         if (lsides & 2) s.efc_src[o++] = (2 << 24) | (lane << 4) | 1;
       }
+      if constexpr (S::WIDE) {
+        if (lane == 0 && ntr) {
+          int o = neq + nlim;
+          for (int t = 0; t < m->nten; t++)
+            for (int side = 0; side < 2; side++)
+              if ((tsides >> (2 * t + side)) & 1) s.efc_src[o++] = (4 << 24) | (t << 4) | side;
+        }
+      }
       if (lane < keep_con) {
-        const int o = neq + nlim + con_pre;
+        const int o = neq + nlim + ntr + con_pre;
         s.con_row[lane] = o;
-        for (int r = 0; r < ncr; r++) s.efc_src[o + r] = (3 << 24) | (lane << 4) | r;
+        if (ncr == 3) {  // elliptic (wide variant only)
+          const int p = s.con_pair[lane];
+          for (int r = 0; r < 3; r++) s.efc_src[o + r] = (5 << 24) | (lane << 14) | (p << 4) | r;
+        } else {
+          for (int r = 0; r < ncr; r++) s.efc_src[o + r] = (3 << 24) | (lane << 4) | r;
+        }
       }
       if (lane == 0) s.nefc = nefc;
       sync();
       // Jacobian entries of equality/limit rows: (row, dof)
-      const int nsimple = neq + nlim;
+      const int nsimple = neq + nlim + ntr;
       for (int idx = lane; idx < nsimple * NVW; idx += S::HL) {
         const int r = idx >> S::LOG_NVW, i = idx & (NVW - 1);
         const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
@@ -2041,6 +2195,26 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             const float* c = m->eq_data[id];
             const float dif = s.qpos[m->jnt_qposadr[j2]] - m->jnt_qpos0[j2];
             v -= c[1] + dif * (2.f * c[2] + dif * (3.f * c[3] + dif * 4.f * c[4]));
+          }
+        } else if (S::WIDE && kind == 4) {  // tendon: +-(dif / len) . (J_p(site2) - J_p(site1))
+          if (i < nv) {
+            const float dif[3] = {s.tenp[id][1][0] - s.tenp[id][0][0], s.tenp[id][1][1] - s.tenp[id][0][1],
+                                  s.tenp[id][1][2] - s.tenp[id][0][2]};
+            const float il = 1.f / fmaxf(sqrtf(dot3(dif, dif)), kMinVal);
+            const float* cd = s.cdof[i];
+#pragma unroll
+            for (int e2 = 0; e2 < 2; e2++) {
+              const int bb = m->ten_body[id][e2];
+              if (bb >= 0 && ((m->body_dofmask[bb] >> i) & 1u)) {
+                const int tr = m->body_tree[bb];
+                float rr[3] = {s.tenp[id][e2][0] - s.com[tr][0], s.tenp[id][e2][1] - s.com[tr][1],
+                               s.tenp[id][e2][2] - s.com[tr][2]}, cr[3];
+                cross(cr, cd, rr);
+                const float jp = (dif[0] * (cd[3] + cr[0]) + dif[1] * (cd[4] + cr[1]) + dif[2] * (cd[5] + cr[2])) * il;
+                v += e2 == 0 ? -jp : jp;
+              }
+            }
+            if (side) v = -v;
           }
         } else if (i == m->jnt_dofadr[id]) {
           v = side == 0 ? 1.f : -1.f;
@@ -2073,6 +2247,10 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         const int off = s.con_row[c];
         if (m->pair_condim[p] == 1) {
           jstore(s, gx, off, i, jn);
+        } else if (S::WIDE && m->cone == 1) {  // elliptic: J_n, J_t1, J_t2
+          jstore(s, gx, off + 0, i, jn);
+          jstore(s, gx, off + 1, i, f[3] * jd[0] + f[4] * jd[1] + f[5] * jd[2]);
+          jstore(s, gx, off + 2, i, f[6] * jd[0] + f[7] * jd[1] + f[8] * jd[2]);
         } else {
           const float mu = m->pair_friction[p];
           const float jt1 = f[3] * jd[0] + f[4] * jd[1] + f[5] * jd[2];
@@ -2117,6 +2295,22 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           diag = m->dof_invweight0[m->jnt_dofadr[id]];
           sref = m->jnt_solref[id];
           simp = m->jnt_solimp[id];
+        } else if (S::WIDE && kind == 4) {
+          const float dx = s.tenp[id][1][0] - s.tenp[id][0][0], dy = s.tenp[id][1][1] - s.tenp[id][0][1],
+                      dz = s.tenp[id][1][2] - s.tenp[id][0][2];
+          const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+          pos = side == 0 ? len - m->ten_range[id][0] : m->ten_range[id][1] - len;
+          margin = m->ten_margin[id];
+          diag = m->ten_invw[id];
+          sref = m->ten_solref[id];
+          simp = m->ten_solimp[id];
+        } else if (S::WIDE && kind == 5) {  // elliptic: all rows take the normal's impedance
+          const int c = (src >> 14) & 1023, p = ell_pair(src);
+          pos = s.con_dist[c];
+          margin = m->pair_margin[p];
+          diag = m->pair_diag[p];
+          sref = m->pair_solref[p];
+          simp = m->pair_solimp[p];
         } else {
           const int p = s.con_pair[id];
           pos = s.con_dist[id];
@@ -2128,7 +2322,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         }
         const float vel = jdot(s, gx, r, s.qvel);
         const float imp = impedance(simp, pos, margin);
-        const float R = fmaxf((1.f - imp) / imp * diag, kMinVal);
+        float R = fmaxf((1.f - imp) / imp * diag, kMinVal);
+        // elliptic friction rows: R_t = R_n / impratio (equal sliding
+        // frictions), no position term in aref
+        const bool efric = S::WIDE && kind == 5 && side > 0;
+        if (efric) R = R / m->impratio;
         float tc = sref[0];
         const float dr = sref[1];
         const float dmax = clampf(simp[1], kMinImp, kMaxImp);
@@ -2142,7 +2340,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           B = -dr / dmax;
         }
         s.efc_D[r] = 1.f / R;
-        s.efc_aref[r] = -B * vel - K * imp * (pos - margin);
+        s.efc_aref[r] = -B * vel - K * imp * (efric ? 0.f : pos - margin);
       }
       sync();
     }
@@ -2166,6 +2364,23 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             const float jw = jdot(s, gx, r, s.qws) - s.efc_aref[r];
             const float js = jdot(s, gx, r, s.qas) - s.efc_aref[r];
             const bool eq = (s.efc_src[r] >> 24) == 1;
+            if constexpr (S::WIDE) {
+              if (ell_row(s.efc_src[r])) {
+                if (ell_head(s.efc_src[r])) {  // the cone cost of the whole contact
+                  const int p = ell_pair(s.efc_src[r]);
+                  const float D[3] = {s.efc_D[r], s.efc_D[r + 1], s.efc_D[r + 2]};
+                  float xw[3] = {jw, 0.f, 0.f}, xs[3] = {js, 0.f, 0.f}, f[3], h[6];
+#pragma unroll
+                  for (int k = 1; k < 3; k++) {
+                    xw[k] = jdot(s, gx, r + k, s.qws) - s.efc_aref[r + k];
+                    xs[k] = jdot(s, gx, r + k, s.qas) - s.efc_aref[r + k];
+                  }
+                  cw += 2.f * cone_update(xw, m->pair_cmu[p], m->pair_friction[p], D, f, h);
+                  cs += 2.f * cone_update(xs, m->pair_cmu[p], m->pair_friction[p], D, f, h);
+                }
+                continue;
+              }
+            }
             if (eq || jw < 0.f) cw += s.efc_D[r] * jw * jw;
             if (eq || js < 0.f) cs += s.efc_D[r] * js * js;
           }
@@ -2190,12 +2405,28 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           float cc = 0.f;
           for (int r = lane; r < nefc; r += S::HL) {
             const float jar = jdot(s, gx, r, s.qacc) - s.efc_aref[r];
-            const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
+            bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
+            if constexpr (S::WIDE) act = act && !ell_row(s.efc_src[r]);  // cone pass below
             const float D = s.efc_D[r];
             s.efc_jar[r] = jar;
             s.efc_f[r] = act ? -D * jar : 0.f;
             s.efc_Da[r] = act ? D : 0.f;
             cc += act ? D * jar * jar : 0.f;
+          }
+          if constexpr (S::WIDE) {  // elliptic contacts: cone cost and forces
+            if (m->cone == 1) {
+              sync();
+              for (int r = lane; r < nefc; r += S::HL) {
+                const int src = s.efc_src[r];
+                if (!ell_head(src)) continue;
+                const int p = ell_pair(src);
+                const float x[3] = {s.efc_jar[r], s.efc_jar[r + 1], s.efc_jar[r + 2]};
+                const float D[3] = {s.efc_D[r], s.efc_D[r + 1], s.efc_D[r + 2]};
+                float f[3], h[6];
+                cc += 2.f * cone_update(x, m->pair_cmu[p], m->pair_friction[p], D, f, h);
+                s.efc_f[r] = f[0]; s.efc_f[r + 1] = f[1]; s.efc_f[r + 2] = f[2];
+              }
+            }
           }
           const float gauss = hsum<S::CPW>(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
           const float cost = 0.5f * gauss + 0.5f * hsum<S::CPW>(cc);
@@ -2235,6 +2466,35 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
                 hq[k].z = fmaf(c, v.z, hq[k].z); hq[k].w = fmaf(c, v.w, hq[k].w);
               }
             });
+            if constexpr (S::WIDE) {  // cone Hessian blocks J_c^T H_c J_c (wave-uniform loop)
+              if (m->cone == 1)
+                for (int r = 0; r < nefc; r++) {
+                  const int src = s.efc_src[r];
+                  if (!ell_head(src)) continue;
+                  const int p = ell_pair(src);
+                  const float x[3] = {s.efc_jar[r], s.efc_jar[r + 1], s.efc_jar[r + 2]};
+                  const float D[3] = {s.efc_D[r], s.efc_D[r + 1], s.efc_D[r + 2]};
+                  float f[3], h[6];
+                  cone_update(x, m->pair_cmu[p], m->pair_friction[p], D, f, h);
+                  const float* J0 = jrow_ptr(s, gx, r);
+                  const float* J1 = jrow_ptr(s, gx, r + 1);
+                  const float* J2 = jrow_ptr(s, gx, r + 2);
+                  const float j0 = J0[gi], j1 = J1[gi], j2 = J2[gi];
+                  const float c0 = h[0] * j0 + h[1] * j1 + h[2] * j2;
+                  const float c1 = h[1] * j0 + h[3] * j1 + h[4] * j2;
+                  const float c2 = h[2] * j0 + h[4] * j1 + h[5] * j2;
+#pragma unroll
+                  for (int k = 0; k < QPL; k++) {
+                    const float4 v0 = reinterpret_cast<const float4*>(J0)[gq + RPW * k];
+                    const float4 v1 = reinterpret_cast<const float4*>(J1)[gq + RPW * k];
+                    const float4 v2 = reinterpret_cast<const float4*>(J2)[gq + RPW * k];
+                    hq[k].x += c0 * v0.x + c1 * v1.x + c2 * v2.x;
+                    hq[k].y += c0 * v0.y + c1 * v1.y + c2 * v2.y;
+                    hq[k].z += c0 * v0.z + c1 * v1.z + c2 * v2.z;
+                    hq[k].w += c0 * v0.w + c1 * v1.w + c2 * v2.w;
+                  }
+                }
+            }
 #pragma unroll
             for (int k = 0; k < QPL; k++) reinterpret_cast<float4*>(Hs + gi * S::LD)[gq + RPW * k] = hq[k];
           }
@@ -2272,7 +2532,20 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           qg[2] = 0.5f * hsum<S::CPW>(search * mvv);
           sync();
           LsPt p0 = ls_eval(s, lane, qg, 0.f);
+          const bool ell_ls = S::WIDE && m->cone == 1;
+          if (ell_ls) {
+            const float al[3] = {0.f, 0.f, 0.f};
+            float e[9];
+            ls_cones3(s, m, lane, al, e);
+            ls_add(p0, e[0], e[1], e[2]);
+          }
           LsPt lo = ls_eval(s, lane, qg, p0.alpha - p0.d0 / p0.d1);
+          if (ell_ls) {
+            const float al[3] = {lo.alpha, 0.f, 0.f};
+            float e[9];
+            ls_cones3(s, m, lane, al, e);
+            ls_add(lo, e[0], e[1], e[2]);
+          }
           LsPt hi;
           if (lo.d0 < p0.d0) { hi = p0; } else { hi = lo; lo = p0; }
           bool swap = true;
@@ -2290,6 +2563,14 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             LsPt lo_next, hi_next, mid;
             ls_eval3(s, lane, qg, lo.alpha - lo.d0 / lo.d1, hi.alpha - hi.d0 / hi.d1, 0.5f * (lo.alpha + hi.alpha),
                      lo_next, hi_next, mid);
+            if (ell_ls) {
+              const float al[3] = {lo_next.alpha, hi_next.alpha, mid.alpha};
+              float e[9];
+              ls_cones3(s, m, lane, al, e);
+              ls_add(lo_next, e[0], e[1], e[2]);
+              ls_add(hi_next, e[3], e[4], e[5]);
+              ls_add(mid, e[6], e[7], e[8]);
+            }
             const bool s1 = lo.d0 > 0.f || lo.d0 < lo_next.d0;
             if (s1) lo = lo_next;
             const bool s2 = mid.d0 < 0.f && lo.d0 < mid.d0;
@@ -2325,8 +2606,22 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           const float jar = jdot(s, gx, r, s.qacc) - s.efc_aref[r];
           const bool act = ((s.efc_src[r] >> 24) == 1) || jar < 0.f;
           s.efc_f[r] = act ? -s.efc_D[r] * jar : 0.f;
+          s.efc_jar[r] = jar;
         }
         sync();
+        if (m->cone == 1) {  // elliptic contacts: cone forces at the final qacc
+          for (int r = lane; r < nefc; r += S::HL) {
+            const int src = s.efc_src[r];
+            if (!ell_head(src)) continue;
+            const int p = ell_pair(src);
+            const float x[3] = {s.efc_jar[r], s.efc_jar[r + 1], s.efc_jar[r + 2]};
+            const float D[3] = {s.efc_D[r], s.efc_D[r + 1], s.efc_D[r + 2]};
+            float f[3], h[6];
+            cone_update(x, m->pair_cmu[p], m->pair_friction[p], D, f, h);
+            s.efc_f[r] = f[0]; s.efc_f[r + 1] = f[1]; s.efc_f[r + 2] = f[2];
+          }
+          sync();
+        }
         constexpr int RPW = S::HL / NVW;
         const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
         float qc = 0.f;

@@ -36,6 +36,8 @@ BUNDLES = {
     "dual_arm": "dual_arm.npz",
     "hande_scene": "hande_scene.npz",
 }
+# the scenes with a planner-controlled arm (num_dof = 6); hande_scene has none
+PLANNER_SCENES = ("planner_scene", "ur5e_hande_mjx", "scene_mjx", "dual_arm")
 
 _SCALARS = ("nbody", "njnt", "nq", "nv", "ngeom", "nsite", "npair", "neq", "ncon", "nslot", "nctrl",
             "hande_body", "tcp_site", "iterations", "ls_iterations", "disableflags", "ntree", "timestep",

@@ -48,7 +48,7 @@ def compare(m, g, o, H):
     return rel, graze
 
 
-@pytest.mark.parametrize("name", list(models.BUNDLES))
+@pytest.mark.parametrize("name", models.PLANNER_SCENES)
 @pytest.mark.parametrize("layout", [MPCR_LAYOUT_XI, MPCR_LAYOUT_THETADOT])
 def test_parity_small(torch_cuda, name, layout):
     n, H = 64, 20

@@ -35,7 +35,7 @@ def _start(m):
     return qpos
 
 
-@pytest.mark.parametrize("name", list(models.BUNDLES))
+@pytest.mark.parametrize("name", models.PLANNER_SCENES)
 def test_plant_steps_equal_rollout_bitwise(torch_cuda, name):
     H = 12
     m = models.load(name, 0.05)
@@ -148,3 +148,60 @@ def test_wide_kernel_convex_contacts_match_oracle(torch_cuda, tmp_path, scene):
         plant.step(None)
         o = oracle.step(m, o["qpos"], o["qvel"], o["qacc_warmstart"])
     np.testing.assert_allclose(plant.qpos, o["qpos"], atol=1e-4)
+
+
+# ---------------------------------------------------------------------------
+# scene_robotiq_hande.xml: elliptic cones + impratio, fluid
+# viscosity, a spatial-tendon length limit; wide kernel variant, no controls
+
+
+def _hande_settled(m, steps=300):
+    """The oracle's state after `steps` from qpos0: the gripper resting on
+    the floor (elliptic contacts active), the box hanging on its tendon."""
+    qpos, qvel, ws = m.qpos0[:m.nq].copy(), np.zeros(m.nv), np.zeros(m.nv)
+    for _ in range(steps):
+        o = oracle.step(m, qpos, qvel, ws)
+        qpos, qvel, ws = o["qpos"], o["qvel"], o["qacc_warmstart"]
+    return qpos, qvel, ws
+
+
+def test_plant_hande_scene_matches_oracle_step(torch_cuda):
+    """Per step from the oracle's fp64 state (re-synced every step): qacc,
+    qpos, qvel of the wide kernel vs oracle_step, with the gripper's
+    elliptic-cone floor contacts, the tendon limit row and viscosity live."""
+    m = models.load("hande_scene")
+    plant = Plant(m)
+    qpos, qvel, ws = _hande_settled(m)
+    nefc_seen = []
+    for t in range(30):
+        plant.set_state(qpos=qpos, qvel=qvel, qacc_warmstart=ws)
+        o = oracle.step(m, qpos, qvel, ws)
+        plant.step()
+        nefc_seen.append(o["nefc"])
+        scale = max(1.0, np.abs(o["qacc"]).max())
+        np.testing.assert_allclose(plant.qacc, o["qacc"], atol=2e-3 * scale, rtol=2e-3)
+        qpos, qvel, ws = o["qpos"], o["qvel"], o["qacc_warmstart"]
+        np.testing.assert_allclose(plant.qpos, qpos, atol=1e-5)
+        np.testing.assert_allclose(plant.qvel, qvel, atol=1e-4, rtol=1e-3)
+    # tendon row + at least two 3-row elliptic contacts every step
+    assert min(nefc_seen) >= 1 + 3 * 2, nefc_seen
+
+
+def test_plant_hande_scene_free_running(torch_cuda):
+    """600 free-running GPU steps from qpos0 (1.2 s): the same physical
+    end state as the oracle's (tests/test_hande_scene.py): the box held at
+    the tendon's 2 cm limit, the gripper resting on the floor."""
+    from manipulator_mujoco_amd import mjcf
+    m = models.load("hande_scene")
+    plant = Plant(m)
+    plant.set_state(qpos=m.qpos0[:m.nq], qvel=np.zeros(m.nv), qacc_warmstart=np.zeros(m.nv))
+    for _ in range(600):
+        plant.step()
+    assert np.isfinite(plant.qpos).all()
+    L = mjcf.tendon_jac(m, mjcf.kinematics0(m, plant.qpos), 0)[0]
+    assert 0.02 <= L < 0.0215
+    ob = m.names["body"].index("object")
+    d0 = int(m.body_dofadr[ob])
+    assert np.abs(plant.qvel[d0:d0 + 3]).max() < 0.05
+    assert np.abs(plant.qvel[0:3]).max() < 0.05 and plant.qpos[2] < 0.05
+
