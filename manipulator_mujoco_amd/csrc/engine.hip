@@ -424,6 +424,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.geom_type[i] = m.geom_type[g];
     d.geom_rbound[i] = (float)m.geom_rbound[g];
     d.geom_hulladr[i] = m.geom_hulladr[g];
+    d.geom_hullnum[i] = m.geom_hullnum[g];
     for (int k = 0; k < 3; k++) d.geom_size[i][k] = (float)m.geom_size[g][k];
     if (dmap[b] >= 0) {
       d.geom_body[i] = dmap[b];
@@ -697,6 +698,7 @@ struct Launch {
   float *cost4 = nullptr, *theta = nullptr, *thetadot = nullptr, *trace_eef = nullptr, *trace_slots = nullptr;
   unsigned long long* key = nullptr;
   int* status = nullptr;
+  float* dbg = nullptr;
   bool reset_key = false;
 };
 
@@ -719,6 +721,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.dpar = l.dpar;
   a.state = l.state;
   a.plant = l.plant;
+  a.dbg = l.dbg;
   a.layout = l.layout;
   a.n = l.n;
   a.H = e->H;
@@ -904,6 +907,37 @@ extern "C" int mpcr_plant_step(mpcr_plant* p, const double* qvel_ctrl, int commi
   int rc = launch_rollout(e, l, st);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(st));
+  return MPCR_OK;
+}
+
+// Debug/parity entry (not part of the stable ABI surface): one committed
+// plant step (as mpcr_plant_step) that also copies the step's active
+// contacts, constraint-row parameters, qacc_smooth and final qacc into
+// dbg_host (mpcr_plant_dbg_size() floats; layout DBG_* of rollout.h, the
+// oracle's oracle_step_debug writes the same).
+extern "C" int mpcr_plant_dbg_size(void) { return DBG_N; }
+extern "C" int mpcr_plant_step_debug(mpcr_plant* p, const double* qvel_ctrl, float* dbg_host) {
+  if (!p || !qvel_ctrl || !dbg_host) return fail(MPCR_EINVAL, "bad debug step arguments");
+  mpcr_engine* e = p->e;
+  HIPCHK(hipSetDevice(e->device));
+  const int nc = e->host.nctrl;
+  float v[DX_NCTRL] = {};
+  for (int k = 0; k < nc; k++) v[k] = (float)qvel_ctrl[k];
+  float* d_dbg = nullptr;
+  HIPCHK(hipMalloc(&d_dbg, sizeof(float) * DBG_N));
+  HIPCHK(hipMemset(d_dbg, 0, sizeof(float) * DBG_N));
+  HIPCHK(hipMemcpy(p->d_in, v, sizeof(float) * nc, hipMemcpyHostToDevice));
+  Launch l;
+  l.layout = MPCR_LAYOUT_THETADOT; l.n = 1; l.in = p->d_in; l.cost4 = p->d_cost;
+  l.state = p->d_state; l.plant = 3; l.dbg = d_dbg;
+  const double q0[DX_NCTRL] = {};
+  const float w[3] = {0.f, 0.f, 0.f}, pt[3] = {0.f, 0.f, 0.f}, qt[4] = {1.f, 0.f, 0.f, 0.f};
+  fill_par(l.par, nc, q0, w, pt, qt);
+  int rc = launch_rollout(e, l, 0);
+  if (rc) { (void)hipFree(d_dbg); return rc; }
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(dbg_host, d_dbg, sizeof(float) * DBG_N, hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(d_dbg));
   return MPCR_OK;
 }
 

@@ -109,6 +109,7 @@ struct DevModel {
 
   // convex hulls of mesh geoms (geom frame), hill-climbing graph -----------------
   int geom_hulladr[DX_NG];
+  int geom_hullnum[DX_NG];
   const float4* hull_vert;  // xyz, w unused
   const int2* hull_info;    // (adjacency start, count) per vertex
   const float4* hull_adjv;  // neighbour xyz | neighbour index (bits in w): one load per neighbour

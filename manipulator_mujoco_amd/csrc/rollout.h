@@ -19,6 +19,14 @@ constexpr float kMaxImp = 0.9999f;
 
 // per-call parameter block (RolloutArgs::par / dpar) and plant state layout
 enum { PAR_Q0 = 0, PAR_W = 8, PAR_PT = 12, PAR_QT = 16, PAR_N = 20 };
+// debug dump of candidate 0's last step (the same layout as the oracle's
+// oracle_step_debug): active contacts (pos xyz, dist, pair, normal xyz),
+// constraint rows (D, aref, vel), qacc_smooth, the final qacc
+enum { DBG_NCON = 0, DBG_NEFC = 1, DBG_CON = 2, DBG_MAXCON = 32, DBG_ROW = DBG_CON + 8 * DBG_MAXCON, DBG_MAXROW = 136,
+       DBG_QAS = DBG_ROW + 3 * DBG_MAXROW, DBG_QACC = DBG_QAS + DX_NV, DBG_INFO = DBG_QACC + DX_NV,
+       DBG_GRAD = DBG_INFO + 8, DBG_SRCH = DBG_GRAD + DX_NV, DBG_N = DBG_SRCH + DX_NV };
+// DBG_INFO: warm start taken, its cost, qacc_smooth's cost, first iteration's p0 cost, alpha, line-search
+// passes, the final bracket's best cost, Newton iterations run
 enum { ST_QPOS = 0, ST_QVEL = DX_NQ, ST_QWS = ST_QVEL + DX_NV, ST_QACC = ST_QWS + DX_NV, ST_EEF = ST_QACC + DX_NV,
        ST_N = ST_EEF + 8 };
 
@@ -37,6 +45,7 @@ struct RolloutArgs {
   float* jx;           // n x (MAXEFC - JL) x LDJ: J rows past the LDS ones
   short* hints;        // n x NHINT x 2: hull-climb start per convex pair and side (dual-arm class)
   unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
+  float* dbg;  // parity debugging (mpcr_plant_step_debug): candidate 0's last step, DBG_* layout
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs
   const float* dpar;
@@ -56,12 +65,13 @@ struct RolloutArgs {
 // multiples of 4 for LD = 20 and 36) -> conflict free, 4x fewer LDS
 // instructions than b32.
 template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false,
-          int JL_ = MAXEFC_, int CPW_ = 1>
+          int JL_ = MAXEFC_, int CPW_ = 1, int MAXACT_ = DX_MAXACT>
 struct __align__(16) SmemT {
   static constexpr int NVW = NVW_, NBW = NBW_, NGW = NGW_, LD = NVW_ + 4;
   // candidates per wave: CPW images per workgroup, HL = 64 / CPW lanes each
   static constexpr int CPW = CPW_, HL = WAVE / CPW_;
   static constexpr int MAXEFC = MAXEFC_, LDJ = LDJ_;      // constraint rows kept, J row stride
+  static constexpr int MAXACT = MAXACT_;                  // active contacts kept
   static constexpr int JL = JL_;  // J rows held in LDS; rows JL.. live in the block's HBM slab (RolloutArgs::jx)
   static_assert(JL <= MAXEFC && JL % 4 == 0, "J rows in LDS");
   static constexpr bool CPREV_GLOBAL = CPREV_GLOBAL_;     // previous slot distances in HBM (L2) instead of LDS
@@ -114,11 +124,11 @@ struct __align__(16) SmemT {
       int efc_src[MAXEFC];  // (kind << 24) | (index << 4) | side
       union {
         struct {  // collision .. constraint rows
-          float con_pos[DX_MAXACT][4];
-          float con_frame[DX_MAXACT][12];
-          float con_dist[DX_MAXACT];
-          int con_pair[DX_MAXACT];
-          int con_row[DX_MAXACT];
+          float con_pos[MAXACT][4];
+          float con_frame[MAXACT][12];
+          float con_dist[MAXACT];
+          int con_pair[MAXACT];
+          int con_row[MAXACT];
           float poly[2][8][4];  // box-box clipping polygon (double buffered)
         };
         struct {  // Newton (the contacts are dead once the rows are built)
@@ -168,7 +178,10 @@ static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU
 #ifndef MPCR_W_JL
 #define MPCR_W_JL 40
 #endif
-using SmemW = SmemT<32, 32, 72, DX_MAXEFC, 36, true, MPCR_W_JL>;
+#ifndef MPCR_W_MAXACT
+#define MPCR_W_MAXACT 32
+#endif
+using SmemW = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT>;
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 static_assert(SmemW::JL * SmemW::LDJ >= SmemW::CVXN, "convex-pair list inside the J rows");

@@ -698,6 +698,96 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   return true;
 }
 
+// argmax step with the oracle's relative tie band (oracle beats()): near-ties
+// resolve to the lowest vertex index in both
+__device__ __forceinline__ bool beats(float v, float best) { return v > best + 1e-4f * fabsf(best) + 1e-12f; }
+
+// plane - mesh manifold, MJX's plane_convex (oracle col_plane_mesh): called
+// once the climb found a penetrating vertex (depth > 0).  Candidate set: hull
+// vertices penetrating by more than max(0, depth - 1 mm); a = first, b =
+// farthest from a, c = farthest from line ab, d = farthest from edge bc or ac
+// (bc on ties); repeated picks stay empty.  Passes 2-4 scan [a, last member].
+template <class S>
+__device__ __noinline__ int plane_mesh_manifold(const DevModel* __restrict__ m, const S& s, int g, const float n[3],
+                                                const float* xp, float depth, float dist[4], float pos[4][3],
+                                                float nrm[4][3]) {
+  const float* R = s.gxmat[g];
+  const float* xg = s.gxpos[g];
+  float nl[3], pl[3];
+  mtv(nl, R, n);
+  const float dx[3] = {xp[0] - xg[0], xp[1] - xg[1], xp[2] - xg[2]};
+  mtv(pl, R, dx);
+  const float thr = fmaxf(0.f, depth - 1e-3f);
+  const int v0 = m->geom_hulladr[g], v1 = v0 + m->geom_hullnum[g];
+  const float4* __restrict__ hv = m->hull_vert;
+  auto sup = [&](const float4& v) { return (pl[0] - v.x) * nl[0] + (pl[1] - v.y) * nl[1] + (pl[2] - v.z) * nl[2]; };
+  int ia = -1, il = -1;
+  for (int i = v0; i < v1; i++) {
+    if (sup(hv[i]) > thr) {
+      if (ia < 0) ia = i;
+      il = i;
+    }
+  }
+  if (ia < 0) return 1;  // the climb's vertex alone (threshold rounding)
+  const float4 a = hv[ia];
+  int ib = ia, ic = ia;
+  float best = -1.f;
+  for (int i = ia; i <= il; i++) {
+    const float4 v = hv[i];
+    if (!(sup(v) > thr)) continue;
+    const float e = (a.x - v.x) * (a.x - v.x) + (a.y - v.y) * (a.y - v.y) + (a.z - v.z) * (a.z - v.z);
+    if (beats(e, best)) { best = e; ib = i; }
+  }
+  const float4 b = hv[ib];
+  float ab[3];
+  {
+    const float amb[3] = {a.x - b.x, a.y - b.y, a.z - b.z};
+    cross(ab, nl, amb);
+  }
+  best = -1.f;
+  for (int i = ia; i <= il; i++) {
+    const float4 v = hv[i];
+    if (!(sup(v) > thr)) continue;
+    const float e = fabsf((a.x - v.x) * ab[0] + (a.y - v.y) * ab[1] + (a.z - v.z) * ab[2]);
+    if (beats(e, best)) { best = e; ic = i; }
+  }
+  const float4 c = hv[ic];
+  float ac[3], bc[3];
+  {
+    const float amc[3] = {a.x - c.x, a.y - c.y, a.z - c.z}, bmc[3] = {b.x - c.x, b.y - c.y, b.z - c.z};
+    cross(ac, nl, amc);
+    cross(bc, nl, bmc);
+  }
+  float bbp = -1.f, bap = -1.f;
+  int ibp = ia, iap = ia;
+  for (int i = ia; i <= il; i++) {
+    const float4 v = hv[i];
+    if (!(sup(v) > thr)) continue;
+    const float e1 = fabsf((b.x - v.x) * bc[0] + (b.y - v.y) * bc[1] + (b.z - v.z) * bc[2]);
+    const float e2 = fabsf((a.x - v.x) * ac[0] + (a.y - v.y) * ac[1] + (a.z - v.z) * ac[2]);
+    if (beats(e1, bbp)) { bbp = e1; ibp = i; }
+    if (beats(e2, bap)) { bap = e2; iap = i; }
+  }
+  const int idx[4] = {ia, ib, ic, beats(bap, bbp) ? iap : ibp};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    bool dup = false;
+#pragma unroll
+    for (int t = 0; t < k; t++) dup |= idx[t] == idx[k];
+    dist[k] = 1e30f;
+    if (dup) continue;
+    const float4 v = hv[idx[k]];
+    const float l[3] = {v.x, v.y, v.z};
+    float w[3];
+    mv(w, R, l);
+    const float d = -sup(v);
+    dist[k] = d;
+#pragma unroll
+    for (int e = 0; e < 3; e++) { pos[k][e] = w[e] + xg[e] - 0.5f * d * n[e]; nrm[k][e] = n[e]; }
+  }
+  return 4;
+}
+
 // per-lane narrow phase for plane/capsule/box-vs-capsule pairs (box-box is
 // wave-cooperative, below).  out: dist[4], pos[4][3], nrm[4][3]
 template <class S>
@@ -845,7 +935,7 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
 #pragma unroll
     for (int c = 0; c < 3; c++) pp[c] = a[c] + ts * dd[c];
     float g = point_box(pp, h, nl, q);
-    if (g <= 0) {
+    if (g <= 1e-6f) {  // on or in the box (penetrating segments land on the surface): the oracle's band
       // deepest point of g(t) = max_k |x_k(t)| - h_k over its kinks
       float gbest = 1e30f, tbest = 0.f;
 #pragma unroll
@@ -926,6 +1016,7 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
       dist[0] = d;
 #pragma unroll
       for (int c = 0; c < 3; c++) { pos[0][c] = q[c] - 0.5f * d * n[c]; nrm[0][c] = n[c]; }
+      if (d < 0.f && m->geom_type[g2] == 7) return plane_mesh_manifold(m, s, g2, n, x1, -d, dist, pos, nrm);
       return 1;
     }
   }
@@ -1058,7 +1149,7 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
     }
     float sc, uc;
     seg_seg(pa, da, pb, db, &sc, &uc);
-    if (lane == 0 && base < DX_MAXACT) {
+    if (lane == 0 && base < S::MAXACT) {
       float f[9];
       make_frame(f, n);
 #pragma unroll
@@ -1179,7 +1270,7 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
       if (keep && rank == (d0 + q * nkeep / 4) % nkeep) slot = q;
     npick = 4;
   }
-  if (slot >= 0 && base + slot < DX_MAXACT) {
+  if (slot >= 0 && base + slot < S::MAXACT) {
     const int o = base + slot;
     float f[9];
     make_frame(f, n);
@@ -1234,7 +1325,7 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       if (c < nsl && dist[c] < mg) {
-        if (o < DX_MAXACT) {
+        if (o < S::MAXACT) {
           float f[9];
           make_frame(f, nrm[c]);
           s.con_pos[o][0] = pos[c][0]; s.con_pos[o][1] = pos[c][1]; s.con_pos[o][2] = pos[c][2];
@@ -2088,10 +2179,10 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         }
       }
     }
-    if (s.ncon > DX_MAXACT) {
+    if (s.ncon > S::MAXACT) {
       status |= 1;
       sync();
-      if (lane == 0) s.ncon = DX_MAXACT;
+      if (lane == 0) s.ncon = S::MAXACT;
       sync();
     }
 
@@ -2341,6 +2432,20 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         }
         s.efc_D[r] = 1.f / R;
         s.efc_aref[r] = -B * vel - K * imp * (efric ? 0.f : pos - margin);
+        if (args.dbg && b == 0 && t == H - 1 && r < DBG_MAXROW) {
+          float* o = args.dbg + DBG_ROW + 3 * r;
+          o[0] = s.efc_D[r]; o[1] = s.efc_aref[r]; o[2] = vel;
+        }
+      }
+      if (args.dbg && b == 0 && t == H - 1) {
+        if (lane == 0) { args.dbg[DBG_NCON] = (float)s.ncon; args.dbg[DBG_NEFC] = (float)s.nefc; }
+        if (lane < s.ncon && lane < DBG_MAXCON) {
+          float* o = args.dbg + DBG_CON + 8 * lane;
+          o[0] = s.con_pos[lane][0]; o[1] = s.con_pos[lane][1]; o[2] = s.con_pos[lane][2];
+          o[3] = s.con_dist[lane]; o[4] = (float)s.con_pair[lane];
+          o[5] = s.con_frame[lane][0]; o[6] = s.con_frame[lane][1]; o[7] = s.con_frame[lane][2];
+        }
+        if (lane < NVW) args.dbg[DBG_QAS + lane] = s.qas[lane];
       }
       sync();
     }
@@ -2387,6 +2492,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           const float costw = 0.5f * hsum<S::CPW>(gw) + 0.5f * hsum<S::CPW>(cw);
           const float costs = 0.5f * hsum<S::CPW>(cs);
           if (costw < costs && lane < NVW) qacc_l = s.qws[lane];
+          if (args.dbg && b == 0 && t == H - 1 && lane == 0) {
+            args.dbg[DBG_INFO + 0] = costw < costs ? 1.f : 0.f;
+            args.dbg[DBG_INFO + 1] = costw;
+            args.dbg[DBG_INFO + 2] = costs;
+          }
         }
         if (lane < NVW) s.qacc[lane] = qacc_l;
         sync();
@@ -2518,6 +2628,10 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             mg = chol_solve<NVW, S::LD>(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
           }
           const float search = lane < nv ? -mg : 0.f;
+          if (args.dbg && b == 0 && t == H - 1 && it == 0 && lane < NVW) {
+            args.dbg[DBG_GRAD + lane] = grad;
+            args.dbg[DBG_SRCH + lane] = search;
+          }
           STAMP(14);
           if (lane < NVW) s.srch[lane] = search;
           sync();
@@ -2554,6 +2668,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 #ifdef MPCR_PROFILE
             prof_acc[15] += 1ull << 32;  // line-search passes (high half of the counter)
 #endif
+            if (args.dbg && b == 0 && t == H - 1 && lane == 0 && it == 0) args.dbg[DBG_INFO + 5] = (float)ls;
             if (lo.d0 < 0.f && lo.d0 > -gtol) break;
             if (hi.d0 > 0.f && hi.d0 < gtol) break;
             // bracket closed to fp32 resolution: further passes only move alpha
@@ -2583,6 +2698,12 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           }
           const bool improved = lo.cost < p0.cost || hi.cost < p0.cost;
           const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+          if (args.dbg && b == 0 && t == H - 1 && lane == 0 && it == 0) {
+            args.dbg[DBG_INFO + 3] = p0.cost;
+            args.dbg[DBG_INFO + 4] = alpha;
+            args.dbg[DBG_INFO + 6] = fminf(lo.cost, hi.cost);
+          }
+          if (args.dbg && b == 0 && t == H - 1 && lane == 0) args.dbg[DBG_INFO + 7] = (float)(it + 1);
           if (improved && lane < NVW) s.qacc[lane] = s.qacc[lane] + alpha * s.srch[lane];
           prev_cost = cost;
           sync();
@@ -2593,6 +2714,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       }
     }
 
+    if (args.dbg && b == 0 && t == H - 1 && lane < NVW) args.dbg[DBG_QACC + lane] = s.qacc[lane];
     STAMP(9);
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- implicitfast (dual-arm class): (M + dt D) a = qfrc_smooth + J^T f at

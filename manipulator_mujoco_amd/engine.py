@@ -229,6 +229,18 @@ class Plant:
         check(_lib.load().mpcr_plant_step(self.handle, None if v is None else v.ctypes.data_as(dp), 1, None))
         self._pull()
 
+    def step_debug(self, qvel_ctrl):
+        """step() that also returns the step's active contacts, constraint-row
+        parameters, qacc_smooth and qacc (``parse_step_debug``; parity
+        debugging, mpcr_plant_step_debug)."""
+        lib = _lib.load()
+        buf = np.zeros(lib.mpcr_plant_dbg_size(), dtype=np.float32)
+        v = np.ascontiguousarray(qvel_ctrl, dtype=np.float64).reshape(self.nctrl)
+        check(lib.mpcr_plant_step_debug(self.handle, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                        buf.ctypes.data_as(ctypes.c_void_p)))
+        self._pull()
+        return parse_step_debug(buf, self.nv)
+
     @property
     def site_xpos_tcp(self):
         return self.eef[:3].copy()
@@ -239,3 +251,22 @@ class Plant:
 
 
 __all__ = ["Engine", "Model", "Plant", "MPCR_LAYOUT_XI", "MPCR_LAYOUT_THETADOT"]
+
+
+DBG_CON, DBG_MAXCON, DBG_MAXROW, DBG_NV = 2, 32, 136, 32  # rollout.h DBG_* layout
+
+
+def parse_step_debug(buf, nv):
+    """DBG_* buffer (kernel or oracle_step_debug) -> dict of numpy arrays."""
+    buf = np.asarray(buf, dtype=np.float64)
+    ncon, nefc = int(buf[0]), int(buf[1])
+    con = buf[DBG_CON:DBG_CON + 8 * DBG_MAXCON].reshape(DBG_MAXCON, 8)[:min(ncon, DBG_MAXCON)]
+    r0 = DBG_CON + 8 * DBG_MAXCON
+    rows = buf[r0:r0 + 3 * DBG_MAXROW].reshape(DBG_MAXROW, 3)[:min(nefc, DBG_MAXROW)]
+    q0 = r0 + 3 * DBG_MAXROW
+    return dict(ncon=ncon, nefc=nefc, con_pos=con[:, 0:3], con_dist=con[:, 3], con_pair=con[:, 4].astype(int),
+                con_normal=con[:, 5:8], efc_D=rows[:, 0], efc_aref=rows[:, 1], efc_vel=rows[:, 2],
+                qacc_smooth=buf[q0:q0 + nv], qacc=buf[q0 + DBG_NV:q0 + DBG_NV + nv],
+                info=buf[q0 + 2 * DBG_NV:q0 + 2 * DBG_NV + 8],
+                grad=buf[q0 + 2 * DBG_NV + 8:q0 + 2 * DBG_NV + 8 + nv],
+                search=buf[q0 + 3 * DBG_NV + 8:q0 + 3 * DBG_NV + 8 + nv])

@@ -124,11 +124,12 @@ CONVEX_TYPES = (2, 3, 5, 6, 7)  # sphere, capsule, cylinder, box, mesh (convex h
 def collision_func(t1, t2):
     """(func, contact slots) of a pair with t1 <= t2: the dedicated primitive
     functions, else the general convex one (one contact, MuJoCo's own
-    general-convex path also yields one)."""
+    general-convex path also yields one).  Plane - mesh owns 4 slots: MJX's
+    plane_convex manifold (oracle col_plane_mesh)."""
     if (t1, t2) in COLLISION_FUNC:
         return COLLISION_FUNC[(t1, t2)]
     if t1 == 0 and t2 in CONVEX_TYPES:
-        return (cmodel.COL_PLANE_CONVEX, 1)
+        return (cmodel.COL_PLANE_CONVEX, 4 if t2 == 7 else 1)
     if t1 in CONVEX_TYPES and t2 in CONVEX_TYPES:
         return (cmodel.COL_CONVEX, 1)
     return None

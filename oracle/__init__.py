@@ -37,7 +37,8 @@ def lib():
         _LIB = ctypes.CDLL(build())
         dp = ctypes.POINTER(ctypes.c_double)
         _LIB.oracle_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, dp,
-                                        dp, dp, dp]
+                                        dp, dp, dp, ctypes.POINTER(ctypes.c_int), ctypes.c_double,
+                                        ctypes.c_uint, ctypes.c_int]
         _LIB.oracle_rollout.restype = ctypes.c_int
         _LIB.oracle_step.argtypes = [ctypes.c_void_p, dp, dp, dp, dp, dp, dp, dp, dp, dp,
                                      ctypes.POINTER(ctypes.c_int)]
@@ -54,8 +55,13 @@ def _p(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
-def rollout(model, thetadot, q0, w, ptgt, qtgt, want_theta=True, want_slots=False, want_eef=False):
-    """fp64 oracle rollout; thetadot is (n, nctrl*H) joint-major."""
+def rollout(model, thetadot, q0, w, ptgt, qtgt, want_theta=True, want_slots=False, want_eef=False, workers=None,
+            noise=0.0, seed=0):
+    """fp64 oracle rollout; thetadot is (n, nctrl*H) joint-major.  workers > 1
+    splits the candidates over that many threads (test checker only).
+    noise > 0: after every step qpos / qvel / warm start are scaled by
+    (1 + noise * u), u uniform in [-1, 1) keyed by (seed, candidate, step) --
+    the conditioning probe of tests/parity_util.py."""
     s = model.to_struct()
     td = np.ascontiguousarray(thetadot, dtype=np.float64)
     n = td.shape[0]
@@ -65,20 +71,74 @@ def rollout(model, thetadot, q0, w, ptgt, qtgt, want_theta=True, want_slots=Fals
     theta = np.zeros((n, nc * H)) if want_theta else None
     slots = np.zeros((n, H, max(model.nslot, 1))) if want_slots else None
     eef = np.zeros((n, H, 7)) if want_eef else None
+    info = np.zeros((n, 2), dtype=np.int32)
     q0 = np.ascontiguousarray(q0, dtype=np.float64)
     w = np.ascontiguousarray(w, dtype=np.float64)
     pt = np.ascontiguousarray(ptgt, dtype=np.float64)
     qt = np.ascontiguousarray(qtgt, dtype=np.float64)
-    st = lib().oracle_rollout(ctypes.byref(s), n, H, _p(td), _p(q0), _p(w), _p(pt), _p(qt), _p(cost4),
-                              _p(theta), _p(slots), _p(eef))
+    L = lib()
+
+    def run(a, b):  # rows [a, b); ctypes drops the GIL, the C side allocates per call
+        def sub(x):
+            return None if x is None else x[a:b]
+        return L.oracle_rollout(ctypes.byref(s), b - a, H, _p(td[a:b]), _p(q0), _p(w), _p(pt), _p(qt),
+                                _p(cost4[a:b]), _p(sub(theta)), _p(sub(slots)), _p(sub(eef)),
+                                info[a:b].ctypes.data_as(ctypes.POINTER(ctypes.c_int)), float(noise), int(seed), int(a))
+
+    nw = max(1, min(workers or 1, n // 16))
+    if nw == 1:
+        st = run(0, n)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        cuts = np.linspace(0, n, nw + 1).astype(int)
+        with ThreadPoolExecutor(nw) as ex:
+            sts = list(ex.map(lambda i: run(cuts[i], cuts[i + 1]), range(nw)))
+        st = min(sts) if min(sts) < 0 else max(sts)
     if st < 0:
         raise RuntimeError(f"oracle_rollout failed ({st})")
-    out = dict(cost4=cost4, theta=theta, status=st)
+    # maxrows / maxcon: the busiest step's constraint rows / active contacts
+    out = dict(cost4=cost4, theta=theta, status=st, maxrows=info[:, 0], maxcon=info[:, 1])
     if want_slots:
         out["slots"] = slots[:, :, :model.nslot]
     if want_eef:
         out["eef"] = eef
     return out
+
+
+class Runner:
+    """Cost-only rollouts on a fixed thread pool over one prepared model
+    struct -- what bench.py's cpu_baseline times: the pool is started and the
+    model converted before the clock, each call is only the C rollouts
+    (ctypes drops the GIL, so the threads run the C code concurrently)."""
+
+    def __init__(self, model, workers, q0, w, ptgt, qtgt):
+        from concurrent.futures import ThreadPoolExecutor
+        self.model, self.workers = model, max(1, int(workers))
+        self.s = model.to_struct()
+        self.L = lib()
+        self.args = [np.ascontiguousarray(x, dtype=np.float64) for x in (q0, w, ptgt, qtgt)]
+        self.ex = ThreadPoolExecutor(self.workers)
+        list(self.ex.map(lambda i: i, range(self.workers)))  # start every thread now
+
+    def rollout(self, td):
+        td = np.ascontiguousarray(td, dtype=np.float64)
+        n, H = td.shape[0], td.shape[1] // self.model.nctrl
+        cost4 = np.zeros((n, 4))
+        cuts = np.linspace(0, n, min(self.workers, n) + 1).astype(int)
+        q0, w, pt, qt = self.args
+
+        def run(i):
+            a, b = cuts[i], cuts[i + 1]
+            return self.L.oracle_rollout(ctypes.byref(self.s), int(b - a), H, _p(td[a:b]), _p(q0), _p(w), _p(pt),
+                                         _p(qt), _p(cost4[a:b]), None, None, None, None, 0.0, 0, 0)
+
+        st = list(self.ex.map(run, range(len(cuts) - 1)))
+        if min(st) < 0:
+            raise RuntimeError(f"oracle_rollout failed ({min(st)})")
+        return cost4
+
+    def close(self):
+        self.ex.shutdown()
 
 
 def cone_eval(mu, fri, D, jar, jv, alpha):
@@ -89,6 +149,17 @@ def cone_eval(mu, fri, D, jar, jv, alpha):
     a = [np.ascontiguousarray(x, dtype=np.float64) for x in (fri, D, jar, jv)]
     lib().oracle_cone_eval(float(mu), *(_p(x) for x in a), float(alpha), ctypes.byref(c), _p(f), _p(H), _p(line))
     return c.value, f, H.reshape(3, 3), line
+
+
+def step_debug(model, qpos, qvel, qacc_ws):
+    """The step's active contacts / rows / qacc_smooth / qacc in the kernel's
+    debug layout (engine.parse_step_debug)."""
+    from manipulator_mujoco_amd.engine import parse_step_debug
+    s = model.to_struct()
+    out = np.zeros(802)
+    a = [np.ascontiguousarray(x, dtype=np.float64) for x in (qpos, qvel, qacc_ws)]
+    lib().oracle_step_debug(ctypes.byref(s), *(_p(x) for x in a), _p(out))
+    return parse_step_debug(out, model.nv)
 
 
 def step(model, qpos, qvel, qacc_ws):

@@ -84,6 +84,9 @@ typedef struct {
   double efc_solref[MAXEFC][2], efc_solimp[MAXEFC][5];
   int efc_trunc; /* constraint rows dropped for capacity (should stay 0) */
   int hint[MPCR_MAX_PAIR][2]; /* hull-climb start per pair and side (-1: none), kept across steps */
+  double dbg[8]; /* solver record of the step (oracle_step_debug, the kernel's DBG_INFO) */
+  double dbg_gs[64]; /* first Newton iteration's gradient | search direction */
+  double* ls_dump; /* non-null: the first line search's inputs (oracle_ls_inputs) */
 } odata;
 
 static void reset_hints(odata* d) {
@@ -721,7 +724,11 @@ static void col_capsule_box(const odata* d, int gc, int gb, const double* sc, co
   double p[3], q[3], nl[3];
   for (int k = 0; k < 3; k++) p[k] = a[k] + ts * dd[k];
   double g = point_box(p, h, nl, q);
-  if (g <= 0) {
+  /* a penetrating segment makes the minimiser above land on the box surface
+     (the entry of f's zero interval), g = 0 up to rounding: anything within
+     1 um of the surface takes the deepest-point path, so fp32 and fp64 agree
+     on the branch (the kernel uses the same band) */
+  if (g <= 1e-6) {
     /* segment reaches the box: deepest point of the convex, piecewise linear
        g(t) = max_k(|x_k(t)| - h_k) over its kinks */
     double cand[17];
@@ -1133,7 +1140,109 @@ static void col_convex(const mpcr_model_t* m, odata* d, int pair, int g1, int g2
   set_contact(out, -depth, pos, n);
 }
 
+/* argmax with a relative tie band: a later candidate replaces the best only
+   if it beats it by more than 1e-4 of its magnitude, so near-ties (symmetric
+   hulls, fp32 vs fp64 rounding) resolve to the lowest vertex index in the
+   oracle and the kernel alike */
+static int beats(double v, double best) { return v > best + 1e-4 * fabs(best) + 1e-12; }
+
+/* plane - mesh: MJX's plane_convex manifold (mujoco-mjx 3.3.1,
+   mjx/_src/collision_convex.py plane_convex + _manifold_points; MJX is the
+   reference's rollout engine, SBP/mjx_planner.py:108,256).  Hull vertices
+   that penetrate the plane and lie within 1 mm of the deepest one form the
+   candidate set; of those: a = the first, b = the farthest from a, c = the
+   farthest from the line ab (in the plane), d = the farthest from the edges
+   bc / ac.  Repeated picks are inactive (dist 1 in MJX, 1e30 here); every
+   contact carries the plane normal and sits half-way through the
+   penetration.  No penetrating vertex: slot 0 reports the deepest vertex's
+   (non-negative) distance, slots 1-3 stay empty -- the restatement for
+   margin 0 (the only margin the reference scenes use) */
+static void col_plane_mesh(const mpcr_model_t* m, odata* d, int pair, int gp, int g, ocontact* out) {
+  const double* R = d->geom_xmat[g];
+  const double* Rp = d->geom_xmat[gp];
+  double n[3] = {Rp[2], Rp[5], Rp[8]}, nn[3] = {-Rp[2], -Rp[5], -Rp[8]}, q[3], pos[3];
+  support(m, d, g, nn, q, &d->hint[pair][1]);
+  double dist0 = (q[0] - d->geom_xpos[gp][0]) * n[0] + (q[1] - d->geom_xpos[gp][1]) * n[1] +
+                 (q[2] - d->geom_xpos[gp][2]) * n[2];
+  if (dist0 >= 0) {
+    for (int k = 0; k < 3; k++) pos[k] = q[k] - 0.5 * dist0 * n[k];
+    set_contact(out, dist0, pos, n);
+    return;
+  }
+  /* convex frame: nl = R^T n, plane point pl = R^T (x_plane - x_geom) */
+  double nl[3], dx[3], pl[3];
+  mulmtv(nl, R, n);
+  for (int k = 0; k < 3; k++) dx[k] = d->geom_xpos[gp][k] - d->geom_xpos[g][k];
+  mulmtv(pl, R, dx);
+  const int v0 = m->geom_hulladr[g], nvh = m->geom_hullnum[g];
+  const double thr = fmax(0.0, -dist0 - 1e-3);
+#define SUP(i) ((pl[0] - m->hull_vert[i][0]) * nl[0] + (pl[1] - m->hull_vert[i][1]) * nl[1] + \
+                (pl[2] - m->hull_vert[i][2]) * nl[2])
+  int ia = -1, ilast = -1;
+  for (int i = v0; i < v0 + nvh; i++)
+    if (SUP(i) > thr) {
+      if (ia < 0) ia = i;
+      ilast = i;
+    }
+  if (ia < 0) { /* the climb's vertex is the only one (thr rounding) */
+    for (int k = 0; k < 3; k++) pos[k] = q[k] - 0.5 * dist0 * n[k];
+    set_contact(out, dist0, pos, n);
+    return;
+  }
+  const double* a = m->hull_vert[ia];
+  int ib = ia, ic = ia, id = ia;
+  double best = -1;
+  for (int i = ia; i <= ilast; i++) {
+    if (!(SUP(i) > thr)) continue;
+    const double* v = m->hull_vert[i];
+    double e = (a[0] - v[0]) * (a[0] - v[0]) + (a[1] - v[1]) * (a[1] - v[1]) + (a[2] - v[2]) * (a[2] - v[2]);
+    if (beats(e, best)) { best = e; ib = i; }
+  }
+  const double* b = m->hull_vert[ib];
+  double amb[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]}, ab[3];
+  cross3(ab, nl, amb);
+  best = -1;
+  for (int i = ia; i <= ilast; i++) {
+    if (!(SUP(i) > thr)) continue;
+    const double* v = m->hull_vert[i];
+    double e = fabs((a[0] - v[0]) * ab[0] + (a[1] - v[1]) * ab[1] + (a[2] - v[2]) * ab[2]);
+    if (beats(e, best)) { best = e; ic = i; }
+  }
+  const double* c = m->hull_vert[ic];
+  double amc[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]}, bmc[3] = {b[0] - c[0], b[1] - c[1], b[2] - c[2]};
+  double ac[3], bc[3];
+  cross3(ac, nl, amc);
+  cross3(bc, nl, bmc);
+  /* MJX takes the argmax of concat(dist_bp, dist_ap): the bc edge wins ties */
+  double bbp = -1, bap = -1;
+  int ibp = ia, iap = ia;
+  for (int i = ia; i <= ilast; i++) {
+    if (!(SUP(i) > thr)) continue;
+    const double* v = m->hull_vert[i];
+    double e1 = fabs((b[0] - v[0]) * bc[0] + (b[1] - v[1]) * bc[1] + (b[2] - v[2]) * bc[2]);
+    double e2 = fabs((a[0] - v[0]) * ac[0] + (a[1] - v[1]) * ac[1] + (a[2] - v[2]) * ac[2]);
+    if (beats(e1, bbp)) { bbp = e1; ibp = i; }
+    if (beats(e2, bap)) { bap = e2; iap = i; }
+  }
+  id = beats(bap, bbp) ? iap : ibp;
+  const int idx[4] = {ia, ib, ic, id};
+  for (int s = 0; s < 4; s++) {
+    int dup = 0;
+    for (int t = 0; t < s; t++) dup |= idx[t] == idx[s];
+    if (dup) continue;
+    double w[3], dist = -SUP(idx[s]);
+    mulmv(w, R, m->hull_vert[idx[s]]);
+    for (int k = 0; k < 3; k++) pos[k] = w[k] + d->geom_xpos[g][k] - 0.5 * dist * n[k];
+    set_contact(&out[s], dist, pos, n);
+  }
+#undef SUP
+}
+
 static void col_plane_convex(const mpcr_model_t* m, odata* d, int pair, int gp, int g, ocontact* out) {
+  if (m->geom_type[g] == MPCR_GEOM_MESH) {
+    col_plane_mesh(m, d, pair, gp, g, out);
+    return;
+  }
   const double* R = d->geom_xmat[gp];
   double n[3] = {R[2], R[5], R[8]}, nn[3] = {-R[2], -R[5], -R[8]}, p[3], pos[3];
   support(m, d, g, nn, p, &d->hint[pair][1]);
@@ -1548,6 +1657,9 @@ static void solve(const mpcr_model_t* m, odata* d) {
     eval_jar(m, d, d->qacc_smooth, js);
     double cw = solver_cost(m, d, d->qacc_warmstart, Mw, jw), cs = solver_cost(m, d, d->qacc_smooth, Ms, js);
     memcpy(qacc, cw < cs ? d->qacc_warmstart : d->qacc_smooth, sizeof(double) * nv);
+    d->dbg[0] = cw < cs;
+    d->dbg[1] = cw;
+    d->dbg[2] = cs;
   } else {
     memcpy(qacc, d->qacc_smooth, sizeof(double) * nv);
   }
@@ -1589,9 +1701,14 @@ static void solve(const mpcr_model_t* m, odata* d) {
           H[i][j] += h;
         }
     }
+    if (d->ls_dump && it == 0)
+      for (int i = 0; i < nv; i++)
+        for (int j = 0; j < nv; j++) d->ls_dump[8 + 4 * 512 + i * nv + j] = H[i][j];
     chol(Lh, H, nv);
     chol_solve(Mgrad, Lh, grad, nv);
     for (int i = 0; i < nv; i++) search[i] = -Mgrad[i];
+    if (it == 0)
+      for (int i = 0; i < nv; i++) { d->dbg_gs[i] = grad[i]; d->dbg_gs[32 + i] = search[i]; }
     /* line search (MJX-style bracketing on the piecewise quadratic) */
     double Mv[NV], jv[MAXEFC], sn = 0;
     mulM(m, d, search, Mv);
@@ -1609,6 +1726,14 @@ static void solve(const mpcr_model_t* m, odata* d) {
       q2 += search[i] * Mv[i];
     }
     double qg[3] = {0.5 * gauss, q1, 0.5 * q2};
+    if (d->ls_dump && it == 0) {
+      d->ls_dump[0] = nefc; d->ls_dump[1] = qg[0]; d->ls_dump[2] = qg[1]; d->ls_dump[3] = qg[2];
+      d->ls_dump[4] = gtol;
+      for (int r = 0; r < nefc && r < 512; r++) {
+        double* o = d->ls_dump + 8 + 4 * r;
+        o[0] = jar[r]; o[1] = jv[r]; o[2] = d->efc_D[r]; o[3] = d->efc_eq[r];
+      }
+    }
     lspt p0 = ls_eval(d, qg, jar, jv, 0.0);
     lspt lo = ls_eval(d, qg, jar, jv, p0.alpha - p0.d0 / p0.d1);
     lspt hi;
@@ -1616,6 +1741,7 @@ static void solve(const mpcr_model_t* m, odata* d) {
     int swap = 1;
     for (int ls = 0; ls < m->ls_iterations; ls++) {
       if (!swap) break;
+      if (it == 0) d->dbg[5] = ls;
       if (lo.d0 < 0 && lo.d0 > -gtol) break;
       if (hi.d0 > 0 && hi.d0 < gtol) break;
       lspt lo_next = ls_eval(d, qg, jar, jv, lo.alpha - lo.d0 / lo.d1);
@@ -1633,6 +1759,8 @@ static void solve(const mpcr_model_t* m, odata* d) {
     }
     int improved = lo.cost < p0.cost || hi.cost < p0.cost;
     double alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+    if (it == 0) { d->dbg[3] = p0.cost; d->dbg[4] = alpha; d->dbg[6] = fmin(lo.cost, hi.cost); }
+    d->dbg[7] = it + 1;
     if (improved) {
       for (int i = 0; i < nv; i++) { qacc[i] += alpha * search[i]; Ma[i] += alpha * Mv[i]; }
       for (int r = 0; r < nefc; r++) jar[r] += alpha * jv[r];
@@ -1748,6 +1876,74 @@ int oracle_step(const mpcr_model_t* m, double* qpos, double* qvel, double* qacc_
   return trunc ? 1 : 0;
 }
 
+/* uniform in [-1, 1) from (seed, candidate, step, index): splitmix64 */
+static double hash_unit(unsigned seed, int b, int t, int i) {
+  uint64_t z = ((uint64_t)seed << 40) ^ ((uint64_t)(unsigned)b << 20) ^ ((uint64_t)(unsigned)t << 8) ^ (uint64_t)i;
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
+/* parity debugging: one step like oracle_step, dumping the active contacts,
+   the constraint rows, qacc_smooth and qacc in the kernel's DBG_* layout
+   (manipulator_mujoco_amd/csrc/rollout.h; 730 doubles) */
+int oracle_step_debug(const mpcr_model_t* m, const double* qpos, const double* qvel, const double* qacc_ws,
+                      double* out) {
+  odata* d = (odata*)calloc(1, sizeof(odata));
+  if (!d) return -1;
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  memcpy(d->qvel, qvel, sizeof(double) * m->nv);
+  memcpy(d->qacc_warmstart, qacc_ws, sizeof(double) * m->nv);
+  reset_hints(d);
+  forward(m, d);
+  memset(out, 0, sizeof(double) * 802);
+  memcpy(out + 730, d->dbg, sizeof(d->dbg));
+  memcpy(out + 738, d->dbg_gs, sizeof(d->dbg_gs));
+  int na = 0;
+  for (int c = 0; c < d->ncon; c++) {
+    const ocontact* k = &d->con[c];
+    if (!k->active) continue;
+    if (na < 32) {
+      double* o = out + 2 + 8 * na;
+      memcpy(o, k->pos, 3 * sizeof(double));
+      o[3] = k->dist; o[4] = k->pair;
+      o[5] = k->frame[0]; o[6] = k->frame[1]; o[7] = k->frame[2];
+    }
+    na++;
+  }
+  out[0] = na;
+  out[1] = d->nefc;
+  for (int r = 0; r < d->nefc && r < 136; r++) {
+    out[258 + 3 * r] = d->efc_D[r];
+    out[258 + 3 * r + 1] = d->efc_aref[r];
+    out[258 + 3 * r + 2] = d->efc_vel[r];
+  }
+  memcpy(out + 666, d->qacc_smooth, sizeof(double) * m->nv);
+  memcpy(out + 698, d->qacc, sizeof(double) * m->nv);
+  free(d);
+  return 0;
+}
+
+/* parity debugging: the inputs of the step's first Newton line search:
+   out[0] nefc, out[1..3] the Gauss quadratic (q0, q1, q2), out[4] gtol,
+   out[8 + 4 r ..] (jar, jv, D, efc_eq) per row, then the Newton Hessian nv x nv
+   (8 + 4 * 512 + 32 * 32 doubles) */
+int oracle_ls_inputs(const mpcr_model_t* m, const double* qpos, const double* qvel, const double* qacc_ws,
+                     double* out) {
+  odata* d = (odata*)calloc(1, sizeof(odata));
+  if (!d) return -1;
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  memcpy(d->qvel, qvel, sizeof(double) * m->nv);
+  memcpy(d->qacc_warmstart, qacc_ws, sizeof(double) * m->nv);
+  reset_hints(d);
+  d->ls_dump = out;
+  forward(m, d);
+  free(d);
+  return 0;
+}
+
 /* Rollout + cost for n candidates (compute_rollout_single +
    compute_cost_single, SBP/mjx_planner.py:265-303).
      thetadot : n x (nctrl*H), joint-major (A_thetadot @ xi, :348)
@@ -1760,7 +1956,8 @@ int oracle_step(const mpcr_model_t* m, double* qpos, double* qvel, double* qacc_
      eef      : n x H x 7 (tcp pos, hande quat) (nullable)              */
 int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, const double* q0,
                    const double* w, const double* ptgt, const double* qtgt, double* cost4, double* theta,
-                   double* slots, double* eef) {
+                   double* slots, double* eef, int* info, double noise, unsigned seed,
+                   int index_base) {
   if (m->magic != MPCR_MODEL_MAGIC || m->nbytes != sizeof(mpcr_model_t)) return -2;
   odata* d = (odata*)calloc(1, sizeof(odata));
   double* cprev = (double*)calloc(m->nslot > 0 ? m->nslot : 1, sizeof(double));
@@ -1777,11 +1974,18 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
     memcpy(d->qvel, m->qvel_init, sizeof(double) * m->nv);
     for (int j = 0; j < nc; j++) d->qpos[m->ctrl_qposadr[j]] = q0[j];
     double cg = 0, cr = 0, cc = 0;
+    int maxrows = 0, maxact = 0;
     const double* td = thetadot + (size_t)b * nc * H;
     for (int t = 0; t < H; t++) {
       for (int j = 0; j < nc; j++) d->qvel[m->ctrl_dofadr[j]] = td[j * H + t];
       forward(m, d);
       if (d->efc_trunc) status = 1;
+      if (d->nefc > maxrows) maxrows = d->nefc;
+      {
+        int na = 0;
+        for (int c = 0; c < m->ncon; c++) na += d->con[c].active;
+        if (na > maxact) maxact = na;
+      }
       /* eef pose and collision distances: pre-integration (from forward) */
       const double* p = m->tcp_site >= 0 ? d->site_xpos[m->tcp_site] : d->xpos[0];
       const double* q = m->hande_body >= 0 ? d->xquat[m->hande_body] : d->xquat[0];
@@ -1810,6 +2014,13 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
         }
       }
       euler(m, d);
+      if (noise > 0) { /* conditioning probe: per-step relative state noise (tests/parity_util.py) */
+        for (int i = 0; i < m->nq; i++) d->qpos[i] *= 1 + noise * hash_unit(seed, index_base + b, t, i);
+        for (int i = 0; i < m->nv; i++) {
+          d->qvel[i] *= 1 + noise * hash_unit(seed, index_base + b, t, 64 + i);
+          d->qacc_warmstart[i] *= 1 + noise * hash_unit(seed, index_base + b, t, 128 + i);
+        }
+      }
       if (theta)
         for (int j = 0; j < nc; j++) theta[(size_t)b * nc * H + j * H + t] = d->qpos[m->ctrl_qposadr[j]];
     }
@@ -1817,6 +2028,7 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
     cost4[4 * b + 1] = cg;
     cost4[4 * b + 2] = cr;
     cost4[4 * b + 3] = cc;
+    if (info) { info[2 * b] = maxrows; info[2 * b + 1] = maxact; }
   }
   free(cprev);
   free(d);

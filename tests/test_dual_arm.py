@@ -201,3 +201,40 @@ def test_actuator_force_and_joint_clamps(tmp_path):
     for q, expect in ((0.0, 1.0), (0.05, -1.5), (0.2, -3.0), (-0.2, 3.0)):  # ctrl 0: f = 1 - 50 q
         r = oracle.step(m, np.array([q]), np.zeros(1), np.zeros(1))
         np.testing.assert_allclose(r["qacc"], [expect], rtol=1e-12, atol=1e-12)
+
+
+def test_ctrl_zero_servos_pull_arm1_home(dual):
+    """The C5 closed loop's drift (profiles/r01_c4_c5.json: eef_dist grows) is
+    the reference's own semantics, not a plant error.  The dual-arm MJCF gives
+    arm 1 position servos (URD/ur5e_1_robotiq_hande.xml:10,169-174: gain 2000,
+    bias 0 -2000 -400) and the planner never writes ctrl, so MjData's default
+    ctrl = 0 holds (SBP/mjx_planner.py:102-107; the keyframe at
+    URD/dual_arm_gripper_scene.xml:30 is ctrl 0 too).  Each step the override
+    qvel[:6] = thetadot (SBP/mjx_planner.py:254) meets the servo's implicit
+    damping (implicitfast) and its position term: most of the commanded
+    velocity is absorbed and the joints creep toward q = 0 whatever the plan.
+    Without the actuators the commanded velocity passes through."""
+    m = dual
+    qa, da = np.asarray(m.ctrl_qposadr[:6]), np.asarray(m.ctrl_dofadr[:6])
+    q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
+    cmd = np.array([0.5, 0, 0, 0, 0, 0])
+
+    def run(model, steps=5):
+        qpos = np.array(model.qpos_init[:model.nq])
+        qpos[qa] = q0
+        qvel, ws = np.zeros(model.nv), np.zeros(model.nv)
+        for _ in range(steps):
+            qv = qvel.copy()
+            qv[da] = cmd
+            o = oracle.step(model, qpos, qv, ws)
+            qpos, qvel, ws = o["qpos"], o["qvel"], o["qacc_warmstart"]
+        return qpos[qa], qvel[da]
+
+    q, v = run(m)
+    assert v[0] < 0.4 * cmd[0]  # the commanded joint keeps < 40 % of its velocity
+    moved = q[1:5] - q0[1:5]
+    assert (np.sign(moved) == -np.sign(q0[1:5])).all() and (np.abs(moved) > 0.05).all()  # toward 0
+    free = models.load("dual_arm", 0.05)
+    free.nu = 0
+    q, v = run(free)
+    assert v[0] > 0.8 * cmd[0]  # (the other joints then sag under gravity: no gravcomp here)

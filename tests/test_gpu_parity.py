@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 import oracle
+import parity_util as pu
 from manipulator_mujoco_amd import basis, models
 from manipulator_mujoco_amd.engine import MPCR_LAYOUT_THETADOT, MPCR_LAYOUT_XI, Engine
 
@@ -14,7 +15,7 @@ Q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
 W = np.array([20.0, 3.0, 80.0])
 PT = np.array([-0.3, -0.3, 0.5])
 QT = np.array([0.0, 1.0, 0.0, 0.0])
-TOL = 1e-4  # north star: costs within 1e-4 relative fp32
+TOL = pu.TOL  # north star: costs within 1e-4 relative fp32
 
 
 @pytest.fixture(scope="module")
@@ -76,9 +77,16 @@ def test_parity_small(torch_cuda, name, layout):
         assert np.abs(g["slots"] - o["slots"]).max() < 1e-3
 
 
+def _td(Pd, xi_h, H):
+    n = xi_h.shape[0]
+    return np.einsum("tk,njk->njt", Pd, xi_h.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
+
+
 @pytest.mark.parametrize("name", ["planner_scene", "scene_mjx", "ur5e_hande_mjx"])
 def test_parity_projected_h50(torch_cuda, name):
-    """Realistic samples (projected to |thetadot| <= 0.8): arm/table/box contacts occur."""
+    """Realistic samples (projected to |thetadot| <= 0.8): arm/table/box
+    contacts occur.  Bar: tests/parity_util.py (per-candidate conditioning,
+    no allowance on well-conditioned candidates, the selection)."""
     torch = torch_cuda
     n, H = 256, 50
     m = models.load(name, 0.05)
@@ -87,14 +95,64 @@ def test_parity_projected_h50(torch_cuda, name):
     xi_h = xi.cpu().numpy()
     e = Engine(m, H, n, Pd)
     g = e.trace(xi_h, MPCR_LAYOUT_XI, Q0, W, PT, QT)
-    td = np.einsum("tk,njk->njt", Pd, xi_h.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
-    o = oracle.rollout(m, td, Q0, W, PT, QT, want_slots=True, want_eef=True)
-    rel, graze = compare(m, g, o, H)
-    ok = rel[~graze] < TOL
-    assert ok.mean() >= 0.98, (ok.mean(), np.sort(rel)[-5:])
-    assert np.median(rel) < 1e-5
-    # the selected candidate agrees
-    assert int(np.argmin(g["cost4"][:, 0])) == int(np.argmin(o["cost4"][:, 0]))
+    o, sens = pu.conditioning(m, _td(Pd, xi_h, H))
+    st = pu.check(m, g["cost4"][:, 0], o, sens, name)
+    assert st["median_rel"] < 1e-5 and st["well"] >= 0.5 * n, st
+
+
+def test_parity_c2_full(torch_cuda):
+    """C2 at its BASELINE size (ur5e_1_robotiq_hande_mjx.xml, 1024 x 50): every
+    candidate against the oracle, the selection.  SURVEY §8d asks whether any
+    contact activates on C2 ("no contacts"): it does -- the model has no
+    gravcomp, the arm sags and the hand / wrist capsules (robot_5..9) reach
+    the table (table_geom_1) after ~1.2 s in almost every candidate; the
+    count is printed and the masked-slot distances must agree with the
+    oracle's sign where they are not grazing."""
+    torch = torch_cuda
+    n, H = 1024, 50
+    m = models.load("ur5e_hande_mjx", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 2, torch.device("cuda:0"))
+    xi_h = xi.cpu().numpy()
+    e = Engine(m, H, n, Pd)
+    g = e.trace(xi_h, MPCR_LAYOUT_XI, Q0, W, PT, QT)
+    o, sens = pu.conditioning(m, _td(Pd, xi_h, H))
+    st = pu.check(m, g["cost4"][:, 0], o, sens, "C2")
+    act_g = (g["slots"] < 0).any(axis=(1, 2))
+    act_o = (o["slots"] < 0).any(axis=(1, 2))
+    print(f"C2 contacts: {int(act_g.sum())}/{n} candidates with an active robot contact (oracle {int(act_o.sum())}); {st}")
+    keep = ~pu.grazing(m, o) & (sens < pu.TOL / 10)
+    assert (act_g[keep] == act_o[keep]).all()
+
+
+def test_parity_c3_full(torch_cuda):
+    """C3 at the BASELINE size (scene_mjx, 4096 x 50), the bench workload:
+    all 4096 candidates against the oracle, the selection.  Includes the
+    candidates whose busiest step needs more constraint rows than the LDS
+    keeps (J rows >= 36 live in the per-candidate HBM slab): they are held
+    to the same bar and counted."""
+    torch = torch_cuda
+    n, H = 4096, 50
+    m = models.load("scene_mjx", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 3, torch.device("cuda:0"))
+    xi_h = xi.cpu().numpy()
+    e = Engine(m, H, n, Pd)
+    st_ = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    key = torch.empty(1, dtype=torch.int64, device="cuda:0")
+    a = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, best_key=key, status=st_).cpu().numpy()
+    o, sens = pu.conditioning(m, _td(Pd, xi_h, H))
+    stats = pu.check(m, a[:, 0], o, sens, "C3")
+    from manipulator_mujoco_amd import _lib
+    idx, _ = _lib.decode_key(int(key.item()) & 0xFFFFFFFFFFFFFFFF)
+    assert idx == stats["sel_gpu"]
+    rows = (st_.cpu().numpy() >> 2) & 63
+    slab = rows > 36
+    rel = np.abs(a[:, 0] - o["cost4"][:, 0]) / np.abs(o["cost4"][:, 0])
+    well = (sens < pu.TOL / 10) & ~pu.grazing(m, o)
+    print(f"C3: {stats}; slab-path candidates {int(slab.sum())}, well-conditioned {int((slab & well).sum())}, "
+          f"their max rel {rel[slab & well].max() if (slab & well).any() else 0:.2e}")
+    assert (slab & well).sum() >= 100
 
 
 def test_thetadot_and_theta_outputs(torch_cuda):
@@ -168,36 +226,6 @@ def test_full_size_properties(torch_cuda):
     i_hi, _ = _lib.decode_key(int(k2.item()) & 0xFFFFFFFFFFFFFFFF)
     assert i_full == int(torch.argmin(a[:, 0]))
     assert i_hi == half + int(torch.argmin(a[half:, 0]))
-    # a 64-candidate sample of the full-size batch still matches the oracle
-    sel = np.arange(0, n, n // 64)
-    td = np.einsum("tk,njk->njt", Pd, xi.cpu().numpy()[sel].reshape(-1, 6, 11).astype(np.float64)).reshape(-1, 6 * H)
-    o = oracle.rollout(m, td, Q0, W, PT, QT, want_theta=False)["cost4"]
-    rel = np.abs(a.cpu().numpy()[sel, 0] - o[:, 0]) / np.abs(o[:, 0])
-    assert (rel < TOL).mean() >= 0.95, np.sort(rel)[-4:]
-
-
-def test_rows_past_lds_match_oracle(torch_cuda):
-    """The narrow kernel keeps the J rows of the first 56 constraint rows in LDS
-    and the rest in a per-candidate HBM slab: candidates of the C3 batch whose
-    busiest step needs more rows than that go through the slab path and must
-    match the oracle like the others (and the wide kernel, LDS only)."""
-    torch = torch_cuda
-    n, H = 4096, 50
-    m = models.load("scene_mjx", 0.05)
-    _, P, Pd, _ = basis.planner_basis(H, 0.05)
-    xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
-    e = Engine(m, H, n, Pd)
-    st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
-    a = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, status=st).cpu().numpy()
-    rows = ((st.cpu().numpy() >> 2) & 63)
-    sel = np.where(rows > 56)[0][:12]
-    assert len(sel) >= 4, np.sort(rows)[-8:]
-    td = np.einsum("tk,njk->njt", Pd, xi.cpu().numpy()[sel].reshape(-1, 6, 11).astype(np.float64)).reshape(-1, 6 * H)
-    o = oracle.rollout(m, td, Q0, W, PT, QT, want_slots=True)
-    rel = np.abs(a[sel, 0] - o["cost4"][:, 0]) / np.abs(o["cost4"][:, 0])
-    graze = (np.abs(o["slots"]) < 1e-5).any(axis=(1, 2))
-    assert (rel[~graze] < TOL).mean() >= 0.75, np.sort(rel)[-4:]
-    assert np.median(rel) < 1e-4
 
 
 def test_compute_cem_dropin(torch_cuda):
@@ -217,45 +245,25 @@ def test_compute_cem_dropin(torch_cuda):
     np.testing.assert_array_equal(out2[0], cost)
 
 
-def _intrinsic(m, td, rng):
-    """The fp64 oracle against itself under 1e-7 and 1e-6 relative input
-    noise (the order of fp32 rounding): how well-conditioned each candidate's
-    cost is.  Returns the unperturbed costs and the larger miss fraction."""
-    a = oracle.rollout(m, td, Q0, W, PT, QT, want_theta=False)["cost4"]
-    miss = 0.0
-    for eps in (1e-7, 1e-6):
-        b = oracle.rollout(m, td * (1 + eps * rng.standard_normal(td.shape)), Q0, W, PT, QT, want_theta=False)["cost4"]
-        miss = max(miss, float((np.abs(a[:, 0] - b[:, 0]) / np.abs(a[:, 0]) > TOL).mean()))
-    return a, miss
-
-
 @pytest.mark.parametrize("H", [50, 100])
 def test_dual_arm_parity_to_conditioning(torch_cuda, H):
     """Dual arm (C4/C5 scene) on realistic projected samples.  Its costs are
     chaotic even in fp64 (the 2F-85 linkage sits in permanent mesh contact and
     the Newton line search couples it to arm 1): 1e-7 input noise moves a
-    share of the candidates by more than 1e-4 (~3% at H = 50, ~30% at
-    H = 100, about independent of the noise level once chaotic).  The bar is
-    therefore the problem's own conditioning: the GPU may not miss 1e-4 on
-    more candidates than the perturbed oracle does, up to 3 binomial standard
-    deviations of the 128-sample fractions + 2%; the median error stays at
-    fp32 level and the GPU's selected candidate is among the oracle's best 3."""
+    share of the candidates by more than 1e-4.  The per-candidate bar of
+    tests/parity_util.py takes that into account."""
     torch = torch_cuda
-    n = 128
+    n = 256
     m = models.load("dual_arm", 0.05)
     _, P, Pd, _ = basis.planner_basis(H, 0.05)
     xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
     xi_h = xi.cpu().numpy()
     e = Engine(m, H, n, Pd)
     g = e.rollout_cost(xi_h, MPCR_LAYOUT_XI, Q0, W, PT, QT).astype(np.float64)
-    td = np.einsum("tk,njk->njt", Pd, xi_h.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
-    o, miss = _intrinsic(m, td, np.random.default_rng(H))
-    rel = np.abs(g[:, 0] - o[:, 0]) / np.abs(o[:, 0])
-    slack = 3 * np.sqrt(max(miss, 0.01) * (1 - miss) / n) + 0.02
-    assert (rel > TOL).mean() <= miss + slack, ((rel > TOL).mean(), miss, slack)
-    assert np.median(rel) < 1e-5
-    i = int(np.argmin(g[:, 0]))
-    assert int((o[:, 0] < o[i, 0]).sum()) < 3
+    o, sens = pu.conditioning(m, _td(Pd, xi_h, H), seed=H)
+    st = pu.check(m, g[:, 0], o, sens, f"dual arm H={H}")
+    print(f"dual arm H={H}: {st}")
+    assert st["median_rel"] < 1e-5
 
 
 def test_dual_arm_c4_properties(torch_cuda):
@@ -280,6 +288,11 @@ def test_dual_arm_c4_properties(torch_cuda):
     assert int((s_ & 1).sum()) == 0
     rows_per_step = (s_ >> 8) / H
     assert rows_per_step.min() >= 8  # 8 equality rows + the linkage contacts
+    # the whole shard against the oracle: conditioning bar and the selection
+    o, sens = pu.conditioning(m, _td(Pd, xi.cpu().numpy(), H), seed=7)
+    assert int(o["maxcon"].max()) <= 32 and int(o["maxrows"].max()) <= 8 + 4 * 32  # the wide image's caps
+    st_ = pu.check(m, a[:, 0].cpu().numpy(), o, sens, "C4 shard")
+    print(f"C4 shard: {st_}")
 
 
 def test_kernel_occupancy_budget(torch_cuda):
