@@ -3,15 +3,21 @@ MuJoCo-semantics steps -> cost -> best) on 1..8 MI355X, one process per GPU.
 
 Workload (BASELINE.json configs[2], the largest single-GPU config, named in
 the metric "UR5e scene"): URD/scene_mjx.xml (UR5e + Hand-E + object.xml free
-box resting on the table), 4096 candidates x 50 steps per GPU (weak scaling:
-N x 4096 candidates in total), order-10 Bernstein, dt = 0.05, Newton solver.
-A step = one rollout_cost launch over the rank's batch (inputs resident in
-HBM, theta/thetadot/cost4 written back like the reference's outputs) + the
-global best-candidate selection (fused atomic-min key; for N > 1 one 8-byte
-RCCL MIN all-reduce).  Synthetic inputs: xi ~ N(0, 10.003 I) (seed
-20250629 + 3 + rank), projected with 10 ADMM iterations before timing.
+box resting on the table), 4096 candidates x 50 steps per GPU, order-10
+Bernstein, dt = 0.05, Newton solver.  A step = one rollout_cost launch over
+the rank's batch (inputs resident in HBM, theta/thetadot/cost4 written back
+like the reference's outputs) + the global selection: the fused atomic-min
+best key (N > 1: one 8-byte RCCL MIN all-reduce) or, with --exchange elite
+(the C4 default), the sharded CEM's elite exchange as well (local top-E,
+RCCL all-gather of (xi row, cost), global top-E).  Synthetic inputs:
+xi ~ N(0, 10.003 I) (seed 20250629 + 3 + shard), projected with 10 ADMM
+iterations before timing.
 
-    python bench.py [--gpus N --steps K --warmup W]
+Scaling: --scaling weak (default): every rank owns --n candidates (N x 4096
+in total); --scaling strong: --n is the global batch, split over the ranks
+(C3's 4096 x 50 on 1..8 GPUs).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4] [--scaling strong]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 
@@ -33,22 +39,23 @@ Q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
 W = (20.0, 3.0, 80.0)
 PT = (-0.3, -0.3, 0.5)
 QT = (0.0, 1.0, 0.0, 0.0)
-PEAK_F32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = f32-MFMA dense peak
+PEAK_F32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (FMA) peak
 PEAK_HBM_GBS = 8000.0
+PROFILE_TAG = "r02"
 
 # BASELINE.json configs; c3 is the metric's workload (default)
 CONFIGS = {
-    "c2": dict(model="ur5e_hande_mjx", n=1024, H=50,
+    "c2": dict(model="ur5e_hande_mjx", n=1024, H=50, exchange="key",
                desc="URD/ur5e_1_robotiq_hande_mjx.xml arm alone, Newton(1 it, 5 ls)"),
-    "c3": dict(model="scene_mjx", n=4096, H=50,
+    "c3": dict(model="scene_mjx", n=4096, H=50, exchange="key",
                desc="UR5e+Hand-E arm + object.xml box (URD/scene_mjx.xml), Newton(1 it, 5 ls)"),
-    "c4": dict(model="dual_arm", n=4096, H=100,
+    "c4": dict(model="dual_arm", n=4096, H=100, exchange="elite",
                desc="dual-arm gripper scene (implicitfast, 14 actuators, connect equalities, convex-hull "
-                    "meshes), Newton(100 it, 50 ls); C4 = 8 GPUs x 4096"),
+                    "meshes), Newton(100 it, 50 ls); C4 = 8 GPUs x 4096, elite exchange per step"),
 }
 
 
-def flops_per_step(m, nefc_mean, ncon_pairs=None):
+def flops_per_step(m, nefc_mean):
     fm = json.load(open(os.path.join(ROOT, "bench", "flops_model.json")))
     nb_moving = int(sum(1 for b in range(1, m.nbody) if m.body_weldid[b] != 0))
     names = {0: "plane_capsule", 1: "plane_box", 2: "capsule_capsule", 3: "capsule_box", 4: "box_box", 9: "convex",
@@ -64,53 +71,87 @@ def flops_per_step(m, nefc_mean, ncon_pairs=None):
     return float(f)
 
 
-def pmc_traffic(path, kernel="rollout_kernel"):
-    """HBM bytes per dispatch from a committed rocprofv3 --pmc CSV (FETCH_SIZE
-    doubled per the gfx950 note in MI355X_MICROARCH.md §HBM, plus WRITE_SIZE)."""
+def _pmc_rows(path, kernel="rollout_kernel"):
     import csv
-    if not os.path.exists(path):
-        return None
-    fetch, write = [], []
+    out = {}
+    if not path or not os.path.exists(path):
+        return out
     with open(path) as f:
         for row in csv.DictReader(f):
             if kernel not in row.get("Kernel_Name", ""):
                 continue
-            name = row.get("Counter_Name", "")
-            val = float(row.get("Counter_Value", 0))
-            if name == "FETCH_SIZE":
-                fetch.append(val)
-            elif name == "WRITE_SIZE":
-                write.append(val)
-    if not fetch and not write:
+            out.setdefault(row.get("Counter_Name", ""), []).append(float(row.get("Counter_Value", 0)))
+    return out
+
+
+def pmc_traffic(path):
+    """HBM bytes per dispatch from a committed rocprofv3 --pmc CSV (FETCH_SIZE
+    doubled per the gfx950 note in MI355X_MICROARCH.md §HBM, plus WRITE_SIZE;
+    both KiB)."""
+    c = _pmc_rows(path)
+    if "FETCH_SIZE" not in c and "WRITE_SIZE" not in c:
         return None
-    kb = 2.0 * (np.mean(fetch) if fetch else 0.0) + (np.mean(write) if write else 0.0)
+    kb = 2.0 * float(np.mean(c.get("FETCH_SIZE", [0.0]))) + float(np.mean(c.get("WRITE_SIZE", [0.0])))
     return kb * 1024.0
 
 
-def cpu_baseline(m, xi, H, Pd, workers):
-    """fp64 scalar C oracle on host cores over a bounded sample of the same workload."""
+def pmc_valu(path, n, H, flops_step):
+    """VALU instructions per candidate-step (one wave = one candidate) and the
+    lane-flop efficiency flops / (64 x VALU instructions) from a committed SQ
+    counter CSV of the same workload."""
+    c = _pmc_rows(path)
+    if "SQ_INSTS_VALU" not in c:
+        return None
+    insts = float(np.mean(c["SQ_INSTS_VALU"]))
+    waves = float(np.mean(c.get("SQ_WAVES", [n])))
+    per = insts / (waves * H)
+    rec = {"valu_insts_per_candidate_step": round(per, 1),
+           "lane_flop_efficiency": round(flops_step / (64.0 * per), 4), "source": os.path.relpath(path, ROOT)}
+    if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        # SQ_ACTIVE_INST_VALU counts quad-cycles; GRBM_GUI_ACTIVE is summed over
+        # the 8 XCDs (MI355X_MICROARCH.md); 1024 SIMDs
+        busy = (4.0 * float(np.mean(c["SQ_ACTIVE_INST_VALU"])) / 1024.0
+                / (float(np.mean(c["GRBM_GUI_ACTIVE"])) / 8.0))
+        rec["valu_busy"] = round(busy, 3)
+    return rec
+
+
+def _host_cpu():
+    """(usable host cores, machine cpu count, model name)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return usable, os.cpu_count() or 1, model
+
+
+def cpu_baseline(m, xi, H, Pd, threads, reps=5):
+    """The fp64 scalar C oracle (oracle/mpcr_oracle.c, a restatement of the
+    reference's rollout + cost, SBP/mjx_planner.py:123-124) on host threads:
+    pool started and model converted before the clock; median of `reps`
+    timed repetitions of the rollout compute only.  Returns rollouts/s."""
     import oracle
-    from concurrent.futures import ProcessPoolExecutor
     oracle.build()
     n = xi.shape[0]
     td = np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
-    chunks = np.array_split(np.arange(n), workers)
-    t0 = time.perf_counter()
-    if workers == 1:
-        oracle.rollout(m, td, Q0, np.array(W), np.array(PT), np.array(QT), want_theta=False)
-    else:
-        with ProcessPoolExecutor(workers) as ex:
-            list(ex.map(_oracle_chunk, [(td[c], m.bundle_name) for c in chunks]))
-    return n / (time.perf_counter() - t0)
-
-
-def _oracle_chunk(args):
-    import oracle
-    from manipulator_mujoco_amd import models
-    td, name = args
-    m = models.load(name, 0.05)
-    oracle.rollout(m, td, Q0, np.array(W), np.array(PT), np.array(QT), want_theta=False)
-    return td.shape[0]
+    run = oracle.Runner(m, threads, Q0, W, PT, QT)
+    run.rollout(td[: max(1, min(n, threads))])  # warm-up (page in, first-touch)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        run.rollout(td)
+        ts.append(time.perf_counter() - t0)
+    run.close()
+    return n / float(np.median(ts)), [round(n / t, 1) for t in ts]
 
 
 def main():
@@ -120,25 +161,32 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
                     help="BASELINE.json config preset (c3 = the metric's workload, the default)")
-    ap.add_argument("--n", type=int, default=None, help="candidates per GPU (default: the config's)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: --n candidates per GPU; strong: --n candidates in total, split over the GPUs")
+    ap.add_argument("--exchange", choices=("key", "elite"), default=None,
+                    help="per-step selection: best-key MIN all-reduce, or also the CEM elite exchange")
+    ap.add_argument("--n", type=int, default=None, help="candidates (per GPU for weak, total for strong)")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--model", default=None)
-    ap.add_argument("--cpu-sample", type=int, default=4096)
-    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-sample", type=int, default=2048)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the usable host cores, at most 16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=None,
-                    help="rocprofv3 --pmc CSV of this workload (default: the committed C3 one for c3, else none)")
+    ap.add_argument("--no-contact-report", action="store_true")
+    ap.add_argument("--pmc", default=None, help="rocprofv3 FETCH/WRITE CSV of this workload")
+    ap.add_argument("--pmc-sq", default=None, help="rocprofv3 SQ counter CSV of this workload")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.model = args.model or cfg["model"]
     args.n = args.n or cfg["n"]
     args.horizon = args.horizon or cfg["H"]
+    args.exchange = args.exchange or cfg["exchange"]
 
     import torch
     import torch.distributed as dist
 
     from manipulator_mujoco_amd import basis, models
     from manipulator_mujoco_amd import dist as md
+    from manipulator_mujoco_amd.cem import topk
     from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine
     from manipulator_mujoco_amd.projection import ProjectionFilter
 
@@ -146,34 +194,45 @@ def main():
     if world == 1 and args.gpus > 1:
         raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
 
-    H, n = args.horizon, args.n
+    H = args.horizon
+    if args.scaling == "strong":
+        lo, hi = md.shard(args.n, rank, world)
+        n, n_total, base = hi - lo, args.n, lo
+    else:
+        n, n_total, base = args.n, args.n * world, rank * args.n
     m = models.load(args.model, 0.05)
-    m.bundle_name = args.model
     _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
-    # synthetic inputs, generated on the host (same bytes on every run)
-    rng = np.random.default_rng(20250629 + 3 + rank)
     cpu = torch.device("cpu")
     proj = ProjectionFilter(P, Pd, Pdd, 6, cpu)
-    xi_host = proj(torch.tensor(rng.normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32)),
-                   proj.boundary(Q0, np.zeros(6), np.zeros(6), n), 10)
+    # synthetic inputs, generated on the host (same bytes on every run); strong
+    # scaling draws the global batch and takes this rank's rows
+    rng = np.random.default_rng(20250629 + 3 + (0 if args.scaling == "strong" else rank))
+    n_draw = n_total if args.scaling == "strong" else n
+    xi_all = proj(torch.tensor(rng.normal(0, np.sqrt(10.003), (n_draw, 66)).astype(np.float32)),
+                  proj.boundary(Q0, np.zeros(6), np.zeros(6), n_draw), 10)
+    xi_host = xi_all[base:base + n] if args.scaling == "strong" else xi_all
     cpu_rec = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # host-core baseline first: its worker processes are forked before
-        # this process initialises the GPU
-        workers = args.cpu_workers or min(16, os.cpu_count() or 1)
+        # host-core baseline before the process initialises the GPU
+        usable, ncpu, model = _host_cpu()
+        threads = args.cpu_threads or min(16, usable)
         sample = xi_host[: args.cpu_sample].numpy()
-        v1 = cpu_baseline(m, sample[: max(64, args.cpu_sample // 16)], H, Pd, 1)
-        vp = cpu_baseline(m, sample, H, Pd, workers)
-        cpu_rec = {"value": round(vp, 1), "unit": "rollouts/s", "cores": workers, "kind": "port",
-                   "sample": f"{sample.shape[0]} of the same {args.config.upper()} candidates x {H} steps, fp64 "
-                             f"scalar C oracle "
-                             f"(oracle/mpcr_oracle.c), {workers} processes; 1 core: {v1:.1f} rollouts/s",
-                   "one_core": round(v1, 1)}
+        vp, reps = cpu_baseline(m, sample, H, Pd, threads)
+        v1, _ = cpu_baseline(m, sample[: max(32, args.cpu_sample // 16)], H, Pd, 1)
+        cpu_rec = {"value": round(vp, 1), "unit": "rollouts/s", "cores": threads, "kind": "port",
+                   "sample": f"{sample.shape[0]} of the same {args.config.upper()} candidates x {H} steps; fp64 "
+                             f"scalar C restatement of the reference rollout + cost (oracle/mpcr_oracle.c, not "
+                             f"CPU-MJX), {threads} threads, median of {len(reps)} timed repetitions (pool and model "
+                             f"set up before the clock); 1 thread: {v1:.1f} rollouts/s",
+                   "precision": "fp64", "one_core": round(v1, 1), "reps": reps,
+                   "host": {"usable_cores": usable, "nproc": ncpu, "cpu_model": model}}
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = None
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        backend = dist.get_backend()
     xi = xi_host.to(dev)
     eng = Engine(m, H, n, Pd, device=local)
     cost4 = torch.empty((n, 4), dtype=torch.float32, device=dev)
@@ -181,14 +240,22 @@ def main():
     thetadot = torch.empty((n, 6 * H), dtype=torch.float32, device=dev)
     key = torch.empty(1, dtype=torch.int64, device=dev)
     status = torch.zeros(n, dtype=torch.int32, device=dev)
+    n_elite = int(0.05 * n_total)
+    topk_fn = (lambda c, k: topk(eng, c, k))
 
     def step(ev=None):
         if ev is not None:
             ev[0].record()
         eng.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, cost4=cost4, theta=theta, thetadot=thetadot,
-                         best_key=key, index_base=rank * n, status=status)
+                         best_key=key, index_base=base, status=status)
         if ev is not None:
             ev[1].record()
+        if args.exchange == "elite":
+            c = cost4[:, 0].contiguous()
+            if world > 1:
+                md.gather_elites(c, xi, n_elite, topk_fn)
+            else:
+                topk_fn(c, n_elite)
         if world > 1:
             md.allreduce_min_key(key)
 
@@ -207,7 +274,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kms = [a.elapsed_time(b) for a, b in events]
+    kern_ms = float(np.median(kms))
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -216,35 +284,57 @@ def main():
     trunc = int((status & 1).sum().item())
     nefc_mean = float((status >> 8).double().mean().item()) / H
 
+    contact = None
+    if rank == 0 and not args.no_contact_report and m.nslot:
+        # SURVEY §8d asks whether contacts activate (C2 "no contacts"): the
+        # masked robot slots of this batch, traced outside the timed region
+        tr = eng.trace(xi_host.numpy(), MPCR_LAYOUT_XI, Q0, W, PT, QT)
+        act = (tr["slots"] < 0).any(axis=2)
+        first = np.where(act.any(axis=1), act.argmax(axis=1), -1)
+        contact = {"candidates_with_active_robot_contact": int(act.any(axis=1).sum()), "of": int(n),
+                   "first_active_step_median": float(np.median(first[first >= 0])) if (first >= 0).any() else None}
+
     if rank == 0:
-        total = n * world
-        value = total * args.steps / elapsed
-        # algorithmic work of the dominant kernel per launch
+        value = n_total * args.steps / elapsed
         fps = flops_per_step(m, nefc_mean)  # mean constraint rows/step measured by the kernel
         flops_launch = fps * H * n
         achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
         hbm_launch = n * (66 * 4 + 16 + 2 * 6 * H * 4 + 4)  # xi in; cost4, theta, thetadot, status out
-        pmc = args.pmc or (os.path.join(ROOT, "profiles", "r01_pmc_rollout.csv") if args.config == "c3" else None)
+        default_prof = args.config == "c3" and args.n == 4096 and args.scaling == "weak"
+        pmc = args.pmc or (os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_rollout.csv") if default_prof else None)
+        pmc_sq = args.pmc_sq or (os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_sq.csv") if default_prof
+                                 else None)
         traffic = pmc_traffic(pmc) if pmc else None
+        valu = pmc_valu(pmc_sq, n, H, fps) if pmc_sq else None
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": "rollouts/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (xi ~ N(0, 10.003 I), 10-iteration ADMM projection; seed 20250629+3+rank)",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (xi ~ N(0, 10.003 I), 10-iteration ADMM projection; seed 20250629+3"
+                    + ("" if args.scaling == "strong" else "+rank") + ")",
             "config": {"workload": f"{args.config.upper()} {args.model}: {cfg['desc']}, {n} candidates x {H} "
                                    f"steps per GPU, order-10 Bernstein, dt 0.05",
-                       "candidates_per_gpu": n, "horizon": H, "global_batch": total,
-                       "parallelism": f"dp{world} (candidate shards, 8-byte RCCL MIN all-reduce)"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_TFLOPS, 5),
+                       "candidates_per_gpu": n, "horizon": H, "global_batch": n_total,
+                       "parallelism": f"dp{world} (candidate shards; {args.exchange} exchange)",
+                       "world_size_seen": world, "backend": backend or "single process",
+                       "exchange": "8-byte RCCL MIN all-reduce of the best key" + (
+                           "; local top-E + RCCL all-gather of (xi, cost) rows + global top-E"
+                           if args.exchange == "elite" else "")},
+            "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_VALU_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_VALU_TFLOPS, 5),
                          "traffic": None if traffic is None else round(traffic),
                          "kernel": "rollout_kernel", "kernel_ms": round(kern_ms, 4),
+                         "kernel_ms_mean": round(float(np.mean(kms)), 4),
                          "flops_per_step": fps, "hbm_algorithmic_bytes": hbm_launch,
                          "hbm_achieved_GBs": round(hbm_launch / (kern_ms * 1e-3) / 1e9, 2),
                          "hbm_frac": round(hbm_launch / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 6)},
             "best": {"index": idx, "cost": best}, "truncated_candidates": trunc,
             "mean_constraint_rows": round(nefc_mean, 2),
         }
+        if valu is not None:
+            rec["roofline"]["valu"] = valu
+        if contact is not None:
+            rec["contacts"] = contact
         if cpu_rec is not None:
             rec["cpu_baseline"] = cpu_rec
         print(json.dumps(rec))

@@ -87,6 +87,11 @@ int mpcr_device_arch(int device, char* buf, int buflen);
 
 /* models: a serialised mpcr_model_t (see mpcr_model.h) */
 int mpcr_model_from_blob(const void* blob, size_t nbytes, mpcr_model** out);
+/* path: an MJCF scene (.xml, or any file starting with '<') -- compiled by
+   the MJCF compiler of libmpcr_mjcf.so (include/mpcr_mjcf.h), dlopened from
+   this library's directory on first use: MjModel.from_xml_path,
+   SBP/mjx_planner.py:100-103 -- or a serialised mpcr_model_t blob.
+   timestep > 0 overrides the model's (opt.timestep = dt, :102). */
 int mpcr_model_load(const char* path, double timestep, mpcr_model** out);
 int mpcr_model_set_timestep(mpcr_model* m, double timestep);
 int mpcr_model_info(const mpcr_model* m, int* nq, int* nv, int* nslot, int* nctrl, int* npair);

@@ -67,7 +67,27 @@ def compile_lib(out: str, extra=(), verbose: bool = False) -> str:
     return out
 
 
+MJCF_SRC = os.path.join(CSRC, "mjcf_embed.cpp")
+MJCF_OUT = os.path.join(HERE, "libmpcr_mjcf.so")
+
+
+def compile_mjcf_lib(out: str = MJCF_OUT) -> str:
+    """libmpcr_mjcf.so: the MJCF compiler (mjcf.py) in an embedded CPython,
+    host C++ only (g++), dlopened by libmpcr.so for .xml model paths."""
+    import sysconfig
+    inc = sysconfig.get_paths()["include"]
+    libdir = sysconfig.get_config_var("LIBDIR")
+    ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+    cmd = [shutil.which("g++") or "g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{inc}", MJCF_SRC,
+           f"-L{libdir}", f"-Wl,-rpath,{libdir}", f"-lpython{ver}", "-ldl", "-o", out + ".tmp"]
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    if force or not os.path.exists(MJCF_OUT) or os.path.getmtime(MJCF_OUT) < os.path.getmtime(MJCF_SRC):
+        compile_mjcf_lib()
     if not force and os.path.exists(OUT):
         mt = os.path.getmtime(OUT)
         if all(os.path.getmtime(d) <= mt for d in DEPS):

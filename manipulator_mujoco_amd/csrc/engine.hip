@@ -1,6 +1,7 @@
 // engine.hip — host side of the C ABI (include/mpcr.h): model blobs, the
 // fp32 device model with its derived tables, engines, launches.
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 
 #include <cmath>
 #include <cstdarg>
@@ -163,8 +164,50 @@ extern "C" int mpcr_model_from_blob(const void* blob, size_t nbytes, mpcr_model*
   return MPCR_OK;
 }
 
+// MJCF: the compiler in libmpcr_mjcf.so (next to this library), dlopened on
+// first use so the engine itself never links Python
+static int load_mjcf(const char* path, double timestep, mpcr_model** out) {
+  using compile_fn = int (*)(const char*, double, void**, size_t*, char*, int);
+  using free_fn = void (*)(void*);
+  static void* so = nullptr;
+  if (!so) {
+    Dl_info info;
+    std::string dir = ".";
+    if (dladdr(reinterpret_cast<void*>(&mpcr_model_load), &info) && info.dli_fname) {
+      dir = info.dli_fname;
+      size_t k = dir.find_last_of('/');
+      dir = k == std::string::npos ? std::string(".") : dir.substr(0, k);
+    }
+    so = dlopen((dir + "/libmpcr_mjcf.so").c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!so) return fail(MPCR_EMODEL, "MJCF compiler unavailable: %s", dlerror());
+  }
+  auto compile = reinterpret_cast<compile_fn>(dlsym(so, "mpcr_mjcf_compile"));
+  auto release = reinterpret_cast<free_fn>(dlsym(so, "mpcr_mjcf_free"));
+  if (!compile || !release) return fail(MPCR_EMODEL, "libmpcr_mjcf.so lacks its entry points");
+  void* blob = nullptr;
+  size_t n = 0;
+  char err[512] = {0};
+  if (compile(path, timestep, &blob, &n, err, sizeof(err)) != 0) return fail(MPCR_EMODEL, "MJCF %s: %s", path, err);
+  int rc = mpcr_model_from_blob(blob, n, out);
+  release(blob);
+  return rc;
+}
+
+static bool is_mjcf(const char* path) {
+  const size_t n = std::strlen(path);
+  if (n >= 4 && std::strcmp(path + n - 4, ".xml") == 0) return true;
+  FILE* f = fopen(path, "rb");
+  if (!f) return false;
+  int c;
+  while ((c = fgetc(f)) == ' ' || c == '\n' || c == '\r' || c == '\t') {
+  }
+  fclose(f);
+  return c == '<';
+}
+
 extern "C" int mpcr_model_load(const char* path, double timestep, mpcr_model** out) {
   if (!path || !out) return fail(MPCR_EINVAL, "null argument");
+  if (is_mjcf(path)) return load_mjcf(path, timestep, out);
   FILE* f = fopen(path, "rb");
   if (!f) return fail(MPCR_EINVAL, "cannot open %s", path);
   std::vector<char> buf(sizeof(mpcr_model_t) + 1);
@@ -652,7 +695,9 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     return fail(MPCR_ENOMEM, "device allocation failed");
   }
   if (hipMemcpy(e->d_model, &e->dev, sizeof(DevModel), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(e->d_pdot, pdot, sizeof(float) * horizon * nbasis, hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(e->d_pdot, pdot, sizeof(float) * horizon * nbasis, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(e->d_hints, 0xff, sizeof(short) * 2 * (size_t)max_n * (e->wide ? SmemW::NHINT : 1)) !=
+          hipSuccess) {
     mpcr_engine_free(e);
     return fail(MPCR_EHIP, "model upload failed");
   }
@@ -861,6 +906,9 @@ extern "C" int mpcr_plant_set_state(mpcr_plant* p, const double* qpos, const dou
   if (qacc_warmstart)
     for (int i = 0; i < h.nv; i++) p->h_state[ST_QWS + i] = (float)qacc_warmstart[i];
   HIPCHK(hipMemcpy(p->d_state, p->h_state, sizeof(float) * ST_N, hipMemcpyHostToDevice));
+  // a new state starts a new trajectory: the hull-climb starts the plant
+  // keeps across steps (like a rollout's, and the oracle's) start over
+  HIPCHK(hipMemset(p->e->d_hints, 0xff, sizeof(short) * 2 * (p->e->wide ? SmemW::NHINT : 1)));
   return MPCR_OK;
 }
 

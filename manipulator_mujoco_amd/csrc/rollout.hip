@@ -422,15 +422,17 @@ __device__ __forceinline__ float point_box(const float p[3], const float h[3], f
     for (int k = 0; k < 3; k++) nl[k] = o[k] / l;
     return l;
   }
-  // inside: the deepest face is argmax_k |p_k| - h_k (first maximum)
+  // inside: the deepest face is argmax_k |p_k| - h_k; ties within 1 um go to
+  // the lower axis and a point on the box's mid-plane to the + face (the
+  // oracle's point_box rule)
   const float g0 = fabsf(p[0]) - h[0], g1 = fabsf(p[1]) - h[1], g2 = fabsf(p[2]) - h[2];
   int best = 0;
   float g = g0;
-  if (g1 > g) { g = g1; best = 1; }
-  if (g2 > g) { g = g2; best = 2; }
+  if (g1 > g + 1e-6f) { g = g1; best = 1; }
+  if (g2 > g + 1e-6f) { g = g2; best = 2; }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const float sg = p[k] >= 0 ? 1.f : -1.f;
+    const float sg = p[k] >= -1e-6f ? 1.f : -1.f;
     nl[k] = k == best ? -sg : 0.f;
     q[k] = k == best ? sg * h[k] : p[k];
   }
@@ -454,15 +456,28 @@ constexpr int kMprIter = MPCR_MPR_ITER;
 constexpr float kMprEps = 1.1920929e-07f;
 __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
 
-// examine the neighbours of vertex v along l: the best strictly better one
-// (first in list order on ties) or -1.  The first 8 neighbours (90 % of hull
-// vertices have <= 8) are 8 independent loads issued together; the rest loop.
+// Ties in the support mapping resolve as in the oracle's support(): a box /
+// capsule / cylinder axis with |l_k| < kSupTie |l| contributes 0 (its face or
+// segment centre) instead of the sign of rounding noise, and the hull climb
+// only moves to a neighbour beating the current vertex by more than kSupBand
+// metres along the unit direction (coplanar vertices are ties, the first in
+// list order wins).
+constexpr float kSupTie = 1e-6f;
+constexpr float kSupBand = 1e-6f;
+__device__ __forceinline__ float tie_sign(float lk, float ln) {
+  return fabsf(lk) < kSupTie * ln ? 0.f : (lk >= 0.f ? 1.f : -1.f);
+}
+
+// examine the neighbours of vertex v along l (unit): one must beat bn (the
+// current vertex + band, then the chosen neighbour + band); -1 if none.
+// The first 8 neighbours (90 % of hull vertices have <= 8) are 8 independent
+// loads issued together; the rest loop.
 __device__ __forceinline__ void climb_scan(const DevModel* __restrict__ m, const float4 (&w)[8], int k0, int end,
-                                           const float l[3], float& best, float4& hv, int& nb) {
+                                           const float l[3], float& bn, float4& hv, int& nb) {
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     const float du = w[j].x * l[0] + w[j].y * l[1] + w[j].z * l[2];
-    if (k0 + j < end && du > best) { best = du; nb = __float_as_int(w[j].w); hv = w[j]; }
+    if (k0 + j < end && du > bn) { bn = du + kSupBand; nb = __float_as_int(w[j].w); hv = w[j]; }
   }
 }
 __device__ __forceinline__ void climb_load(const DevModel* __restrict__ m, int k0, int last, float4 (&w)[8]) {
@@ -474,13 +489,15 @@ __device__ __forceinline__ int climb_round(const DevModel* __restrict__ m, int v
   const int2 info = m->hull_info[v];
   const int end = info.x + info.y;
   int nb = -1;
+  float bn = best + kSupBand;
   float4 w[8];
   climb_load(m, info.x, end - 1, w);
-  climb_scan(m, w, info.x, end, l, best, hv, nb);
+  climb_scan(m, w, info.x, end, l, bn, hv, nb);
   for (int k0 = info.x + 8; k0 < end; k0 += 8) {
     climb_load(m, k0, end - 1, w);
-    climb_scan(m, w, k0, end, l, best, hv, nb);
+    climb_scan(m, w, k0, end, l, bn, hv, nb);
   }
+  if (nb >= 0) best = bn - kSupBand;
   return nb;
 }
 
@@ -493,25 +510,27 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
   const float* sz = m->geom_size[g];
   float l[3], p[3] = {0.f, 0.f, 0.f};
   mtv(l, R, dir);
+  const float ln = sqrtf(dot3(l, l));
   const int type = m->geom_type[g];
   if (type == 2 || type == 3) {  // sphere, capsule
-    const float n = sqrtf(dot3(l, l));
-    if (n > 0.f) { p[0] = sz[0] * l[0] / n; p[1] = sz[0] * l[1] / n; p[2] = sz[0] * l[2] / n; }
-    if (type == 3) p[2] += l[2] >= 0.f ? sz[1] : -sz[1];
+    if (ln > 0.f) { p[0] = sz[0] * l[0] / ln; p[1] = sz[0] * l[1] / ln; p[2] = sz[0] * l[2] / ln; }
+    if (type == 3) p[2] += tie_sign(l[2], ln) * sz[1];
   } else if (type == 5) {  // cylinder
     const float r = sqrtf(l[0] * l[0] + l[1] * l[1]);
-    if (r > 0.f) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
-    p[2] = l[2] >= 0.f ? sz[1] : -sz[1];
+    if (r > kSupTie * ln) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
+    p[2] = tie_sign(l[2], ln) * sz[1];
   } else if (type == 6) {  // box
-    p[0] = l[0] >= 0.f ? sz[0] : -sz[0];
-    p[1] = l[1] >= 0.f ? sz[1] : -sz[1];
-    p[2] = l[2] >= 0.f ? sz[2] : -sz[2];
+    p[0] = tie_sign(l[0], ln) * sz[0];
+    p[1] = tie_sign(l[1], ln) * sz[1];
+    p[2] = tie_sign(l[2], ln) * sz[2];
   } else if (type == 7) {  // mesh hull: steepest ascent on the vertex graph from its first vertex
+    const float il = ln > 0.f ? 1.f / ln : 0.f;
+    const float lu[3] = {l[0] * il, l[1] * il, l[2] * il};
     int v = hint >= 0 ? hint : m->geom_hulladr[g];
     float4 hv = m->hull_vert[v];
-    float best = hv.x * l[0] + hv.y * l[1] + hv.z * l[2];
+    float best = hv.x * lu[0] + hv.y * lu[1] + hv.z * lu[2];
     for (int guard = 0; guard < 4096; guard++) {
-      const int nb = climb_round(m, v, l, best, hv);
+      const int nb = climb_round(m, v, lu, best, hv);
       if (nb < 0) break;
       v = nb;
     }
@@ -585,17 +604,31 @@ __device__ __forceinline__ void tri_closest(const float a[3], const float b[3], 
     for (int k = 0; k < 3; k++) out[k] = b[k] + t * (c[k] - b[k]);
     return;
   }
-  const float den = 1.f / (va + vb + vc), v = vb * den, w = vc * den;
+  // face region: the plane projection n (n.a) / |n|^2 (the oracle's
+  // tri_closest): the barycentric a + v ab + w ac cancels catastrophically in
+  // fp32 for MPR's cm-sized final portal around a sub-mm penetration
+  float n[3];
+  cross(n, ab, ac);
+  const float sc = dot3(n, a) / dot3(n, n);
 #pragma unroll
-  for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
+  for (int k = 0; k < 3; k++) out[k] = n[k] * sc;
+  (void)va; (void)vb; (void)vc;
 }
 
-// returns true and (depth, dir g1 -> g2, pos) when the geoms overlap
+// returns true and (depth, dir g1 -> g2, pos) when the geoms overlap.
+// Zero tests are geometric and in metres, identical in the oracle: libccd's
+// are absolute DBL_EPSILON tests on lengths, areas and volumes alike, which
+// in fp32 call two cm-scale vectors parallel (|v0 x v1|^2 ~ 1e-8 < eps);
+// here a length is zero below kMprEps (1.2e-7 m, fp32 resolution of world
+// coordinates), two vectors are parallel when one passes within kMprEps of
+// the other's line, and a point lies on a plane within kMprEps of it.
 template <class S>
 __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int g2, float& depth, float dir[3],
                          float pos[3], int (&hint)[2]) {
   MprPt p[4], v4;
   float va[3], vb[3], dd;
+  // point x off the plane through the origin with (unnormalised) normal c by more than kMprEps
+  auto off_plane = [](float x, const float c[3]) { return fabsf(x) >= kMprEps * sqrtf(dot3(c, c)); };
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     p[0].a[k] = s.gxpos[g1][k];
@@ -609,18 +642,21 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   dd = dot3(p[1].v, dir);
   if (mpr_zero(dd) || dd < 0.f) return false;
   cross(dir, p[0].v, p[1].v);
-  if (mpr_zero(dot3(dir, dir))) {
+  {
+    const float thr = kMprEps * (sqrtf(dot3(p[0].v, p[0].v)) + sqrtf(dot3(p[1].v, p[1].v)));
+    if (dot3(dir, dir) < thr * thr) {  // v1 on the ray from v0 through the origin
 #pragma unroll
-    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].a[k] + p[1].b[k]);
-    if (mpr_zero(p[1].v[0]) && mpr_zero(p[1].v[1]) && mpr_zero(p[1].v[2])) {
-      depth = 0.f;
-      dir[0] = dir[1] = dir[2] = 0.f;
-    } else {
-      dir[0] = p[1].v[0]; dir[1] = p[1].v[1]; dir[2] = p[1].v[2];
-      depth = sqrtf(dot3(dir, dir));
-      nrm3(dir);
+      for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].a[k] + p[1].b[k]);
+      if (mpr_zero(p[1].v[0]) && mpr_zero(p[1].v[1]) && mpr_zero(p[1].v[2])) {
+        depth = 0.f;
+        dir[0] = dir[1] = dir[2] = 0.f;
+      } else {
+        dir[0] = p[1].v[0]; dir[1] = p[1].v[1]; dir[2] = p[1].v[2];
+        depth = sqrtf(dot3(dir, dir));
+        nrm3(dir);
+      }
+      return true;
     }
-    return true;
   }
   nrm3(dir);
   mpr_support(m, s, g1, g2, dir, p[2], hint);
@@ -642,11 +678,11 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     bool cont = false;
     cross(va, p[1].v, p[3].v);
     dd = dot3(va, p[0].v);
-    if (dd < 0.f && !mpr_zero(dd)) { p[2] = p[3]; cont = true; }
+    if (dd < 0.f && off_plane(dd, va)) { p[2] = p[3]; cont = true; }
     if (!cont) {
       cross(va, p[3].v, p[2].v);
       dd = dot3(va, p[0].v);
-      if (dd < 0.f && !mpr_zero(dd)) { p[1] = p[3]; cont = true; }
+      if (dd < 0.f && off_plane(dd, va)) { p[1] = p[3]; cont = true; }
     }
     if (!cont) break;
 #pragma unroll
@@ -675,13 +711,19 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   if (mpr_zero(depth)) { dir[0] = dir[1] = dir[2] = 0.f; }
   else { dir[0] = w[0] / depth; dir[1] = w[1] / depth; dir[2] = w[2] / depth; }
   float pd[3], b[4], x[3];
-  mpr_dir(p, pd);
+  {
+    float e1[3] = {p[2].v[0] - p[1].v[0], p[2].v[1] - p[1].v[1], p[2].v[2] - p[1].v[2]};
+    float e2[3] = {p[3].v[0] - p[1].v[0], p[3].v[1] - p[1].v[1], p[3].v[2] - p[1].v[2]};
+    cross(pd, e1, e2);  // portal normal, |pd| = twice the portal's area
+  }
   cross(x, p[2].v, p[3].v); b[0] = dot3(x, p[1].v);
   cross(x, p[3].v, p[2].v); b[1] = dot3(x, p[0].v);
   cross(x, p[0].v, p[1].v); b[2] = dot3(x, p[3].v);
   cross(x, p[2].v, p[1].v); b[3] = dot3(x, p[0].v);
   float sum = b[0] + b[1] + b[2] + b[3];
-  if (mpr_zero(sum) || sum < 0.f) {
+  // sum = 6 x the tetrahedron's volume: degenerate when v0 lies within kMprEps of the portal's plane
+  if (!off_plane(sum, pd) || sum < 0.f) {
+    nrm3(pd);
     b[0] = 0.f;
     cross(x, p[2].v, p[3].v); b[1] = dot3(x, pd);
     cross(x, p[3].v, p[1].v); b[2] = dot3(x, pd);
@@ -1621,11 +1663,15 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
   //      (plant mode: the caller's state, no init_pos override)
   if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
-  if constexpr (S::WIDE) {
-    int* h = reinterpret_cast<int*>(args.hints + (size_t)b * S::NHINT * 2);
-    for (int i = lane; i < S::NHINT; i += S::HL) h[i] = -1;  // both sides -1
-  }
   const bool from_state = (args.plant & 1) != 0;
+  if constexpr (S::WIDE) {
+    // a rollout starts its hull climbs afresh; the plant keeps them across
+    // steps (reset by mpcr_plant_set_state), so k plant steps = a k-step rollout
+    if (!from_state) {
+      int* h = reinterpret_cast<int*>(args.hints + (size_t)b * S::NHINT * 2);
+      for (int i = lane; i < S::NHINT; i += S::HL) h[i] = -1;  // both sides -1
+    }
+  }
   for (int i = lane; i < S::NQW; i += S::HL)
     s.qpos[i] = i < m->nq ? (from_state ? args.state[ST_QPOS + i] : m->qpos_init[i]) : 0.f;
   if (lane < NVW) {

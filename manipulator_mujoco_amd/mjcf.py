@@ -1299,6 +1299,14 @@ def set_const(m):
     return m
 
 
+def compile_blob(path: str, timestep: float = 0.0) -> bytes:
+    """The serialised mpcr_model_t of an MJCF file (timestep <= 0: the file's
+    own): what libmpcr_mjcf.so hands to mpcr_model_from_blob when
+    mpcr_model_load is given an .xml path (the C-ABI's MJCF entry)."""
+    m = compile_mjcf(path, timestep if timestep and timestep > 0 else None)
+    return bytes(m.to_struct())
+
+
 def load_model(path: str, timestep: float | None = None) -> Model:
     """Load an MJCF (.xml) or a precompiled model bundle (.npz)."""
     if path.endswith(".npz"):

@@ -667,12 +667,15 @@ static double point_box(const double p[3], const double h[3], double nl[3], doub
     for (int k = 0; k < 3; k++) nl[k] = o[k] / l;
     return l;
   }
-  /* inside: deepest face is the one with max(|p_k| - h_k) */
+  /* inside: deepest face is the one with max(|p_k| - h_k); ties (within
+     1 um) go to the lower axis and, for a point on the mid-plane of the box
+     (a capsule pushed right through a thin box), to the + face -- the
+     kernel's rule, so fp32 and fp64 pick the same face */
   int best = 0;
   double g = fabs(p[0]) - h[0];
   for (int k = 1; k < 3; k++)
-    if (fabs(p[k]) - h[k] > g) { g = fabs(p[k]) - h[k]; best = k; }
-  double sg = p[best] >= 0 ? 1.0 : -1.0;
+    if (fabs(p[k]) - h[k] > g + 1e-6) { g = fabs(p[k]) - h[k]; best = k; }
+  double sg = p[best] >= -1e-6 ? 1.0 : -1.0;
   nl[0] = nl[1] = nl[2] = 0;
   nl[best] = -sg;
   memcpy(q, p, 3 * sizeof(double));
@@ -908,43 +911,57 @@ static void col_box_box(const odata* d, int ga, int gb, const double* ha, const 
 
 /* world support point of geom g along dir (any length); *hint: hull vertex the
    previous query on this geom ended at (-1: none), where the climb starts */
+/* ties in the support mapping resolve the same way in fp32 and fp64: a box /
+   capsule / cylinder axis with |l_k| < SUP_TIE |l| contributes its face (or
+   segment) centre, 0, instead of the sign of rounding noise; the hull climb
+   only moves to a neighbour that beats the current vertex by more than
+   SUP_BAND metres (coplanar vertices are ties) */
+#define SUP_TIE 1e-6
+#define SUP_BAND 1e-6
+static double tie_sign(double lk, double ln) { return fabs(lk) < SUP_TIE * ln ? 0.0 : (lk >= 0 ? 1.0 : -1.0); }
+
+/* world support point of geom g along dir (any length); *hint: hull vertex the
+   previous query on this geom ended at (-1: none), where the climb starts */
 static void support(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint) {
   const double* R = d->geom_xmat[g];
   const double* sz = m->geom_size[g];
   double l[3], p[3] = {0, 0, 0};
   mulmtv(l, R, dir);
+  const double ln = norm3(l);
   switch (m->geom_type[g]) {
     case MPCR_GEOM_SPHERE: {
-      double n = norm3(l);
-      if (n > 0) for (int k = 0; k < 3; k++) p[k] = sz[0] * l[k] / n;
+      if (ln > 0) for (int k = 0; k < 3; k++) p[k] = sz[0] * l[k] / ln;
       break;
     }
     case MPCR_GEOM_CAPSULE: {
-      double n = norm3(l);
-      if (n > 0) for (int k = 0; k < 3; k++) p[k] = sz[0] * l[k] / n;
-      p[2] += l[2] >= 0 ? sz[1] : -sz[1];
+      if (ln > 0) for (int k = 0; k < 3; k++) p[k] = sz[0] * l[k] / ln;
+      p[2] += tie_sign(l[2], ln) * sz[1];
       break;
     }
     case MPCR_GEOM_CYLINDER: {
       double r = sqrt(l[0] * l[0] + l[1] * l[1]);
-      if (r > 0) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
-      p[2] = l[2] >= 0 ? sz[1] : -sz[1];
+      if (r > SUP_TIE * ln) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
+      p[2] = tie_sign(l[2], ln) * sz[1];
       break;
     }
     case MPCR_GEOM_BOX:
-      for (int k = 0; k < 3; k++) p[k] = l[k] >= 0 ? sz[k] : -sz[k];
+      for (int k = 0; k < 3; k++) p[k] = tie_sign(l[k], ln) * sz[k];
       break;
     case MPCR_GEOM_MESH: { /* steepest-ascent hill climbing on the hull graph from its first vertex */
       int v = *hint >= 0 ? *hint : m->geom_hulladr[g];
-      double best = dot3(m->hull_vert[v], l);
+      double lu[3] = {0, 0, 0};
+      if (ln > 0) for (int k = 0; k < 3; k++) lu[k] = l[k] / ln;
+      double best = dot3(m->hull_vert[v], lu);
       for (;;) {
         int nb = v;
+        double bn = best + SUP_BAND; /* a neighbour must beat this; ties within the band go to the first */
         for (int k = m->hull_adjadr[v]; k < m->hull_adjadr[v] + m->hull_adjnum[v]; k++) {
           int u = m->hull_adj[k];
-          double du = dot3(m->hull_vert[u], l);
-          if (du > best) { best = du; nb = u; }
+          double du = dot3(m->hull_vert[u], lu);
+          if (du > bn) { bn = du + SUP_BAND; nb = u; }
         }
         if (nb == v) break;
+        best = bn - SUP_BAND;
         v = nb;
       }
       memcpy(p, m->hull_vert[v], sizeof(p));
@@ -961,8 +978,13 @@ typedef struct { double v[3], a[3], b[3]; } mpt; /* v = a - b */
 
 #define MPR_TOL 1e-6
 #define MPR_ITER 50
-#define MPR_EPS 2.220446049250313e-16
+/* zero tests in metres (the kernel's kMprEps): lengths below 1.2e-7 m, two
+   vectors parallel when one passes within it of the other's line, a point on
+   a plane within it -- libccd tests lengths, areas and volumes against
+   DBL_EPSILON alike, which cannot carry over to the fp32 kernel */
+#define MPR_EPS 1.1920929e-07
 static int iszero(double x) { return fabs(x) < MPR_EPS; }
+static int off_plane(double x, const double c[3]) { return fabs(x) >= MPR_EPS * sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]); }
 
 static void msupport(const mpcr_model_t* m, const odata* d, int g1, int g2, const double dir[3], mpt* o, int hint[2]) {
   double nd[3] = {-dir[0], -dir[1], -dir[2]};
@@ -1022,8 +1044,15 @@ static void tri_closest(const double a[3], const double b[3], const double c[3],
     for (int k = 0; k < 3; k++) out[k] = b[k] + t * (c[k] - b[k]);
     return;
   }
-  double den = 1 / (va + vb + vc), v = vb * den, w = vc * den;
-  for (int k = 0; k < 3; k++) out[k] = a[k] + ab[k] * v + ac[k] * w;
+  /* face region: the plane projection n (n.a) / |n|^2 -- Ericson's
+     barycentric a + v ab + w ac loses the answer to cancellation in fp32
+     when the triangle is large against its distance from the origin (MPR's
+     final portal: cm-sized around a sub-mm penetration); the kernel does the same */
+  double n[3];
+  cross3(n, ab, ac);
+  double s = dot3(n, a) / dot3(n, n);
+  for (int k = 0; k < 3; k++) out[k] = n[k] * s;
+  (void)va; (void)vb; (void)vc;
 }
 
 /* MPR penetration of geoms g1, g2: 1 and (depth, dir from g1 to g2, pos) if
@@ -1045,7 +1074,8 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
   dd = dot3(p[1].v, dir);
   if (iszero(dd) || dd < 0) return 0;
   cross3(dir, p[0].v, p[1].v);
-  if (iszero(dot3(dir, dir))) {
+  double thr = MPR_EPS * (norm3(p[0].v) + norm3(p[1].v));
+  if (dot3(dir, dir) < thr * thr) { /* v1 on the ray from v0 through the origin */
     for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p[1].a[k] + p[1].b[k]);
     if (iszero(p[1].v[0]) && iszero(p[1].v[1]) && iszero(p[1].v[2])) { /* touching at v1 */
       *depth = 0;
@@ -1076,11 +1106,11 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
     int cont = 0;
     cross3(va, p[1].v, p[3].v);
     dd = dot3(va, p[0].v);
-    if (dd < 0 && !iszero(dd)) { p[2] = p[3]; cont = 1; }
+    if (dd < 0 && off_plane(dd, va)) { p[2] = p[3]; cont = 1; }
     if (!cont) {
       cross3(va, p[3].v, p[2].v);
       dd = dot3(va, p[0].v);
-      if (dd < 0 && !iszero(dd)) { p[1] = p[3]; cont = 1; }
+      if (dd < 0 && off_plane(dd, va)) { p[1] = p[3]; cont = 1; }
     }
     if (!cont) break;
     for (int k = 0; k < 3; k++) { va[k] = p[1].v[k] - p[0].v[k]; vb[k] = p[2].v[k] - p[0].v[k]; }
@@ -1108,14 +1138,17 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
       if (iszero(*depth)) dir[0] = dir[1] = dir[2] = 0;
       else for (int k = 0; k < 3; k++) dir[k] = w[k] / *depth;
       /* barycentric position of the origin in the tetrahedron (libccd findPos) */
-      double pd[3], b[4], x[3];
-      portal_dir(p, pd);
+      double pd[3], b[4], x[3], e1[3], e2[3];
+      for (int k = 0; k < 3; k++) { e1[k] = p[2].v[k] - p[1].v[k]; e2[k] = p[3].v[k] - p[1].v[k]; }
+      cross3(pd, e1, e2); /* portal normal, |pd| = twice the portal's area */
       cross3(x, p[2].v, p[3].v); b[0] = dot3(x, p[1].v);
       cross3(x, p[3].v, p[2].v); b[1] = dot3(x, p[0].v);
       cross3(x, p[0].v, p[1].v); b[2] = dot3(x, p[3].v);
       cross3(x, p[2].v, p[1].v); b[3] = dot3(x, p[0].v);
       double sum = b[0] + b[1] + b[2] + b[3];
-      if (iszero(sum) || sum < 0) {
+      /* sum = 6 x the tetrahedron's volume: degenerate when v0 lies on the portal's plane */
+      if (!off_plane(sum, pd) || sum < 0) {
+        normalize3(pd);
         b[0] = 0;
         cross3(x, p[2].v, p[3].v); b[1] = dot3(x, pd);
         cross3(x, p[3].v, p[1].v); b[2] = dot3(x, pd);
@@ -1874,6 +1907,30 @@ int oracle_step(const mpcr_model_t* m, double* qpos, double* qvel, double* qacc_
   int trunc = d->efc_trunc;
   free(d);
   return trunc ? 1 : 0;
+}
+
+/* parity debugging: world geom poses at qpos (xpos 3, xmat 9 per geom) and
+   the oracle's MPR on one pair (out: hit, depth, dir 3, pos 3) */
+int oracle_geom_poses(const mpcr_model_t* m, const double* qpos, double* xpos, double* xmat, int pair,
+                      double* mpr_out) {
+  odata* d = (odata*)calloc(1, sizeof(odata));
+  if (!d) return -1;
+  memcpy(d->qpos, qpos, sizeof(double) * m->nq);
+  reset_hints(d);
+  kinematics(m, d);
+  for (int g = 0; g < m->ngeom; g++) {
+    memcpy(xpos + 3 * g, d->geom_xpos[g], 3 * sizeof(double));
+    memcpy(xmat + 9 * g, d->geom_xmat[g], 9 * sizeof(double));
+  }
+  if (pair >= 0 && mpr_out) {
+    double depth = 0, dir[3] = {0, 0, 0}, pos[3] = {0, 0, 0};
+    mpr_out[0] = mpr(m, d, m->pair_geom1[pair], m->pair_geom2[pair], &depth, dir, pos, d->hint[pair]);
+    mpr_out[1] = depth;
+    memcpy(mpr_out + 2, dir, sizeof(dir));
+    memcpy(mpr_out + 5, pos, sizeof(pos));
+  }
+  free(d);
+  return 0;
 }
 
 /* uniform in [-1, 1) from (seed, candidate, step, index): splitmix64 */

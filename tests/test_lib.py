@@ -76,3 +76,65 @@ def test_engine_without_gpu_fails_loudly():
     _, _, Pd, _ = basis.planner_basis(20, 0.05)
     with pytest.raises(_lib.MpcrError):
         Engine(models.load("planner_scene", 0.05), 20, 8, Pd)
+
+
+def test_c_host_loads_mjcf(tmp_path):
+    """§8b: a host with no Python of its own loads a scene from its MJCF
+    through the C ABI (mpcr_model_load on an .xml path -> the embedded
+    compiler of libmpcr_mjcf.so), replacing MjModel.from_xml_path
+    (SBP/mjx_planner.py:100-103).  The sizes match the Python compiler's."""
+    import shutil
+    import subprocess
+
+    from manipulator_mujoco_amd import mjcf
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("no C compiler")
+    exe = tmp_path / "mjcf_host"
+    subprocess.run([gcc, "-O1", "-o", str(exe), os.path.join(ROOT, "tests", "c_host", "mjcf_host.c"), "-ldl"],
+                   check=True)
+    xml = tmp_path / "scene.xml"
+    xml.write_text("""<mujoco><option timestep="0.01"/><worldbody>
+      <geom name="floor" type="plane" size="1 1 0.1"/>
+      <body name="a" pos="0 0 0.5"><joint type="hinge" axis="0 1 0"/><geom type="capsule" size="0.05 0.2"/>
+        <body name="b" pos="0 0 0.4"><joint type="slide" axis="1 0 0" range="-0.1 0.1"/><geom type="box" size="0.05 0.05 0.05"/></body>
+      </body></worldbody></mujoco>""")
+    libpath = os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr.so")
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    r = subprocess.run([str(exe), libpath, str(xml), "0.05"], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    m = mjcf.compile_mjcf(str(xml), 0.05)
+    assert r.stdout.strip() == f"nq={m.nq} nv={m.nv} nslot={m.nslot} nctrl={m.nctrl} npair={m.npair}"
+    # a broken file comes back as an error code, not a crash
+    bad = tmp_path / "bad.xml"
+    bad.write_text("<mujoco><worldbody><body></mujoco>")
+    r = subprocess.run([str(exe), libpath, str(bad), "0.05"], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 5 and "MJCF" in r.stderr
+
+
+def test_mjcf_load_through_ctypes(tmp_path):
+    """The same entry from a Python host (ctypes): the blob the embedded
+    compiler returns equals the Python compiler's struct byte for byte."""
+    from manipulator_mujoco_amd import mjcf
+    xml = tmp_path / "s.xml"
+    xml.write_text('<mujoco><worldbody><body pos="0 0 1"><freejoint/><geom type="sphere" size="0.1"/></body>'
+                   '</worldbody></mujoco>')
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    _lib.check(lib.mpcr_model_load(str(xml).encode(), 0.02, ctypes.byref(h)))
+    info = [ctypes.c_int() for _ in range(5)]
+    _lib.check(lib.mpcr_model_info(h, *(ctypes.byref(x) for x in info)))
+    m = mjcf.compile_mjcf(str(xml), 0.02)
+    assert [x.value for x in info] == [m.nq, m.nv, m.nslot, m.nctrl, m.npair]
+    lib.mpcr_model_free(h)
+    assert mjcf.compile_blob(str(xml), 0.02) == bytes(m.to_struct())
+
+
+def test_mjcf_library_exports_its_header():
+    src = open(os.path.join(ROOT, "include", "mpcr_mjcf.h")).read()
+    names = re.findall(r"^(?:int|void)\s+(mpcr_[a-z_]+)\s*\(", src, flags=re.M)
+    so = ctypes.CDLL(os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr_mjcf.so"))
+    assert names == ["mpcr_mjcf_compile", "mpcr_mjcf_free"]
+    for n in names:
+        assert hasattr(so, n), n

@@ -82,6 +82,33 @@ def main():
             qpos, qvel, ws = st["qpos"], st["qvel"], st["qacc_warmstart"]
         rec["steps"] = steps
         worst = sorted(steps, key=lambda s: -s["qacc_err"] / s["qacc_scale"])[:4]
+        # the worst step in detail: contacts that differ between the plant and the oracle
+        tw = worst[0]["t"]
+        qpos = np.array(m.qpos_init[:m.nq], dtype=np.float64)
+        qpos[qa] = pu.Q0
+        qvel = np.array(m.qvel_init[:m.nv], dtype=np.float64)
+        ws = np.zeros(m.nv)
+        for t in range(tw):
+            qv = qvel.copy()
+            qv[da] = v[:, t]
+            st = oracle.step(m, qpos, qv, ws)
+            qpos, qvel, ws = st["qpos"], st["qvel"], st["qacc_warmstart"]
+        qv = qvel.copy()
+        qv[da] = v[:, tw]
+        od = oracle.step_debug(m, qpos, qv, ws)
+        plant.set_state(qpos=qpos, qvel=qv, qacc_warmstart=ws)
+        gd = plant.step_debug(v[:, tw])
+        G = m.names["geom"]
+        print(f"  step {tw}: ncon g {gd['ncon']} o {od['ncon']}, solver g {np.round(gd['info'], 4)} o {np.round(od['info'], 4)}")
+        for k in range(min(gd["ncon"], od["ncon"])):
+            dn = np.abs(gd["con_normal"][k] - od["con_normal"][k]).max()
+            dp = np.abs(gd["con_pos"][k] - od["con_pos"][k]).max()
+            if dn > 1e-3 or dp > 1e-4 or gd["con_pair"][k] != od["con_pair"][k]:
+                p_ = int(od["con_pair"][k])
+                print(f"    con {k} pair g{gd['con_pair'][k]} o{p_} ({G[m.pair_geom1[p_]]}:{m.geom_type[m.pair_geom1[p_]]}-"
+                      f"{G[m.pair_geom2[p_]]}:{m.geom_type[m.pair_geom2[p_]]} func {m.pair_func[p_]}) "
+                      f"d g {gd['con_dist'][k]:.6e} o {od['con_dist'][k]:.6e} n g {np.round(gd['con_normal'][k], 4)} "
+                      f"o {np.round(od['con_normal'][k], 4)} pos g {np.round(gd['con_pos'][k], 5)} o {np.round(od['con_pos'][k], 5)}")
         print(f"cand {c}: gpu {rec['cost_gpu']:.6f} oracle {rec['cost_oracle']:.6f} "
               f"parts g{np.round(rec['parts_gpu'], 5)} o{np.round(rec['parts_oracle'], 5)} "
               f"first theta err step {rec['first_step_theta_err_gt_1e-5']}; worst resynced steps "

@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-2 measurement session on one MI355X: bench lines (C3 default, C2,
+# C4 with the elite exchange, C3 strong-scaling mode on 1 GPU), the rocprofv3
+# kernel-trace summary of the default bench command, and the PMC passes
+# (FETCH_SIZE, WRITE_SIZE, SQ instruction counters) -- each pass its own run.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/r02
+mkdir -p $OUT
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "[session] $name: $*"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[session] $name rc=$rc"; tail -3 "$OUT/$name.log"
+  if fatal $rc; then echo "[session] fatal rc=$rc in $name, stopping"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-bench,prof,pmc}
+if [[ $STEPS == *bench* ]]; then
+  run bench_c3 300 python bench.py
+  run bench_c2 300 python bench.py --config c2
+  run bench_c4 300 python bench.py --config c4 --no-cpu-baseline --steps 5 --warmup 1
+  run bench_c3_strong 300 python bench.py --scaling strong --no-cpu-baseline
+fi
+if [[ $STEPS == *prof* ]]; then
+  run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 10 --warmup 2
+fi
+if [[ $STEPS == *pmc* ]]; then
+  i=0
+  for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    run pmc$i 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
+  done
+fi
+echo "[session] done"

@@ -17,7 +17,10 @@ PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rn
 
 def main():
     so = os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr_prof.so")
-    build.compile_lib(so, ["-DMPCR_PROFILE"])
+    if "--build" in sys.argv:  # build here (CPU container), run on the GPU box
+        build.compile_lib(so, ["-DMPCR_PROFILE"])
+        print(so)
+        return
     _lib.LIB_PATH = so
     lib = _lib.load()
     lib.mpcr_rollout_profile.restype = ctypes.c_int
@@ -28,6 +31,7 @@ def main():
     from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine
     from manipulator_mujoco_amd.projection import ProjectionFilter
     name = sys.argv[1] if len(sys.argv) > 1 else "scene_mjx"
+    out = sys.argv[2] if len(sys.argv) > 2 else None
     n, H = int(os.environ.get("N", 4096)), int(os.environ.get("H", 50))
     m = models.load(name, 0.05)
     _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
@@ -49,6 +53,13 @@ def main():
         print(f"  {p:16s} {ph[i] / n / H:10.0f} cyc  {100 * ph[i] / tot:5.1f}%")
     print(f"  Newton iterations per step: {(ph[15] & 0xFFFFFFFF) / n / H:.2f}, line-search passes per step: "
           f"{(ph[15] >> 32) / n / H:.2f} (steps with constraints only)")
+    if out:
+        import json
+        with open(out, "w") as fh:
+            json.dump({"model": name, "n": n, "H": H, "cycles_per_wave_step": tot / n / H,
+                       "phases": {p: {"cycles": ph[i] / n / H, "share": ph[i] / tot} for i, p in enumerate(PHASES)},
+                       "newton_iters_per_step": (ph[15] & 0xFFFFFFFF) / n / H,
+                       "ls_passes_per_step": (ph[15] >> 32) / n / H}, fh, indent=1)
 
 
 if __name__ == "__main__":
