@@ -82,7 +82,7 @@ def load():
     lib.mpcr_plant_get_state.argtypes = [vp, P(d), P(d), P(d), P(d)]
     lib.mpcr_plant_step.argtypes = [vp, P(d), i, vp]
     lib.mpcr_rollout_occupancy.argtypes = [i, P(i)]
-    lib.mpcr_plant_step_debug.argtypes = [vp, P(d), vp]
+    lib.mpcr_plant_step_debug.argtypes = [vp, P(d), vp, i]
     lib.mpcr_plant_dbg_size.argtypes = []
     for name in EXPORTS + ("mpcr_rollout_trace", "mpcr_plant_step_debug", "mpcr_plant_dbg_size"):
         if name not in _VOID:

@@ -964,7 +964,7 @@ extern "C" int mpcr_plant_step(mpcr_plant* p, const double* qvel_ctrl, int commi
 // dbg_host (mpcr_plant_dbg_size() floats; layout DBG_* of rollout.h, the
 // oracle's oracle_step_debug writes the same).
 extern "C" int mpcr_plant_dbg_size(void) { return DBG_N; }
-extern "C" int mpcr_plant_step_debug(mpcr_plant* p, const double* qvel_ctrl, float* dbg_host) {
+extern "C" int mpcr_plant_step_debug(mpcr_plant* p, const double* qvel_ctrl, float* dbg_host, int mpr_pair) {
   if (!p || !qvel_ctrl || !dbg_host) return fail(MPCR_EINVAL, "bad debug step arguments");
   mpcr_engine* e = p->e;
   HIPCHK(hipSetDevice(e->device));
@@ -974,6 +974,8 @@ extern "C" int mpcr_plant_step_debug(mpcr_plant* p, const double* qvel_ctrl, flo
   float* d_dbg = nullptr;
   HIPCHK(hipMalloc(&d_dbg, sizeof(float) * DBG_N));
   HIPCHK(hipMemset(d_dbg, 0, sizeof(float) * DBG_N));
+  const float pf = (float)mpr_pair;  // the pair whose MPR the kernel traces (DBG_MPR), -1: none
+  HIPCHK(hipMemcpy(d_dbg + DBG_MPR, &pf, sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p->d_in, v, sizeof(float) * nc, hipMemcpyHostToDevice));
   Launch l;
   l.layout = MPCR_LAYOUT_THETADOT; l.n = 1; l.in = p->d_in; l.cost4 = p->d_cost;

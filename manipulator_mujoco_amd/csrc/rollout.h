@@ -24,7 +24,11 @@ enum { PAR_Q0 = 0, PAR_W = 8, PAR_PT = 12, PAR_QT = 16, PAR_N = 20 };
 // constraint rows (D, aref, vel), qacc_smooth, the final qacc
 enum { DBG_NCON = 0, DBG_NEFC = 1, DBG_CON = 2, DBG_MAXCON = 32, DBG_ROW = DBG_CON + 8 * DBG_MAXCON, DBG_MAXROW = 136,
        DBG_QAS = DBG_ROW + 3 * DBG_MAXROW, DBG_QACC = DBG_QAS + DX_NV, DBG_INFO = DBG_QACC + DX_NV,
-       DBG_GRAD = DBG_INFO + 8, DBG_SRCH = DBG_GRAD + DX_NV, DBG_N = DBG_SRCH + DX_NV };
+       DBG_GRAD = DBG_INFO + 8, DBG_SRCH = DBG_GRAD + DX_NV, DBG_MPR = DBG_SRCH + DX_NV, DBG_N = DBG_MPR + 112 };
+// DBG_MPR: the host puts a pair index in [0]; the kernel's MPR on that pair writes [1] hit, [2] depth,
+// [3..5] dir, [6..8] pos, [9..11] phase counts (discovery, refinement, penetration), [12..47] the final
+// portal's v / a / b of vertices 0..3 (4 x 9), [48..111] the hull vertices (side 0, side 1) after each of
+// the first 32 support queries
 // DBG_INFO: warm start taken, its cost, qacc_smooth's cost, first iteration's p0 cost, alpha, line-search
 // passes, the final bracket's best cost, Newton iterations run
 enum { ST_QPOS = 0, ST_QVEL = DX_NQ, ST_QWS = ST_QVEL + DX_NV, ST_QACC = ST_QWS + DX_NV, ST_EEF = ST_QACC + DX_NV,

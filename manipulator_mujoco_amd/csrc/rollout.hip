@@ -446,12 +446,12 @@ __device__ __forceinline__ float point_box(const float p[3], const float h[3], f
 // (libccd MPR; one penetration contact per pair)
 
 #ifndef MPCR_MPR_TOL
-#define MPCR_MPR_TOL 1e-6f
+#define MPCR_MPR_TOL 1e-5f  // the oracle's MPR_TOL (see there: not MuJoCo's 1e-6)
 #endif
 #ifndef MPCR_MPR_ITER
 #define MPCR_MPR_ITER 50
 #endif
-constexpr float kMprTol = MPCR_MPR_TOL;  // MuJoCo's ccd_tolerance / ccd_iterations defaults
+constexpr float kMprTol = MPCR_MPR_TOL;  // gap tolerance (oracle MPR_TOL); MuJoCo ccd_iterations cap below
 constexpr int kMprIter = MPCR_MPR_ITER;
 constexpr float kMprEps = 1.1920929e-07f;
 __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
@@ -463,7 +463,7 @@ __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
 // metres along the unit direction (coplanar vertices are ties, the first in
 // list order wins).
 constexpr float kSupTie = 1e-6f;
-constexpr float kSupBand = 1e-6f;
+constexpr float kSupBand = 1e-5f;
 __device__ __forceinline__ float tie_sign(float lk, float ln) {
   return fabsf(lk) < kSupTie * ln ? 0.f : (lk >= 0.f ? 1.f : -1.f);
 }
@@ -503,9 +503,12 @@ __device__ __forceinline__ int climb_round(const DevModel* __restrict__ m, int v
 
 // hint: hull vertex the previous query on this geom ended at (-1: none); the
 // climb starts there (successive MPR directions are close)
+// org (nullable): the result relative to org, with (geom centre - org)
+// formed first -- MPR works relative to the second geom's centre, so the
+// Minkowski points carry cm-scale rounding instead of world-scale (1 m) rounding
 template <class S>
 __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
-                                             float out[3], int& hint) {
+                                             float out[3], int& hint, const float* org = nullptr) {
   const float* R = s.gxmat[g];
   const float* sz = m->geom_size[g];
   float l[3], p[3] = {0.f, 0.f, 0.f};
@@ -538,18 +541,26 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
     hint = v;
   }
   mv(out, R, p);
-  out[0] += s.gxpos[g][0]; out[1] += s.gxpos[g][1]; out[2] += s.gxpos[g][2];
+  if (org) {
+    out[0] += s.gxpos[g][0] - org[0]; out[1] += s.gxpos[g][1] - org[1]; out[2] += s.gxpos[g][2] - org[2];
+  } else {
+    out[0] += s.gxpos[g][0]; out[1] += s.gxpos[g][1]; out[2] += s.gxpos[g][2];
+  }
 }
 
 struct MprPt { float v[3], a[3], b[3]; };
 
 template <class S>
 __device__ __forceinline__ void mpr_support(const DevModel* __restrict__ m, const S& s, int g1, int g2,
-                                            const float dir[3], MprPt& o, int (&hint)[2]) {
+                                            const float dir[3], MprPt& o, int (&hint)[2], float* trace = nullptr) {
   const float nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support_geom(m, s, g1, dir, o.a, hint[0]);
-  support_geom(m, s, g2, nd, o.b, hint[1]);
+  support_geom(m, s, g1, dir, o.a, hint[0], s.gxpos[g2]);  // relative to g2's centre
+  support_geom(m, s, g2, nd, o.b, hint[1], s.gxpos[g2]);
   o.v[0] = o.a[0] - o.b[0]; o.v[1] = o.a[1] - o.b[1]; o.v[2] = o.a[2] - o.b[2];
+  if (trace) {
+    const int q = (int)trace[47];
+    if (q < 32) { trace[48 + 2 * q] = (float)hint[0]; trace[49 + 2 * q] = (float)hint[1]; trace[47] = (float)(q + 1); }
+  }
 }
 __device__ __forceinline__ void nrm3(float v[3]) {
   const float n = sqrtf(dot3(v, v));
@@ -561,10 +572,10 @@ __device__ __forceinline__ void mpr_dir(const MprPt p[4], float dir[3]) {
   cross(dir, a, b);
   nrm3(dir);
 }
-__device__ __forceinline__ bool mpr_reach(const MprPt p[4], const MprPt& v4, const float dir[3]) {
+__device__ __forceinline__ bool mpr_reach(const MprPt p[4], const MprPt& v4, const float dir[3], float tol) {
   const float d4 = dot3(v4.v, dir);
   const float t = fminf(d4 - dot3(p[1].v, dir), fminf(d4 - dot3(p[2].v, dir), d4 - dot3(p[3].v, dir)));
-  return fabsf(t - kMprTol) < kMprEps || t < kMprTol;
+  return t < tol;
 }
 __device__ __forceinline__ void mpr_expand(MprPt p[4], const MprPt& v4) {
   float x[3];
@@ -624,21 +635,22 @@ __device__ __forceinline__ void tri_closest(const float a[3], const float b[3], 
 // the other's line, and a point lies on a plane within kMprEps of it.
 template <class S>
 __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int g2, float& depth, float dir[3],
-                         float pos[3], int (&hint)[2]) {
+                         float pos[3], int (&hint)[2], float* trace = nullptr) {
   MprPt p[4], v4;
   float va[3], vb[3], dd;
+  const float tol = kMprTol;
   // point x off the plane through the origin with (unnormalised) normal c by more than kMprEps
   auto off_plane = [](float x, const float c[3]) { return fabsf(x) >= kMprEps * sqrtf(dot3(c, c)); };
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
-    p[0].a[k] = s.gxpos[g1][k];
-    p[0].b[k] = s.gxpos[g2][k];
-    p[0].v[k] = p[0].a[k] - p[0].b[k];
+  for (int k = 0; k < 3; k++) {  // the frame of the Minkowski points: origin at g2's centre
+    p[0].a[k] = s.gxpos[g1][k] - s.gxpos[g2][k];
+    p[0].b[k] = 0.f;
+    p[0].v[k] = p[0].a[k];
   }
   if (mpr_zero(p[0].v[0]) && mpr_zero(p[0].v[1]) && mpr_zero(p[0].v[2])) p[0].v[0] += 10.f * kMprEps;
   dir[0] = -p[0].v[0]; dir[1] = -p[0].v[1]; dir[2] = -p[0].v[2];
   nrm3(dir);
-  mpr_support(m, s, g1, g2, dir, p[1], hint);
+  mpr_support(m, s, g1, g2, dir, p[1], hint, trace);
   dd = dot3(p[1].v, dir);
   if (mpr_zero(dd) || dd < 0.f) return false;
   cross(dir, p[0].v, p[1].v);
@@ -646,7 +658,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     const float thr = kMprEps * (sqrtf(dot3(p[0].v, p[0].v)) + sqrtf(dot3(p[1].v, p[1].v)));
     if (dot3(dir, dir) < thr * thr) {  // v1 on the ray from v0 through the origin
 #pragma unroll
-      for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].a[k] + p[1].b[k]);
+      for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p[1].a[k] + p[1].b[k]) + s.gxpos[g2][k];
       if (mpr_zero(p[1].v[0]) && mpr_zero(p[1].v[1]) && mpr_zero(p[1].v[2])) {
         depth = 0.f;
         dir[0] = dir[1] = dir[2] = 0.f;
@@ -659,7 +671,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     }
   }
   nrm3(dir);
-  mpr_support(m, s, g1, g2, dir, p[2], hint);
+  mpr_support(m, s, g1, g2, dir, p[2], hint, trace);
   dd = dot3(p[2].v, dir);
   if (mpr_zero(dd) || dd < 0.f) return false;
 #pragma unroll
@@ -672,7 +684,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   }
   for (int guard = 0;; guard++) {
     if (guard > kMprIter) return false;
-    mpr_support(m, s, g1, g2, dir, p[3], hint);
+    mpr_support(m, s, g1, g2, dir, p[3], hint, trace);
     dd = dot3(p[3].v, dir);
     if (mpr_zero(dd) || dd < 0.f) return false;
     bool cont = false;
@@ -684,6 +696,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
       dd = dot3(va, p[0].v);
       if (dd < 0.f && off_plane(dd, va)) { p[1] = p[3]; cont = true; }
     }
+    if (trace) trace[9] = (float)guard;
     if (!cont) break;
 #pragma unroll
     for (int k = 0; k < 3; k++) { va[k] = p[1].v[k] - p[0].v[k]; vb[k] = p[2].v[k] - p[0].v[k]; }
@@ -691,20 +704,29 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     nrm3(dir);
   }
   for (int it = 0;; it++) {
+    if (trace) trace[10] = (float)it;
     mpr_dir(p, dir);
     dd = dot3(dir, p[1].v);
     if (mpr_zero(dd) || dd > 0.f) break;
-    mpr_support(m, s, g1, g2, dir, v4, hint);
+    mpr_support(m, s, g1, g2, dir, v4, hint, trace);
     dd = dot3(v4.v, dir);
-    if (!(mpr_zero(dd) || dd > 0.f) || mpr_reach(p, v4, dir) || it > kMprIter) return false;
+    if (!(mpr_zero(dd) || dd > 0.f) || mpr_reach(p, v4, dir, tol) || it > kMprIter) return false;
     mpr_expand(p, v4);
   }
   for (int it = 0;; it++) {
+    if (trace) trace[11] = (float)it;
     mpr_dir(p, dir);
-    mpr_support(m, s, g1, g2, dir, v4, hint);
-    if (mpr_reach(p, v4, dir) || it > kMprIter) break;
+    mpr_support(m, s, g1, g2, dir, v4, hint, trace);
+    if (mpr_reach(p, v4, dir, tol) || it > kMprIter) break;
     mpr_expand(p, v4);
   }
+  if (trace)
+    for (int i = 0; i < 4; i++)
+      for (int k = 0; k < 3; k++) {
+        trace[12 + 9 * i + k] = p[i].v[k];
+        trace[12 + 9 * i + 3 + k] = p[i].a[k];
+        trace[12 + 9 * i + 6 + k] = p[i].b[k];
+      }
   float w[3];
   tri_closest(p[1].v, p[2].v, p[3].v, w);
   depth = sqrtf(dot3(w, w));
@@ -735,7 +757,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     float pa = 0.f, pb = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; i++) { pa += b[i] * p[i].a[k]; pb += b[i] * p[i].b[k]; }
-    pos[k] = 0.5f * (pa + pb) / sum;
+    pos[k] = 0.5f * (pa + pb) / sum + s.gxpos[g2][k];
   }
   return true;
 }
@@ -834,7 +856,7 @@ __device__ __noinline__ int plane_mesh_manifold(const DevModel* __restrict__ m, 
 // wave-cooperative, below).  out: dist[4], pos[4][3], nrm[4][3]
 template <class S>
 __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const S& s, short* hints, int p, float dist[4],
-                            float pos[4][3], float nrm[4][3]) {
+                            float pos[4][3], float nrm[4][3], float* dbg = nullptr) {
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   const int func = m->pair_func[p];
   const float* x1 = s.gxpos[g1];
@@ -1040,7 +1062,12 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
     int hint[2] = {(int)(short)(hv & 0xffff), hv >> 16};
     if (func == 9) {  // general convex (MPR)
       float depth, n[3], pp[3];
-      const bool hit = mpr_lane(m, s, g1, g2, depth, n, pp, hint);
+      float* tr = (dbg && (int)dbg[DBG_MPR] == p) ? dbg + DBG_MPR : nullptr;
+      const bool hit = mpr_lane(m, s, g1, g2, depth, n, pp, hint, tr);
+      if (tr) {
+        tr[1] = hit ? 1.f : 0.f; tr[2] = depth;
+        tr[3] = n[0]; tr[4] = n[1]; tr[5] = n[2]; tr[6] = pp[0]; tr[7] = pp[1]; tr[8] = pp[2];
+      }
       *hp = (hint[0] & 0xffff) | (hint[1] << 16);
       if (hit) {
         if (n[0] == 0.f && n[1] == 0.f && n[2] == 0.f) n[2] = 1.f;
@@ -2216,7 +2243,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             const bool v = i0 + lane < nc;
             const int pc = v ? s.cvx[i0 + lane] : 0;
             float cd[4] = {1e30f, 1e30f, 1e30f, 1e30f}, cp[4][3] = {}, cn[4][3] = {};
-            const int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn) : 0;
+            const int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn, (args.dbg && b == 0 && t == H - 1) ? args.dbg
+                                                                                                     : nullptr)
+                                : 0;
             emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c);
           }
           sync();

@@ -229,7 +229,7 @@ class Plant:
         check(_lib.load().mpcr_plant_step(self.handle, None if v is None else v.ctypes.data_as(dp), 1, None))
         self._pull()
 
-    def step_debug(self, qvel_ctrl):
+    def step_debug(self, qvel_ctrl, mpr_pair=-1):
         """step() that also returns the step's active contacts, constraint-row
         parameters, qacc_smooth and qacc (``parse_step_debug``; parity
         debugging, mpcr_plant_step_debug)."""
@@ -237,7 +237,7 @@ class Plant:
         buf = np.zeros(lib.mpcr_plant_dbg_size(), dtype=np.float32)
         v = np.ascontiguousarray(qvel_ctrl, dtype=np.float64).reshape(self.nctrl)
         check(lib.mpcr_plant_step_debug(self.handle, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-                                        buf.ctypes.data_as(ctypes.c_void_p)))
+                                        buf.ctypes.data_as(ctypes.c_void_p), int(mpr_pair)))
         self._pull()
         return parse_step_debug(buf, self.nv)
 
@@ -269,4 +269,5 @@ def parse_step_debug(buf, nv):
                 qacc_smooth=buf[q0:q0 + nv], qacc=buf[q0 + DBG_NV:q0 + DBG_NV + nv],
                 info=buf[q0 + 2 * DBG_NV:q0 + 2 * DBG_NV + 8],
                 grad=buf[q0 + 2 * DBG_NV + 8:q0 + 2 * DBG_NV + 8 + nv],
-                search=buf[q0 + 3 * DBG_NV + 8:q0 + 3 * DBG_NV + 8 + nv])
+                search=buf[q0 + 3 * DBG_NV + 8:q0 + 3 * DBG_NV + 8 + nv],
+                mpr=buf[q0 + 4 * DBG_NV + 8:q0 + 4 * DBG_NV + 8 + 112])

@@ -917,12 +917,20 @@ static void col_box_box(const odata* d, int ga, int gb, const double* ha, const 
    only moves to a neighbour that beats the current vertex by more than
    SUP_BAND metres (coplanar vertices are ties) */
 #define SUP_TIE 1e-6
-#define SUP_BAND 1e-6
+#define SUP_BAND 1e-5
 static double tie_sign(double lk, double ln) { return fabs(lk) < SUP_TIE * ln ? 0.0 : (lk >= 0 ? 1.0 : -1.0); }
 
 /* world support point of geom g along dir (any length); *hint: hull vertex the
    previous query on this geom ended at (-1: none), where the climb starts */
+static void support_rel(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint,
+                        const double* org);
 static void support(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint) {
+  support_rel(m, d, g, dir, out, hint, NULL);
+}
+/* org (nullable): the support point relative to org, (geom centre - org)
+   formed first (MPR works relative to the second geom's centre, as the kernel) */
+static void support_rel(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint,
+                        const double* org) {
   const double* R = d->geom_xmat[g];
   const double* sz = m->geom_size[g];
   double l[3], p[3] = {0, 0, 0};
@@ -971,12 +979,20 @@ static void support(const mpcr_model_t* m, const odata* d, int g, const double d
     default: break;
   }
   mulmv(out, R, p);
-  for (int k = 0; k < 3; k++) out[k] += d->geom_xpos[g][k];
+  for (int k = 0; k < 3; k++) out[k] += org ? d->geom_xpos[g][k] - org[k] : d->geom_xpos[g][k];
 }
 
 typedef struct { double v[3], a[3], b[3]; } mpt; /* v = a - b */
 
-#define MPR_TOL 1e-6
+/* MPR's gap tolerance: 1e-5 m, not MuJoCo's ccd_tolerance 1e-6.  The
+   refinement stops when a new support point gains less than tol over the
+   portal; near the end the portal faces of two mesh hulls differ in normal by
+   0.01-0.05 rad, so the answer hinges on which side of tol the last gap
+   lands.  fp32 computes those gaps to ~3e-8 m (1e-7 on metre-sized boxes):
+   at 1e-6 that decided a visible share of the dual arm's rollouts
+   differently in the kernel and here, at 1e-5 it rarely does; the depth it
+   leaves is within 1e-5 m of converged (both sides use the same value) */
+#define MPR_TOL 1e-5
 #define MPR_ITER 50
 /* zero tests in metres (the kernel's kMprEps): lengths below 1.2e-7 m, two
    vectors parallel when one passes within it of the other's line, a point on
@@ -988,8 +1004,8 @@ static int off_plane(double x, const double c[3]) { return fabs(x) >= MPR_EPS * 
 
 static void msupport(const mpcr_model_t* m, const odata* d, int g1, int g2, const double dir[3], mpt* o, int hint[2]) {
   double nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support(m, d, g1, dir, o->a, &hint[0]);
-  support(m, d, g2, nd, o->b, &hint[1]);
+  support_rel(m, d, g1, dir, o->a, &hint[0], d->geom_xpos[g2]);
+  support_rel(m, d, g2, nd, o->b, &hint[1], d->geom_xpos[g2]);
   for (int k = 0; k < 3; k++) o->v[k] = o->a[k] - o->b[k];
 }
 static void normalize3(double v[3]) {
@@ -1002,10 +1018,10 @@ static void portal_dir(const mpt p[4], double dir[3]) {
   cross3(dir, a, b);
   normalize3(dir);
 }
-static int reach_tol(const mpt p[4], const mpt* v4, const double dir[3]) {
+static int reach_tol(const mpt p[4], const mpt* v4, const double dir[3], double tol) {
   double d4 = dot3(v4->v, dir);
   double t = fmin(d4 - dot3(p[1].v, dir), fmin(d4 - dot3(p[2].v, dir), d4 - dot3(p[3].v, dir)));
-  return fabs(t - MPR_TOL) < MPR_EPS || t < MPR_TOL;
+  return t < tol;
 }
 static void expand(mpt p[4], const mpt* v4) {
   double x[3];
@@ -1059,13 +1075,14 @@ static void tri_closest(const double a[3], const double b[3], const double c[3],
    they overlap, else 0 */
 static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* depth, double dir[3], double pos[3],
                int* hint) {
+  const double tol = MPR_TOL;
   mpt p[4], v4;
   double va[3], vb[3], dd;
   /* phase 1: portal discovery; v0 = interior point of the difference */
   for (int k = 0; k < 3; k++) {
-    p[0].a[k] = d->geom_xpos[g1][k];
-    p[0].b[k] = d->geom_xpos[g2][k];
-    p[0].v[k] = p[0].a[k] - p[0].b[k];
+    p[0].a[k] = d->geom_xpos[g1][k] - d->geom_xpos[g2][k]; /* frame origin: g2's centre */
+    p[0].b[k] = 0;
+    p[0].v[k] = p[0].a[k];
   }
   if (iszero(p[0].v[0]) && iszero(p[0].v[1]) && iszero(p[0].v[2])) p[0].v[0] += 10 * MPR_EPS;
   for (int k = 0; k < 3; k++) dir[k] = -p[0].v[k];
@@ -1076,7 +1093,7 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
   cross3(dir, p[0].v, p[1].v);
   double thr = MPR_EPS * (norm3(p[0].v) + norm3(p[1].v));
   if (dot3(dir, dir) < thr * thr) { /* v1 on the ray from v0 through the origin */
-    for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p[1].a[k] + p[1].b[k]);
+    for (int k = 0; k < 3; k++) pos[k] = 0.5 * (p[1].a[k] + p[1].b[k]) + d->geom_xpos[g2][k];
     if (iszero(p[1].v[0]) && iszero(p[1].v[1]) && iszero(p[1].v[2])) { /* touching at v1 */
       *depth = 0;
       dir[0] = dir[1] = dir[2] = 0;
@@ -1124,14 +1141,14 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
     if (iszero(dd) || dd > 0) break;
     msupport(m, d, g1, g2, dir, &v4, hint);
     dd = dot3(v4.v, dir);
-    if (!(iszero(dd) || dd > 0) || reach_tol(p, &v4, dir) || it > MPR_ITER) return 0;
+    if (!(iszero(dd) || dd > 0) || reach_tol(p, &v4, dir, tol) || it > MPR_ITER) return 0;
     expand(p, &v4);
   }
   /* phase 3: penetration depth / direction / position */
   for (int it = 0;; it++) {
     portal_dir(p, dir);
     msupport(m, d, g1, g2, dir, &v4, hint);
-    if (reach_tol(p, &v4, dir) || it > MPR_ITER) {
+    if (reach_tol(p, &v4, dir, tol) || it > MPR_ITER) {
       double w[3];
       tri_closest(p[1].v, p[2].v, p[3].v, w);
       *depth = norm3(w);
@@ -1158,7 +1175,7 @@ static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* de
       for (int k = 0; k < 3; k++) {
         double pa = 0, pb = 0;
         for (int i = 0; i < 4; i++) { pa += b[i] * p[i].a[k]; pb += b[i] * p[i].b[k]; }
-        pos[k] = 0.5 * (pa + pb) / sum;
+        pos[k] = 0.5 * (pa + pb) / sum + d->geom_xpos[g2][k];
       }
       return 1;
     }
@@ -1712,7 +1729,12 @@ static void solve(const mpcr_model_t* m, odata* d) {
     double gn = 0;
     for (int i = 0; i < nv; i++) gn += grad[i] * grad[i];
     gn = sqrt(gn);
-    if (it >= m->iterations || scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance) break;
+    /* MuJoCo's stop test, plus the kernel's fp32 resolution floor (an
+       improvement within 1e-6 of the cost ends the solve): the same rule on
+       both sides, so neither iterates where the other cannot */
+    if (it >= m->iterations || scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance ||
+        prev_cost - cost <= 1e-6 * fabs(cost))
+      break;
     for (int i = 0; i < nv; i++)
       for (int j = 0; j < nv; j++) {
         double h = d->M[i][j];
@@ -1777,6 +1799,8 @@ static void solve(const mpcr_model_t* m, odata* d) {
       if (it == 0) d->dbg[5] = ls;
       if (lo.d0 < 0 && lo.d0 > -gtol) break;
       if (hi.d0 > 0 && hi.d0 < gtol) break;
+      /* the kernel's bracket floor: closed to 1e-6 relative */
+      if (fabs(hi.alpha - lo.alpha) <= 1e-6 * fmax(fabs(lo.alpha), fabs(hi.alpha))) break;
       lspt lo_next = ls_eval(d, qg, jar, jv, lo.alpha - lo.d0 / lo.d1);
       lspt hi_next = ls_eval(d, qg, jar, jv, hi.alpha - hi.d0 / hi.d1);
       lspt mid = ls_eval(d, qg, jar, jv, 0.5 * (lo.alpha + hi.alpha));

