@@ -32,7 +32,7 @@
  * PARITY STATUS: MuJoCo/MJX are not importable or buildable here
  * (SURVEY.md §0.2, §8c), so the physics restatement is pinned only by the
  * reference's own logged CPU-MuJoCo run (SBP/data/theta.csv + thetadot.csv,
- * tests/test_oracle_replay.py) and by analytic invariants; contact slot
+ * tests/test_oracle.py::test_replay_*) and by analytic invariants; contact slot
  * layout and solver details are "parity unpinned" (DESIGN.md §Oracle).
  */
 #include <math.h>
