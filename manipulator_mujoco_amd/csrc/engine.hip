@@ -69,6 +69,7 @@ struct mpcr_engine {
   int* d_idx = nullptr;
   float* d_slot_prev = nullptr;  // max_n x nslot (variants keeping cost_c history in HBM)
   float* d_jx = nullptr;         // max_n x (MAXEFC - JL) x LDJ: J rows past the LDS ones
+  float* d_td = nullptr;         // (max_n + 1) x nctrl x H joint-velocity table (thetadot not requested)
   short* d_hints = nullptr;      // max_n x NHINT x 2 (dual-arm class): hull-climb starts
   // convex hulls (dual-arm class)
   float4* d_hull_vert = nullptr;
@@ -690,7 +691,9 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
                               (e->wide ? (SmemW::MAXEFC - SmemW::JL + 1) * SmemW::LDJ
                                        : (SmemN::MAXEFC - SmemN::JL + 1) * SmemN::LDJ)) !=
           hipSuccess ||
-      hipMalloc(&e->d_hints, sizeof(short) * 2 * (size_t)max_n * (e->wide ? SmemW::NHINT : 1)) != hipSuccess) {
+      hipMalloc(&e->d_hints, sizeof(short) * 2 * (size_t)max_n * (e->wide ? SmemW::NHINT : 1)) != hipSuccess ||
+      hipMalloc(&e->d_td, sizeof(float) * ((size_t)max_n + 1) * (size_t)(e->host.nctrl > 0 ? e->host.nctrl : 1) *
+                              (size_t)horizon) != hipSuccess) {
     mpcr_engine_free(e);
     return fail(MPCR_ENOMEM, "device allocation failed");
   }
@@ -718,6 +721,7 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_idx);
   (void)hipFree(e->d_slot_prev);
   (void)hipFree(e->d_jx);
+  (void)hipFree(e->d_td);
   (void)hipFree(e->d_hints);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
@@ -762,6 +766,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.trace_slots = l.trace_slots;
   a.slot_prev = e->d_slot_prev;
   a.jx = e->d_jx;
+  a.tdscratch = e->d_td;
   a.hints = e->d_hints;
   a.dpar = l.dpar;
   a.state = l.state;
@@ -1040,6 +1045,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
   a.slot_prev = e->d_slot_prev;
   a.jx = e->d_jx;
+  a.tdscratch = e->d_td;
   a.hints = e->d_hints;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);

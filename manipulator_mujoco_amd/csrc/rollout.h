@@ -49,6 +49,7 @@ struct RolloutArgs {
   float* jx;           // n x (MAXEFC - JL) x LDJ: J rows past the LDS ones
   short* hints;        // n x NHINT x 2: hull-climb start per convex pair and side (dual-arm class)
   unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
+  float* tdscratch;  // (n + 1) x nctrl x H: the joint-velocity table when thetadot is not requested
   float* dbg;  // parity debugging (mpcr_plant_step_debug): candidate 0's last step, DBG_* layout
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs

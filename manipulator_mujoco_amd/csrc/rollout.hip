@@ -36,6 +36,18 @@ namespace mpcr {
 #define STAMP(i)
 #define PROF_FLUSH
 #endif
+#ifndef MPCR_TD_TABLE
+#define MPCR_TD_TABLE 1
+#endif
+// instruction-count attribution builds (-DMPCR_STOP_AFTER=k, diagnostic only):
+// the step ends right after phase stamp k, so PMC differences between k and
+// the previous stop are that phase's instructions
+#ifdef MPCR_STOP_AFTER
+#define STOP_AT(k) \
+  if (MPCR_STOP_AFTER == (k)) continue;
+#else
+#define STOP_AT(k)
+#endif
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -1717,6 +1729,32 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   if (lane < nc && !from_state) s.qpos[m->ctrl_qposadr[lane]] = s.par[PAR_Q0 + lane];
   sync();
 
+#if MPCR_TD_TABLE
+  // the candidate's joint velocities for the whole horizon, computed up front
+  // by all lanes (theta_dot = A_thetadot xi, SBP/mjx_planner.py:348) into the
+  // thetadot output (or a scratch row); each step then reads its value with a
+  // load issued one step ahead, so no per-step basis latency is exposed
+  const float* tdp;
+  if (args.layout == 0) {
+    float* tdw = (args.thetadot && live ? args.thetadot : args.tdscratch) + (size_t)b * nc * H;
+    for (int idx = lane; idx < nc * H; idx += S::HL) {
+      const int j = idx / H, tt = idx - j * H;
+      const float* pd = args.pdot + (size_t)tt * args.nbasis;
+      const float* xj = args.input + ((size_t)bi * nc + j) * args.nbasis;
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 12; k++)
+        if (k < args.nbasis) v = fmaf(pd[k], xj[k], v);
+      tdw[idx] = v;
+    }
+    __threadfence_block();
+    sync();
+    tdp = tdw;
+  } else {
+    tdp = args.input + (size_t)bi * nc * H;
+  }
+  float vnext = lane < nc ? tdp[lane * H] : 0.f;
+#else
   // lane j < nctrl keeps joint j's Bernstein coefficients in registers for
   // the whole horizon (nbasis <= 12, checked by the engine)
   float xir[12];
@@ -1724,6 +1762,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   for (int k = 0; k < 12; k++)
     xir[k] = (args.layout == 0 && lane < nc && k < args.nbasis)
                  ? args.input[((size_t)bi * nc + lane) * args.nbasis + k] : 0.f;
+#endif
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
   int status = 0, nefc_sum = 0, nefc_max = 0;
   PROF_DECL
@@ -1735,7 +1774,15 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     // stay in their phases and hit L1/L2.
     LAUNDER_MODEL();
     if constexpr (!WIDE && MPCR_LANE_LAUNDER) LAUNDER_LANE();
-    // ---- qvel[:nctrl] = thetadot_t (basis evaluated on the fly) -------------
+    // ---- qvel[:nctrl] = thetadot_t ----------------------------------------------
+#if MPCR_TD_TABLE
+    if (lane < nc) {
+      const float v = vnext;
+      if (t + 1 < H) vnext = tdp[lane * H + t + 1];  // next step's, in flight during this one
+      s.qvel[m->ctrl_dofadr[lane]] = v;
+      if (args.layout != 0 && args.thetadot && live) args.thetadot[(size_t)b * nc * H + lane * H + t] = v;
+    }
+#else
     if (lane < nc) {
       float v;
       if (args.layout == 0) {
@@ -1750,9 +1797,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       s.qvel[m->ctrl_dofadr[lane]] = v;
       if (args.thetadot && live) args.thetadot[(size_t)b * nc * H + lane * H + t] = v;
     }
+#endif
     sync();
 
     STAMP(0);
+    STOP_AT(0)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- kinematics: local pose per body, then pointer jumping ----------------
     {
@@ -1828,6 +1877,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     sync();
 
     STAMP(1);
+    STOP_AT(1)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- geom poses, tree COMs ------------------------------------------------
     if (lane < m->ngeom) {
@@ -1930,6 +1980,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     }
 
     STAMP(2);
+    STOP_AT(2)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- cinert, cdof (+ actuator forces) -------------------------------------
     if constexpr (S::WIDE) {
@@ -2019,6 +2070,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     sync();
 
     STAMP(3);
+    STOP_AT(3)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- CRB, velocity, RNE + gravcomp (subtree sums by bitmask) -----------
     for (int idx = lane; idx < nb * 10; idx += S::HL) {
@@ -2107,6 +2159,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     }
     sync();
     STAMP(4);
+    STOP_AT(4)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // mass matrix entries (chain-masked) + bias forces
     for (int idx = lane; idx < NVW * NVW; idx += S::HL) {
@@ -2152,6 +2205,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     sync();
 
     STAMP(5);
+    STOP_AT(5)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
     {
@@ -2172,6 +2226,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     }
 
     STAMP(6);
+    STOP_AT(6)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
     //      slots; active contacts compacted into the list; box-box pairs
@@ -2262,6 +2317,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     }
 
     STAMP(7);
+    STOP_AT(7)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- constraint rows: equality, limits, contacts ------------------------
     {
@@ -2528,6 +2584,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     nefc_max = max(nefc_max, s.nefc);
 
     STAMP(8);
+    STOP_AT(8)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- Newton solver (primal), MJX-style line search ------------------------
     {
@@ -2576,6 +2633,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         if (lane < NVW) s.qacc[lane] = qacc_l;
         sync();
         STAMP(13);
+        STOP_AT(13)
         const float scale = 1.f / (m->meaninertia * (float)(nv > 1 ? nv : 1));
         float prev_cost = 3.4e38f;
         for (int it = 0;; it++) {
@@ -2791,6 +2849,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 
     if (args.dbg && b == 0 && t == H - 1 && lane < NVW) args.dbg[DBG_QACC + lane] = s.qacc[lane];
     STAMP(9);
+    STOP_AT(9)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- implicitfast (dual-arm class): (M + dt D) a = qfrc_smooth + J^T f at
     //      the final qacc; the velocity update uses a, the warm start qacc --
