@@ -2260,7 +2260,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
               run = sqrtf(o2) <= m->geom_rbound[b1 ? g2 : g1] + m->pair_margin[p];
             }
           }
-        } else if constexpr (S::WIDE) {  // plane vs the other geom's bounding sphere
+        } else {  // plane vs the other geom's bounding sphere (C3: the box far above the floor)
           const float* R1 = s.gxmat[g1];
           run = R1[2] * dx + R1[5] * dy + R1[8] * dz <= m->geom_rbound[g2] + m->pair_margin[p];
         }
