@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 #define MPCR_MODEL_MAGIC   0x4d504352u /* 'MPCR' */
-#define MPCR_MODEL_VERSION 5
+#define MPCR_MODEL_VERSION 6
 
 #define MPCR_MAX_BODY   48
 #define MPCR_MAX_JNT    40
@@ -38,6 +38,8 @@ extern "C" {
 #define MPCR_MAX_ACT    16   /* actuators */
 #define MPCR_MAX_HULLV  8192 /* convex-hull vertices of all collision meshes */
 #define MPCR_MAX_HULLA  49152 /* hull-graph adjacency entries */
+#define MPCR_LUT_R      16    /* support start table: 6 cube faces x R x R cells per hull */
+#define MPCR_MAX_HULLLUT (24 * 6 * MPCR_LUT_R * MPCR_LUT_R) /* 24 hulls */
 #define MPCR_MAX_TEN    4    /* spatial (site-site) tendons with limits */
 
 /* joint types (MuJoCo mjtJoint) */
@@ -249,6 +251,12 @@ typedef struct mpcr_model_t {
   double ten_solimp[MPCR_MAX_TEN][5];
   double ten_margin[MPCR_MAX_TEN];
   double ten_invweight0[MPCR_MAX_TEN]; /* J_ten M^-1 J_ten^T at qpos0 */
+  /* support start table of every hull (derived from hull_vert when packed):
+     the local direction's cube-map cell (mpcr_lut_cell) names the vertex
+     extreme along the cell centre; hull climbs start there (or at the
+     query's hint if that beats it by the tie band) */
+  int32_t geom_lutadr[MPCR_MAX_GEOM]; /* first cell, -1: no hull          */
+  int32_t hull_lut[MPCR_MAX_HULLLUT];  /* global vertex index per cell     */
 } mpcr_model_t;
 
 #ifdef __cplusplus

@@ -3,10 +3,12 @@
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -75,6 +77,8 @@ struct mpcr_engine {
   float4* d_hull_vert = nullptr;
   int2* d_hull_info = nullptr;
   float4* d_hull_adjv = nullptr;
+  float4* d_hull_head = nullptr;
+  float4* d_hull_lut = nullptr;
   bool wide = false;  // kernel variant: rollout_kernel<32, 32, 72, true>
 };
 
@@ -139,9 +143,19 @@ static int check_model(const mpcr_model_t& m) {
   if (m.density != 0) return fail(MPCR_EMODEL, "fluid density (inertia-box drag terms) not supported");
   if (m.viscosity != 0 && m.integrator != MPCR_INT_EULER)
     return fail(MPCR_EMODEL, "fluid viscosity with implicit integration not supported");
-  for (int g = 0; g < m.ngeom; g++)
+  for (int g = 0; g < m.ngeom; g++) {
     if (m.geom_hulladr[g] >= 0 && m.geom_hulladr[g] + m.geom_hullnum[g] > m.nhullv)
       return fail(MPCR_EMODEL, "geom %d hull outside the vertex table", g);
+    if (m.geom_hulladr[g] >= 0 && m.geom_hullnum[g] > 0) {  // the support start table (cmodel.hull_luts)
+      const int la = m.geom_lutadr[g], nc = 6 * MPCR_LUT_R * MPCR_LUT_R;
+      if (la < 0 || la + nc > MPCR_MAX_HULLLUT) return fail(MPCR_EMODEL, "geom %d has no hull start table", g);
+      for (int c = 0; c < nc; c++) {
+        const int v = m.hull_lut[la + c];
+        if (v < m.geom_hulladr[g] || v >= m.geom_hulladr[g] + m.geom_hullnum[g])
+          return fail(MPCR_EMODEL, "geom %d start table names vertex %d outside its hull", g, v);
+      }
+    }
+  }
   for (int v = 0; v < m.nhullv; v++)
     if (m.hull_adjadr[v] < 0 || m.hull_adjadr[v] + m.hull_adjnum[v] > m.nhulla)
       return fail(MPCR_EMODEL, "hull vertex %d adjacency outside the table", v);
@@ -469,6 +483,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.geom_rbound[i] = (float)m.geom_rbound[g];
     d.geom_hulladr[i] = m.geom_hulladr[g];
     d.geom_hullnum[i] = m.geom_hullnum[g];
+    d.geom_lutadr[i] = m.geom_lutadr[g];
     for (int k = 0; k < 3; k++) d.geom_size[i][k] = (float)m.geom_size[g][k];
     if (dmap[b] >= 0) {
       d.geom_body[i] = dmap[b];
@@ -648,22 +663,38 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     std::vector<float4> hv(h.nhullv);
     std::vector<int2> hi(h.nhullv);
     std::vector<float4> ha(h.nhulla);
-    for (int k = 0; k < h.nhulla; k++) {
-      const int u = h.hull_adj[k];
-      int bits = u;
-      float fu;
-      std::memcpy(&fu, &bits, 4);
-      ha[k] = make_float4((float)h.hull_vert[u][0], (float)h.hull_vert[u][1], (float)h.hull_vert[u][2], fu);
+    std::vector<float4> hh((size_t)h.nhullv * 8);
+    if (h.nhullv > 65535) {
+      mpcr_engine_free(e);
+      return fail(MPCR_EINVAL, "%d hull vertices: the climb records hold 16-bit vertex indices", h.nhullv);
     }
+    auto bitsf = [](int bits) {
+      float f;
+      std::memcpy(&f, &bits, 4);
+      return f;
+    };
+    // neighbour record: xyz | index | degree << 16 -- the chosen neighbour's
+    // own adjacency is then addressed without another dependent load
+    auto rec = [&](int u) {
+      return make_float4((float)h.hull_vert[u][0], (float)h.hull_vert[u][1], (float)h.hull_vert[u][2],
+                         bitsf(u | (h.hull_adjnum[u] << 16)));
+    };
+    for (int k = 0; k < h.nhulla; k++) ha[k] = rec(h.hull_adj[k]);
+    const float nan = std::numeric_limits<float>::quiet_NaN();
     for (int v = 0; v < h.nhullv; v++) {
-      hv[v] = make_float4((float)h.hull_vert[v][0], (float)h.hull_vert[v][1], (float)h.hull_vert[v][2], 0.f);
+      hv[v] = make_float4((float)h.hull_vert[v][0], (float)h.hull_vert[v][1], (float)h.hull_vert[v][2],
+                          bitsf(h.hull_adjnum[v]));
       hi[v] = make_int2(h.hull_adjadr[v], h.hull_adjnum[v]);
+      for (int j = 0; j < 8; j++)  // NaN pads never beat the current vertex
+        hh[(size_t)v * 8 + j] = j < h.hull_adjnum[v] ? rec(h.hull_adj[h.hull_adjadr[v] + j]) : make_float4(nan, nan, nan, bitsf(-1));
     }
     if (hipMalloc(&e->d_hull_vert, sizeof(float4) * hv.size()) != hipSuccess ||
         hipMalloc(&e->d_hull_info, sizeof(int2) * hi.size()) != hipSuccess ||
         hipMalloc(&e->d_hull_adjv, sizeof(float4) * (ha.size() ? ha.size() : 1)) != hipSuccess ||
+        hipMalloc(&e->d_hull_head, sizeof(float4) * hh.size()) != hipSuccess ||
         hipMemcpy(e->d_hull_vert, hv.data(), sizeof(float4) * hv.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(e->d_hull_info, hi.data(), sizeof(int2) * hi.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_hull_head, hh.data(), sizeof(float4) * hh.size(), hipMemcpyHostToDevice) != hipSuccess ||
         (ha.size() && hipMemcpy(e->d_hull_adjv, ha.data(), sizeof(float4) * ha.size(), hipMemcpyHostToDevice) != hipSuccess)) {
       mpcr_engine_free(e);
       return fail(MPCR_ENOMEM, "hull upload failed");
@@ -671,6 +702,21 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     e->dev.hull_vert = e->d_hull_vert;
     e->dev.hull_info = e->d_hull_info;
     e->dev.hull_adjv = e->d_hull_adjv;
+    e->dev.hull_head = e->d_hull_head;
+    std::vector<float4> hl(MPCR_MAX_HULLLUT);
+    int nlut = 0;
+    for (int g = 0; g < h.ngeom; g++)
+      if (h.geom_hulladr[g] >= 0 && h.geom_hullnum[g] > 0) {
+        const int la = h.geom_lutadr[g], nc = 6 * MPCR_LUT_R * MPCR_LUT_R;
+        for (int c = 0; c < nc; c++) hl[la + c] = rec(h.hull_lut[la + c]);
+        nlut = std::max(nlut, la + nc);
+      }
+    if (hipMalloc(&e->d_hull_lut, sizeof(float4) * (nlut ? nlut : 1)) != hipSuccess ||
+        (nlut && hipMemcpy(e->d_hull_lut, hl.data(), sizeof(float4) * nlut, hipMemcpyHostToDevice) != hipSuccess)) {
+      mpcr_engine_free(e);
+      return fail(MPCR_ENOMEM, "hull table upload failed");
+    }
+    e->dev.hull_lut = e->d_hull_lut;
   }
   const int nc = e->host.nctrl;
   const size_t in_cols = (size_t)nc * (horizon > nbasis ? horizon : nbasis);
@@ -726,6 +772,8 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
   (void)hipFree(e->d_hull_adjv);
+  (void)hipFree(e->d_hull_head);
+  (void)hipFree(e->d_hull_lut);
   delete e;
 }
 
@@ -1032,13 +1080,15 @@ extern "C" int mpcr_rollout_trace(mpcr_engine* e, const float* input, int layout
 // diagnostic build only: per-phase s_memtime cycles summed over all waves
 extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
                                     const float* w, const float* ptgt, const float* qtgt,
-                                    unsigned long long* phases16) {
+                                    unsigned long long* phases16 /* 24 slots */) {
   HIPCHK(hipSetDevice(e->device));
   const int nc = e->host.nctrl;
   const size_t cols = layout == MPCR_LAYOUT_XI ? (size_t)nc * e->nbasis : (size_t)nc * e->H;
   unsigned long long* d_prof = nullptr;
-  HIPCHK(hipMalloc(&d_prof, 16 * sizeof(unsigned long long)));
-  HIPCHK(hipMemset(d_prof, 0, 16 * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&d_prof, 24 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(d_prof, 0, 24 * sizeof(unsigned long long)));
+  e->dev.prof = d_prof;  // wave-level counters for this launch only
+  HIPCHK(hipMemcpy(e->d_model, &e->dev, sizeof(DevModel), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice));
   RolloutArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1051,7 +1101,9 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(phases16, d_prof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(phases16, d_prof, 24 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  e->dev.prof = nullptr;
+  HIPCHK(hipMemcpy(e->d_model, &e->dev, sizeof(DevModel), hipMemcpyHostToDevice));
   (void)hipFree(d_prof);
   return MPCR_OK;
 }

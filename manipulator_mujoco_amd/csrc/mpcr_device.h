@@ -110,9 +110,14 @@ struct DevModel {
   // convex hulls of mesh geoms (geom frame), hill-climbing graph -----------------
   int geom_hulladr[DX_NG];
   int geom_hullnum[DX_NG];
-  const float4* hull_vert;  // xyz, w unused
+  int geom_lutadr[DX_NG];  // first hull_lut cell, -1: no table
+  const float4* hull_vert;  // xyz | degree (int bits in w)
   const int2* hull_info;    // (adjacency start, count) per vertex
-  const float4* hull_adjv;  // neighbour xyz | neighbour index (bits in w): one load per neighbour
+  const float4* hull_adjv;  // neighbour xyz | (index | degree << 16) (bits in w): one load per neighbour
+  const float4* hull_lut;   // support start table records (as hull_adjv), MPCR_LUT_R cube-map cells per hull
+  unsigned long long* prof;  // wave-level event counters (MPCR_PROFILE builds; else null)
+  const float4* hull_head;  // per vertex its first 8 neighbour records as hull_adjv, padded with NaN records:
+                            // a climb round addresses them from the vertex index alone (no hull_info load)
 
   int ctrl_qposadr[DX_NCTRL], ctrl_dofadr[DX_NCTRL];
 

@@ -15,13 +15,14 @@
 //   cost                     SBP/mjx_planner.py:276-303
 //   mjx.step                 mujoco-mjx 3.3.1 (third party)
 #include "rollout.h"
+#include "../../include/mpcr_model.h"  // MPCR_LUT_R (the hull start table layout)
 
 namespace mpcr {
 
 // ---------------------------------------------------------------------------
 // diagnostic phase stamps (separate -DMPCR_PROFILE build; never in the timed one)
 #ifdef MPCR_PROFILE
-#define PROF_DECL unsigned long long prof_acc[16] = {0}; unsigned long long prof_last = __builtin_amdgcn_s_memtime();
+#define PROF_DECL unsigned long long prof_acc[24] = {0}; unsigned long long prof_last = __builtin_amdgcn_s_memtime();
 #define STAMP(i)                                              \
   do {                                                        \
     unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
@@ -30,11 +31,17 @@ namespace mpcr {
   } while (0)
 #define PROF_FLUSH                                                          \
   if (lane == 0 && args.prof)                                               \
-    for (int i_ = 0; i_ < 16; i_++) atomicAdd(&args.prof[i_], prof_acc[i_]);
+    for (int i_ = 0; i_ < 24; i_++) atomicAdd(&args.prof[i_], prof_acc[i_]);
+// wave-level event counter (first active lane adds 1; diagnostic only)
+#define PROF_COUNT(m, i)                                                                  \
+  do {                                                                                    \
+    if ((m)->prof && (int)__lane_id() == __builtin_ctzll(__ballot(1))) atomicAdd((m)->prof + (i), 1ull); \
+  } while (0)
 #else
 #define PROF_DECL
 #define STAMP(i)
 #define PROF_FLUSH
+#define PROF_COUNT(m, i)
 #endif
 #ifndef MPCR_TD_TABLE
 #define MPCR_TD_TABLE 1
@@ -482,35 +489,52 @@ __device__ __forceinline__ float tie_sign(float lk, float ln) {
 
 // examine the neighbours of vertex v along l (unit): one must beat bn (the
 // current vertex + band, then the chosen neighbour + band); -1 if none.
-// The first 8 neighbours (90 % of hull vertices have <= 8) are 8 independent
-// loads issued together; the rest loop.
-__device__ __forceinline__ void climb_scan(const DevModel* __restrict__ m, const float4 (&w)[8], int k0, int end,
-                                           const float l[3], float& bn, float4& hv, int& nb) {
+// Neighbour records carry (index | degree << 16), so the next round's loads
+// need no lookup: the first 8 neighbours (90 % of hull vertices have <= 8)
+// sit in v's NaN-padded head block (addressed by v alone, 8 independent
+// loads), the rest of a longer list in hull_adjv after one hull_info load.
+__device__ __forceinline__ void climb_scan(const float4 (&w)[8], const float l[3], float& bn, float4& hv, int& nb) {
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    const float du = w[j].x * l[0] + w[j].y * l[1] + w[j].z * l[2];
-    if (k0 + j < end && du > bn) { bn = du + kSupBand; nb = __float_as_int(w[j].w); hv = w[j]; }
+    const float du = w[j].x * l[0] + w[j].y * l[1] + w[j].z * l[2];  // NaN pads never win
+    if (du > bn) { bn = du + kSupBand; nb = __float_as_int(w[j].w); hv = w[j]; }
   }
 }
-__device__ __forceinline__ void climb_load(const DevModel* __restrict__ m, int k0, int last, float4 (&w)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; j++) w[j] = m->hull_adjv[min(k0 + j, last)];
-}
-__device__ __forceinline__ int climb_round(const DevModel* __restrict__ m, int v, const float l[3], float& best,
-                                           float4& hv) {
-  const int2 info = m->hull_info[v];
-  const int end = info.x + info.y;
+__device__ __forceinline__ int climb_round(const DevModel* __restrict__ m, int v, int deg, const float l[3],
+                                           float& best, float4& hv) {
   int nb = -1;
   float bn = best + kSupBand;
   float4 w[8];
-  climb_load(m, info.x, end - 1, w);
-  climb_scan(m, w, info.x, end, l, bn, hv, nb);
-  for (int k0 = info.x + 8; k0 < end; k0 += 8) {
-    climb_load(m, k0, end - 1, w);
-    climb_scan(m, w, k0, end, l, bn, hv, nb);
+#pragma unroll
+  for (int j = 0; j < 8; j++) w[j] = m->hull_head[(size_t)v * 8 + j];
+  climb_scan(w, l, bn, hv, nb);
+  if (deg > 8) {
+    const int a = m->hull_info[v].x, last = a + deg - 1;
+    for (int k0 = a + 8; k0 <= last; k0 += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) w[j] = m->hull_adjv[min(k0 + j, last)];  // repeats of the last never win twice
+      climb_scan(w, l, bn, hv, nb);
+    }
   }
   if (nb >= 0) best = bn - kSupBand;
   return nb;
+}
+
+// cube-map cell of a local direction (the model's hull_lut order, oracle
+// lut_cell): major axis (lowest on ties), its sign, the other two components
+// (cyclic order) over |l_axis| in MPCR_LUT_R bins
+__device__ __forceinline__ int lut_cell(const float l[3]) {
+  const float a0 = fabsf(l[0]), a1 = fabsf(l[1]), a2 = fabsf(l[2]);
+  const int ax = (a0 >= a1 && a0 >= a2) ? 0 : (a1 >= a2 ? 1 : 2);
+  const float lax = ax == 0 ? l[0] : (ax == 1 ? l[1] : l[2]);
+  const float lu = ax == 0 ? l[1] : (ax == 1 ? l[2] : l[0]);
+  const float lv = ax == 0 ? l[2] : (ax == 1 ? l[0] : l[1]);
+  const float la = fabsf(lax);
+  if (!(la > 0.f)) return 0;
+  constexpr int R = MPCR_LUT_R;
+  const int iu = min(max((int)floorf((lu / la + 1.f) * 0.5f * R), 0), R - 1);
+  const int iv = min(max((int)floorf((lv / la + 1.f) * 0.5f * R), 0), R - 1);
+  return (2 * ax + (lax < 0.f ? 1 : 0)) * R * R + iu * R + iv;
 }
 
 // hint: hull vertex the previous query on this geom ended at (-1: none); the
@@ -541,13 +565,26 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
   } else if (type == 7) {  // mesh hull: steepest ascent on the vertex graph from its first vertex
     const float il = ln > 0.f ? 1.f / ln : 0.f;
     const float lu[3] = {l[0] * il, l[1] * il, l[2] * il};
-    int v = hint >= 0 ? hint : m->geom_hulladr[g];
-    float4 hv = m->hull_vert[v];
+    // start: the table vertex of l's cube-map cell, or the hint (where the
+    // previous query on this pair ended) when it beats that by the band --
+    // both loads issue together (the oracle's rule)
+    const int la = m->geom_lutadr[g];
+    float4 hv = la >= 0 ? m->hull_lut[la + lut_cell(l)] : m->hull_vert[m->geom_hulladr[g]];
+    int v = la >= 0 ? (__float_as_int(hv.w) & 0xffff) : m->geom_hulladr[g];
+    int deg = la >= 0 ? (__float_as_int(hv.w) >> 16) : __float_as_int(hv.w);
     float best = hv.x * lu[0] + hv.y * lu[1] + hv.z * lu[2];
+    if (hint >= 0) {
+      const float4 hh = m->hull_vert[hint];
+      const float bh = hh.x * lu[0] + hh.y * lu[1] + hh.z * lu[2];
+      if (bh > best + kSupBand) { v = hint; hv = hh; deg = __float_as_int(hh.w); best = bh; }
+    }
+    PROF_COUNT(m, 20);
     for (int guard = 0; guard < 4096; guard++) {
-      const int nb = climb_round(m, v, lu, best, hv);
+      PROF_COUNT(m, 19);
+      const int nb = climb_round(m, v, deg, lu, best, hv);
       if (nb < 0) break;
-      v = nb;
+      v = nb & 0xffff;
+      deg = nb >> 16;
     }
     p[0] = hv.x; p[1] = hv.y; p[2] = hv.z;
     hint = v;
@@ -2291,6 +2328,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           box_box_wave(m, s, k * S::HL + q - hbase<S::CPW>(), lane);
         }
       }
+      STAMP(16);
       if constexpr (S::WIDE) {
         if (s.ncvx > S::CVXN - WAVE || (k + 1) * S::HL >= m->npair) {  // flush (pair order is kept)
           const int nc = s.ncvx;
@@ -2301,7 +2339,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             const int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn, (args.dbg && b == 0 && t == H - 1) ? args.dbg
                                                                                                      : nullptr)
                                 : 0;
+            STAMP(17);
             emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c);
+            STAMP(18);
           }
           sync();
           if (lane == 0) s.ncvx = 0;

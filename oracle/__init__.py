@@ -35,6 +35,8 @@ def lib():
     global _LIB
     if _LIB is None:
         _LIB = ctypes.CDLL(build())
+        if os.environ.get("MPCR_ORACLE_CRASH_BT"):
+            _LIB.oracle_install_crash_bt()
         dp = ctypes.POINTER(ctypes.c_double)
         _LIB.oracle_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, dp,
                                         dp, dp, dp, ctypes.POINTER(ctypes.c_int), ctypes.c_double,

@@ -36,6 +36,9 @@
  * layout and solver details are "parity unpinned" (DESIGN.md §Oracle).
  */
 #include <math.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -922,6 +925,26 @@ static double tie_sign(double lk, double ln) { return fabs(lk) < SUP_TIE * ln ? 
 
 /* world support point of geom g along dir (any length); *hint: hull vertex the
    previous query on this geom ended at (-1: none), where the climb starts */
+/* cube-map cell of a local direction l (the model's hull_lut order): major
+   axis (lowest on ties), its sign, then the other two components (cyclic
+   order) over |l_axis| in R bins; the kernel's lut_cell in fp32 */
+static int lut_cell(const double l[3]) {
+  const double a0 = fabs(l[0]), a1 = fabs(l[1]), a2 = fabs(l[2]);
+  const int ax = (a0 >= a1 && a0 >= a2) ? 0 : (a1 >= a2 ? 1 : 2);
+  const double la = fabs(l[ax]);
+  if (!(la > 0)) return 0;
+  const int R = MPCR_LUT_R;
+  int iu = (int)floor((l[(ax + 1) % 3] / la + 1.0) * 0.5 * R), iv = (int)floor((l[(ax + 2) % 3] / la + 1.0) * 0.5 * R);
+  iu = iu < 0 ? 0 : (iu > R - 1 ? R - 1 : iu);
+  iv = iv < 0 ? 0 : (iv > R - 1 ? R - 1 : iv);
+  return (2 * ax + (l[ax] < 0)) * R * R + iu * R + iv;
+}
+
+/* MPR work counters of the calling thread (diagnostic: tools/mpr_stats.py, workers = 1):
+   0 calls, 1 support pairs, 2 climb rounds, 3 neighbour evaluations, 4 hits,
+   5 discovery iterations, 6 phase-2 iterations, 7 phase-3 iterations,
+   16.. histogram of support pairs per call (capped at 47) */
+static __thread long g_mpr_stats[64]; /* per thread: the checker's pool threads never share it */
 static void support_rel(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint,
                         const double* org);
 static void support(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint) {
@@ -955,13 +978,21 @@ static void support_rel(const mpcr_model_t* m, const odata* d, int g, const doub
     case MPCR_GEOM_BOX:
       for (int k = 0; k < 3; k++) p[k] = tie_sign(l[k], ln) * sz[k];
       break;
-    case MPCR_GEOM_MESH: { /* steepest-ascent hill climbing on the hull graph from its first vertex */
-      int v = *hint >= 0 ? *hint : m->geom_hulladr[g];
+    case MPCR_GEOM_MESH: { /* steepest-ascent hill climbing on the hull graph */
       double lu[3] = {0, 0, 0};
       if (ln > 0) for (int k = 0; k < 3; k++) lu[k] = l[k] / ln;
+      /* start: the table vertex of l's cube-map cell, or the hint (where the
+         previous query on this pair ended) when it beats that by the band */
+      int v = m->geom_lutadr[g] >= 0 ? m->hull_lut[m->geom_lutadr[g] + lut_cell(l)] : m->geom_hulladr[g];
       double best = dot3(m->hull_vert[v], lu);
+      if (*hint >= 0) {
+        const double bh = dot3(m->hull_vert[*hint], lu);
+        if (bh > best + SUP_BAND) { v = *hint; best = bh; }
+      }
       for (;;) {
         int nb = v;
+        g_mpr_stats[2]++;
+        g_mpr_stats[3] += m->hull_adjnum[v];
         double bn = best + SUP_BAND; /* a neighbour must beat this; ties within the band go to the first */
         for (int k = m->hull_adjadr[v]; k < m->hull_adjadr[v] + m->hull_adjnum[v]; k++) {
           int u = m->hull_adj[k];
@@ -1002,7 +1033,12 @@ typedef struct { double v[3], a[3], b[3]; } mpt; /* v = a - b */
 static int iszero(double x) { return fabs(x) < MPR_EPS; }
 static int off_plane(double x, const double c[3]) { return fabs(x) >= MPR_EPS * sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]); }
 
+void oracle_mpr_stats(long* out, int reset) {
+  if (out) memcpy(out, g_mpr_stats, sizeof(g_mpr_stats));
+  if (reset) memset(g_mpr_stats, 0, sizeof(g_mpr_stats));
+}
 static void msupport(const mpcr_model_t* m, const odata* d, int g1, int g2, const double dir[3], mpt* o, int hint[2]) {
+  g_mpr_stats[1]++;
   double nd[3] = {-dir[0], -dir[1], -dir[2]};
   support_rel(m, d, g1, dir, o->a, &hint[0], d->geom_xpos[g2]);
   support_rel(m, d, g2, nd, o->b, &hint[1], d->geom_xpos[g2]);
@@ -1073,8 +1109,20 @@ static void tri_closest(const double a[3], const double b[3], const double c[3],
 
 /* MPR penetration of geoms g1, g2: 1 and (depth, dir from g1 to g2, pos) if
    they overlap, else 0 */
+static int mpr_impl(const mpcr_model_t* m, const odata* d, int g1, int g2, double* depth, double dir[3],
+                    double pos[3], int* hint);
 static int mpr(const mpcr_model_t* m, const odata* d, int g1, int g2, double* depth, double dir[3], double pos[3],
                int* hint) {
+  const long s0 = g_mpr_stats[1];
+  const int hit = mpr_impl(m, d, g1, g2, depth, dir, pos, hint);
+  const long k = g_mpr_stats[1] - s0;
+  g_mpr_stats[0]++;
+  g_mpr_stats[4] += hit;
+  g_mpr_stats[16 + (k < 0 ? 0 : (k < 47 ? k : 47))]++;
+  return hit;
+}
+static int mpr_impl(const mpcr_model_t* m, const odata* d, int g1, int g2, double* depth, double dir[3],
+                    double pos[3], int* hint) {
   const double tol = MPR_TOL;
   mpt p[4], v4;
   double va[3], vb[3], dd;
@@ -2139,3 +2187,21 @@ int oracle_cone_eval(double mu, const double fri[2], const double D[3], const do
   free(d);
   return 0;
 }
+
+/* crash diagnostics (test infrastructure, MPCR_ORACLE_CRASH_BT=1 in oracle.lib()):
+   print the C backtrace of a fault in the oracle, then die with the signal */
+static void oracle_crash_bt(int sig) {
+  void* buf[64];
+  const int n = backtrace(buf, 64);
+  static const char msg[] = "oracle: fatal signal, C backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(buf, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+void oracle_install_crash_bt(void) {
+  signal(SIGSEGV, oracle_crash_bt);
+  signal(SIGILL, oracle_crash_bt);
+  signal(SIGBUS, oracle_crash_bt);
+}
+

@@ -13,6 +13,9 @@ from manipulator_mujoco_amd import _lib, basis, build, models  # noqa: E402
 PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rne", "M/bias", "M solve",
           "coll: box-box", "constraint rows", "newton: line search", "euler", "coll: narrow", "coll: cost+compact",
           "newton: warm start", "newton: grad/H/chol"]
+# slot 7 is the collision loop's tail (box-box moved to 16); 15 packs iteration counts
+EXTRA = {16: "coll: box-box (wave)", 17: "coll: convex narrow (MPR)", 18: "coll: convex emit"}
+COUNTS = {19: "hull-climb rounds (wave level)", 20: "mesh support calls (wave level)"}
 
 
 def main():
@@ -40,24 +43,30 @@ def main():
     xi = proj(torch.tensor(np.random.default_rng(20250632).normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32)),
               proj.boundary(q0, np.zeros(6), np.zeros(6), n), 10).numpy()
     e = Engine(m, H, n, Pd)
-    ph = (ctypes.c_ulonglong * 16)()
+    ph = (ctypes.c_ulonglong * 24)()
     f = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
     w, pt, qt = np.array([20, 3, 80.]), np.array([-0.3, -0.3, 0.5]), np.array([0, 1, 0, 0.])
     for _ in range(2):
-        ph = (ctypes.c_ulonglong * 16)()
+        ph = (ctypes.c_ulonglong * 24)()
         _lib.check(lib.mpcr_rollout_profile(e.handle, xi.ctypes.data, MPCR_LAYOUT_XI, n,
                                             q0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), f(w), f(pt), f(qt), ph))
-    tot = sum(ph[:15])
+    tot = sum(ph[:15]) + sum(ph[i] for i in EXTRA)
     print(f"{name}: n={n} H={H} cycles/wave-step {tot / n / H:.0f}")
-    for i, p in enumerate(PHASES):
-        print(f"  {p:16s} {ph[i] / n / H:10.0f} cyc  {100 * ph[i] / tot:5.1f}%")
+    names = dict(enumerate(PHASES))
+    names[7] = "coll: loop tail"
+    names.update(EXTRA)
+    for i, p in names.items():
+        print(f"  {p:26s} {ph[i] / n / H:10.0f} cyc  {100 * ph[i] / tot:5.1f}%")
+    for i, p in COUNTS.items():
+        print(f"  {p:34s} {ph[i] / n / H:8.2f} per wave-step")
     print(f"  Newton iterations per step: {(ph[15] & 0xFFFFFFFF) / n / H:.2f}, line-search passes per step: "
           f"{(ph[15] >> 32) / n / H:.2f} (steps with constraints only)")
     if out:
         import json
         with open(out, "w") as fh:
             json.dump({"model": name, "n": n, "H": H, "cycles_per_wave_step": tot / n / H,
-                       "phases": {p: {"cycles": ph[i] / n / H, "share": ph[i] / tot} for i, p in enumerate(PHASES)},
+                       "phases": {p: {"cycles": ph[i] / n / H, "share": ph[i] / tot} for i, p in names.items()},
+                       "counts": {p: ph[i] / n / H for i, p in COUNTS.items()},
                        "newton_iters_per_step": (ph[15] & 0xFFFFFFFF) / n / H,
                        "ls_passes_per_step": (ph[15] >> 32) / n / H}, fh, indent=1)
 
