@@ -465,6 +465,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.dof_damping[i] = no_passive ? 0.f : (float)m.dof_damping[i];
     d.dof_invweight0[i] = (float)m.dof_invweight0[i];
   }
+  for (int i = 0; i < m.nv; i++) d.dof_submask[i] = d.dof_body[i] >= 0 ? d.body_submask[d.dof_body[i]] : 0u;
   for (int i = 0; i < m.nq; i++) d.qpos_init[i] = (float)m.qpos_init[i];
   for (int i = 0; i < m.nv; i++) d.qvel_init[i] = (float)m.qvel_init[i];
   // collision geoms referenced by pairs
@@ -526,6 +527,9 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     for (int k = 0; k < 2; k++) d.pair_solref[p][k] = (float)m.pair_solref[p][k];
     for (int k = 0; k < 5; k++) d.pair_solimp[p][k] = (float)m.pair_solimp[p][k];
     d.pair_diag[p] = (float)(m.body_invweight0[m.geom_bodyid[g1]][0] + m.body_invweight0[m.geom_bodyid[g2]][0]);
+    const int b1 = d.geom_body[d.pair_g1[p]], b2 = d.geom_body[d.pair_g2[p]];
+    d.pair_jinfo[p] = make_int4(b1 >= 0 ? (int)d.body_dofmask[b1] : 0, b2 >= 0 ? (int)d.body_dofmask[b2] : 0,
+                                b1 >= 0 ? d.body_tree[b1] : 0, b2 >= 0 ? d.body_tree[b2] : 0);
   }
   // equalities: joint (1 row) and connect (3 rows), rows in model order
   int nrow = 0;

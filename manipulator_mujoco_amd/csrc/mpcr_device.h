@@ -69,6 +69,7 @@ struct DevModel {
   int dof_sub[DX_NV];            // free: axis index 0..2
   uint32_t dof_chainmask[DX_NV]; // dofs j with M[i][j] possibly nonzero (ancestors incl. self)
   uint32_t dof_velmask[DX_NV];   // dofs forming the velocity cdof_dot uses
+  uint32_t dof_submask[DX_NV];   // bodies in the subtree of the dof's body (bias force sum)
   float dof_armature[DX_NV], dof_damping[DX_NV], dof_invweight0[DX_NV];
 
   float qpos_init[DX_NQ];
@@ -81,6 +82,7 @@ struct DevModel {
 
   // pairs ---------------------------------------------------------------
   int pair_g1[DX_NP], pair_g2[DX_NP], pair_func[DX_NP], pair_ncon[DX_NP];
+  int4 pair_jinfo[DX_NP];  // contact Jacobian per pair: (dof mask of body 1, of body 2, tree 1, tree 2); world: mask 0
   int pair_slotadr[DX_NP], pair_condim[DX_NP];
   float pair_friction[DX_NP], pair_margin[DX_NP];  // margin = includemargin (margin - gap)
   float pair_solref[DX_NP][2], pair_solimp[DX_NP][5];

@@ -187,7 +187,7 @@ static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU
 #define MPCR_W_MAXACT 32
 #endif
 using SmemW = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT>;
-static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD, "Hessian scratch");
+static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD + SmemN::NVW, "Hessian + J^T f scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 static_assert(SmemW::JL * SmemW::LDJ >= SmemW::CVXN, "convex-pair list inside the J rows");
 #if !defined(MPCR_N_LDS_UNCHECKED)

@@ -99,6 +99,8 @@ __device__ __forceinline__ int wscan_excl(int v, int& total) {
   return pre;
 }
 __device__ __forceinline__ void sync() { __syncthreads(); }
+// (a wave-scope fence pair + wave barrier instead -- the workgroup is one
+// wave -- measured the same: 1.963 vs 1.964 ms on C3)
 
 // Candidate groups: a wave may carry CPW candidates of HL = 64 / CPW lanes
 // (lanes [32 h, 32 h + 32) for candidate h when CPW = 2).  These are the
@@ -1701,6 +1703,12 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 #ifndef MPCR_DPP_CHOL
 #define MPCR_DPP_CHOL 1
 #endif
+// narrow variant: the Newton gradient J^T f and Hessian J^T D J on the matrix
+// core (v_mfma_f32_16x16x4_f32) instead of per-row VALU loops
+#ifndef MPCR_MFMA_HESS
+#define MPCR_MFMA_HESS 1
+#endif
+typedef float mfx4 __attribute__((ext_vector_type(4)));
 // The dual-arm variant is compiled for 2 waves/SIMD (<= 256 registers incl.
 // AGPRs; uncapped it took 274 and ran 1 wave/SIMD): with its 21.6 KB image,
 // 7 blocks per CU instead of 4 (dual arm 4096 x 50: 47.5 -> 35.8 ms).
@@ -2217,7 +2225,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       s.M[i][j] = v;
     }
     if (lane < nv) {
-      uint32_t sm = m->body_submask[m->dof_body[lane]];
+      uint32_t sm = m->dof_submask[lane];
       float f[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       while (sm) {
         const int c = __builtin_ctz(sm);
@@ -2487,15 +2495,14 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       for (int idx = lane; idx < keep_con * NVW; idx += S::HL) {
         const int c = idx >> S::LOG_NVW, i = idx & (NVW - 1);
         const int p = s.con_pair[c];
-        const int b1 = m->geom_body[m->pair_g1[p]], b2 = m->geom_body[m->pair_g2[p]];
+        const int4 ji = m->pair_jinfo[p];  // one load: both bodies' dof masks and trees
         float jd[3] = {0.f, 0.f, 0.f};
         if (i < nv) {
           const float* cd = s.cdof[i];
 #pragma unroll
           for (int side = 0; side < 2; side++) {
-            const int bb = side == 0 ? b1 : b2;
-            if (bb >= 0 && ((m->body_dofmask[bb] >> i) & 1u)) {
-              const int tr = m->body_tree[bb];
+            if (((unsigned)(side == 0 ? ji.x : ji.y) >> i) & 1u) {
+              const int tr = side == 0 ? ji.z : ji.w;
               float r[3] = {s.con_pos[c][0] - s.com[tr][0], s.con_pos[c][1] - s.com[tr][1],
                             s.con_pos[c][2] - s.com[tr][2]}, cr[3];
               cross(cr, cd, r);
@@ -2523,7 +2530,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           jstore(s, gx, off + 3, i, jn - mu * jt2);
         }
       }
-      sync();
+      sync();  // (also orders the J rows past JL written to the HBM slab by other lanes)
       // row parameters: vel, impedance, D, aref
       for (int r = lane; r < nefc; r += S::HL) {
         const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
@@ -2714,15 +2721,46 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           const float gauss = hsum<S::CPW>(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
           const float cost = 0.5f * gauss + 0.5f * hsum<S::CPW>(cc);
           sync();
-          // grad = Ma - qfrc_smooth - J^T f: lane (dof i, row group q); RPW
-          // lanes share a dof (4 at NVW 16, 2 at NVW 32)
+          constexpr bool MFMA_HESS = NVW == 16 && S::CPW == 1 && MPCR_MFMA_HESS;
           constexpr int RPW = S::HL / NVW;
           const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
-          float qc = 0.f;
-          jrows(s, gx, gq, RPW, nefc, [&](const float* J, int r) { qc = fmaf(J[gi], s.efc_f[r], qc); });
+          float* Hs = &s.gxpos[0][0];  // geom poses are dead during Newton
+          float grad;
+          if constexpr (MFMA_HESS) {
+            // J^T f and H = M + J^T D_active J together on the matrix core,
+            // 4 rows per v_mfma_f32_16x16x4_f32: lane (dof gi, row r0 + gq)
+            // supplies A = J[r][gi] and B = D_a J[r][gi] (Hessian) / f[r]
+            // (gradient); accumulator register v of lane l is column gi of
+            // row 4 gq + v -- read as row gi of H that is the float4
+            // H[gi][4 gq ..], the same products in the same row order as the
+            // VALU build (the MFMA is a k-ordered fmaf chain), so H is
+            // bitwise the VALU one
+            const float4 m4 = reinterpret_cast<const float4*>(s.M[gi])[gq];
+            mfx4 hacc = {m4.x, m4.y, m4.z, m4.w};
+            mfx4 gacc = {0.f, 0.f, 0.f, 0.f};
+            for (int r0 = 0; r0 < nefc; r0 += 4) {
+              const int r = r0 + gq;
+              const bool ok = r < nefc;
+              const float a = ok ? jrow_ptr(s, gx, r)[gi] : 0.f;
+              const float da = ok ? s.efc_Da[r] : 0.f;
+              const float fr = ok ? s.efc_f[r] : 0.f;
+              hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, da * a, hacc, 0, 0, 0);
+              gacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, fr, gacc, 0, 0, 0);
+            }
+            reinterpret_cast<float4*>(Hs + gi * S::LD)[gq] = make_float4(hacc[0], hacc[1], hacc[2], hacc[3]);
+            float* qcs = Hs + NVW * S::LD;  // J^T f: lanes 0, 16, 32, 48 hold dofs 4 gq ..
+            if (gi == 0) reinterpret_cast<float4*>(qcs)[gq] = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
+            sync();
+            grad = lane < nv ? ma - s.qfs[lane] - qcs[gi] : 0.f;
+          } else {
+            // grad = Ma - qfrc_smooth - J^T f: lane (dof i, row group q); RPW
+            // lanes share a dof (4 at NVW 16, 2 at NVW 32)
+            float qc = 0.f;
+            jrows(s, gx, gq, RPW, nefc, [&](const float* J, int r) { qc = fmaf(J[gi], s.efc_f[r], qc); });
 #pragma unroll
-          for (int o = NVW; o < S::HL; o <<= 1) qc += __shfl_xor(qc, o);
-          const float grad = lane < nv ? ma - s.qfs[lane] - qc : 0.f;
+            for (int o = NVW; o < S::HL; o <<= 1) qc += __shfl_xor(qc, o);
+            grad = lane < nv ? ma - s.qfs[lane] - qc : 0.f;
+          }
           const float gn = sqrtf(hsum<S::CPW>(grad * grad));
           // MuJoCo's stop test, plus its fp32 floor: an improvement within ~8 ulp
           // of the cost is rounding noise (without it fp32 iterates on noise
@@ -2731,12 +2769,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           if (scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance ||
               prev_cost - cost <= 1e-6f * fabsf(cost))
             break;
-          // Hessian H = M + J^T D_active J: lane (row i, column quads q, q + RPW,
-          // ...) builds QPL float4s of row i; rows are gathered to lanes
-          // 0..NVW-1 through LDS
-          constexpr int QPL = NVW / 4 / RPW;
-          float* Hs = &s.gxpos[0][0];  // geom poses are dead during Newton
-          {
+          if constexpr (!MFMA_HESS) {
+            // Hessian H = M + J^T D_active J: lane (row i, column quads q, q + RPW,
+            // ...) builds QPL float4s of row i; rows are gathered to lanes
+            // 0..NVW-1 through LDS
+            constexpr int QPL = NVW / 4 / RPW;
             float4 hq[QPL];
 #pragma unroll
             for (int k = 0; k < QPL; k++) hq[k] = reinterpret_cast<const float4*>(s.M[gi])[gq + RPW * k];
@@ -2780,8 +2817,8 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             }
 #pragma unroll
             for (int k = 0; k < QPL; k++) reinterpret_cast<float4*>(Hs + gi * S::LD)[gq + RPW * k] = hq[k];
+            sync();
           }
-          sync();
           float h[NVW];
           {
             const float4* row = reinterpret_cast<const float4*>(Hs + (lane & (NVW - 1)) * S::LD);
