@@ -32,11 +32,16 @@ namespace mpcr {
 #define PROF_FLUSH                                                          \
   if (lane == 0 && args.prof)                                               \
     for (int i_ = 0; i_ < 24; i_++) atomicAdd(&args.prof[i_], prof_acc[i_]);
-// wave-level event counter (first active lane adds 1; diagnostic only)
+// wave-level event counter (first active lane adds 1; -DMPCR_PROFILE_COUNTS
+// only: the shared atomics distort the cycle shares)
+#ifdef MPCR_PROFILE_COUNTS
 #define PROF_COUNT(m, i)                                                                  \
   do {                                                                                    \
     if ((m)->prof && (int)__lane_id() == __builtin_ctzll(__ballot(1))) atomicAdd((m)->prof + (i), 1ull); \
   } while (0)
+#else
+#define PROF_COUNT(m, i)
+#endif
 #else
 #define PROF_DECL
 #define STAMP(i)

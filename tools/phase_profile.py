@@ -20,8 +20,8 @@ COUNTS = {19: "hull-climb rounds (wave level)", 20: "mesh support calls (wave le
 
 def main():
     so = os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr_prof.so")
-    if "--build" in sys.argv:  # build here (CPU container), run on the GPU box
-        build.compile_lib(so, ["-DMPCR_PROFILE"])
+    if "--build" in sys.argv:  # build here (CPU container), run on the GPU box; --counts: wave-level event counters
+        build.compile_lib(so, ["-DMPCR_PROFILE"] + (["-DMPCR_PROFILE_COUNTS"] if "--counts" in sys.argv else []))
         print(so)
         return
     _lib.LIB_PATH = so
