@@ -1714,6 +1714,13 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 #define MPCR_MFMA_HESS 1
 #endif
 typedef float mfx4 __attribute__((ext_vector_type(4)));
+typedef float mfx16 __attribute__((ext_vector_type(16)));
+// the same for the 32-wide (dual-arm) Newton on v_mfma_f32_32x32x2_f32 (off:
+// measured neutral on C4, 68.3 / 70.4 vs 70.5 / 70.2 ms -- its 32-wide
+// readlane Cholesky, not the Hessian sum, is the cost)
+#ifndef MPCR_MFMA_HESS_W
+#define MPCR_MFMA_HESS_W 0
+#endif
 // The dual-arm variant is compiled for 2 waves/SIMD (<= 256 registers incl.
 // AGPRs; uncapped it took 274 and ran 1 wave/SIMD): with its 21.6 KB image,
 // 7 blocks per CU instead of 4 (dual arm 4096 x 50: 47.5 -> 35.8 ms).
@@ -2727,6 +2734,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           const float cost = 0.5f * gauss + 0.5f * hsum<S::CPW>(cc);
           sync();
           constexpr bool MFMA_HESS = NVW == 16 && S::CPW == 1 && MPCR_MFMA_HESS;
+          constexpr bool MFMA_HESS_W = NVW == 32 && S::CPW == 1 && MPCR_MFMA_HESS_W;
           constexpr int RPW = S::HL / NVW;
           const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
           float* Hs = &s.gxpos[0][0];  // geom poses are dead during Newton
@@ -2757,6 +2765,29 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             if (gi == 0) reinterpret_cast<float4*>(qcs)[gq] = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
             sync();
             grad = lane < nv ? ma - s.qfs[lane] - qcs[gi] : 0.f;
+          } else if constexpr (MFMA_HESS_W) {
+            // 32-wide: J^T f on v_mfma_f32_32x32x2_f32, 2 rows per instruction
+            // (lane: A = J[r0 + gq][gi], B = f[r0 + gq]); accumulator register
+            // v of lane l holds (J^T f)[(v & 3) + 8 (v >> 2) + 4 gq]
+            mfx16 gacc;
+#pragma unroll
+            for (int v = 0; v < 16; v++) gacc[v] = 0.f;
+            for (int r0 = 0; r0 < nefc; r0 += 2) {
+              const int r = r0 + gq;
+              const bool ok = r < nefc;
+              const float a = ok ? jrow_ptr(s, gx, r)[gi] : 0.f;
+              gacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, ok ? s.efc_f[r] : 0.f, gacc, 0, 0, 0);
+            }
+            float* qcs = s.srch;  // free until this iteration's search direction
+            if (gi == 0) {
+#pragma unroll
+              for (int k = 0; k < 4; k++)
+                reinterpret_cast<float4*>(qcs + 8 * k + 4 * gq)[0] =
+                    make_float4(gacc[4 * k], gacc[4 * k + 1], gacc[4 * k + 2], gacc[4 * k + 3]);
+            }
+            sync();
+            grad = lane < nv ? ma - s.qfs[lane] - qcs[gi] : 0.f;
+            sync();  // qcs (srch) is rewritten below
           } else {
             // grad = Ma - qfrc_smooth - J^T f: lane (dof i, row group q); RPW
             // lanes share a dof (4 at NVW 16, 2 at NVW 32)
@@ -2782,15 +2813,35 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             float4 hq[QPL];
 #pragma unroll
             for (int k = 0; k < QPL; k++) hq[k] = reinterpret_cast<const float4*>(s.M[gi])[gq + RPW * k];
-            jrows(s, gx, 0, 1, nefc, [&](const float* J, int r) {
-              const float c = s.efc_Da[r] * J[gi];
+            if constexpr (MFMA_HESS_W) {
+              // J^T D J on v_mfma_f32_32x32x2_f32: accumulator register 4k + e of
+              // lane (gi, gq) is H[gi][4 (gq + 2k) + e] in the transposed view --
+              // exactly hq[k].e, the VALU build's ownership, and the same
+              // products in the same row order (bitwise the VALU H)
+              mfx16 acc;
 #pragma unroll
               for (int k = 0; k < QPL; k++) {
-                const float4 v = reinterpret_cast<const float4*>(J)[gq + RPW * k];
-                hq[k].x = fmaf(c, v.x, hq[k].x); hq[k].y = fmaf(c, v.y, hq[k].y);
-                hq[k].z = fmaf(c, v.z, hq[k].z); hq[k].w = fmaf(c, v.w, hq[k].w);
+                acc[4 * k] = hq[k].x; acc[4 * k + 1] = hq[k].y; acc[4 * k + 2] = hq[k].z; acc[4 * k + 3] = hq[k].w;
               }
-            });
+              for (int r0 = 0; r0 < nefc; r0 += 2) {
+                const int r = r0 + gq;
+                const bool ok = r < nefc;
+                const float a = ok ? jrow_ptr(s, gx, r)[gi] : 0.f;
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, ok ? s.efc_Da[r] * a : 0.f, acc, 0, 0, 0);
+              }
+#pragma unroll
+              for (int k = 0; k < QPL; k++) hq[k] = make_float4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
+            } else {
+              jrows(s, gx, 0, 1, nefc, [&](const float* J, int r) {
+                const float c = s.efc_Da[r] * J[gi];
+#pragma unroll
+                for (int k = 0; k < QPL; k++) {
+                  const float4 v = reinterpret_cast<const float4*>(J)[gq + RPW * k];
+                  hq[k].x = fmaf(c, v.x, hq[k].x); hq[k].y = fmaf(c, v.y, hq[k].y);
+                  hq[k].z = fmaf(c, v.z, hq[k].z); hq[k].w = fmaf(c, v.w, hq[k].w);
+                }
+              });
+            }
             if constexpr (S::WIDE) {  // cone Hessian blocks J_c^T H_c J_c (wave-uniform loop)
               if (m->cone == 1)
                 for (int r = 0; r < nefc; r++) {
