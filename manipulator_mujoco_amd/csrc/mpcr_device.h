@@ -70,6 +70,12 @@ struct DevModel {
   uint32_t dof_chainmask[DX_NV]; // dofs j with M[i][j] possibly nonzero (ancestors incl. self)
   uint32_t dof_velmask[DX_NV];   // dofs forming the velocity cdof_dot uses
   uint32_t dof_submask[DX_NV];   // bodies in the subtree of the dof's body (bias force sum)
+  // blocked Cholesky (narrow kernel): every kinematic tree's dofs (<= 8 each,
+  // <= 4 trees) in their own 16-lane DPP row, so M -- block diagonal by tree --
+  // and an uncoupled Newton H factor as ntree simultaneous 8-column chains
+  int blk_ok;                    // the layout applies (else the dense 16-wide path)
+  int eq_cross;                  // an equality couples two trees (Newton stays dense)
+  int blane_dof[64];             // lane 16 tree + k -> dof (-1: pad)
   float dof_armature[DX_NV], dof_damping[DX_NV], dof_invweight0[DX_NV];
 
   float qpos_init[DX_NQ];

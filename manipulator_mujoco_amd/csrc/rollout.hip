@@ -370,6 +370,10 @@ template <int STEP>
 struct Sweep16<-1, STEP> {
   static __device__ __forceinline__ void run(const float (&)[16], float&, float) {}
 };
+// the blocked (per-tree) Cholesky for M and uncoupled Newton Hessians
+#ifndef MPCR_BLOCK_CHOL
+#define MPCR_BLOCK_CHOL 1
+#endif
 // MPCR_CHOL_LANE_LAUNDER: re-derive the lane compares inside the solves (one
 // v_cmp each) instead of letting them be hoisted into spilled SGPR pairs
 #ifndef MPCR_CHOL_LANE_LAUNDER
@@ -380,6 +384,93 @@ __device__ __forceinline__ void chol16(float (&a)[16], float& dinv, int lane) {
   dinv = 0.f;
   Chol16<0>::run(a, dinv, lane);
 }
+// Blocked variant for block-diagonal systems (the mass matrix is block
+// diagonal by kinematic tree): tree t's <= 8 dofs are rows of lanes 16 t ..
+// 16 t + 7, and row_newbcast:K broadcasts each tree's K-th row to its own
+// lanes, so all trees factor in ONE 8-column chain (36 fused updates instead
+// of 120) -- the same operations per block as the dense factorisation
+// (off-block entries are exact zeros there), in the same order.
+template <int N, int K, int J>
+struct CholNUpd {
+  static __device__ __forceinline__ void run(float (&a)[N], float lik) {
+    fnmac_bc<J, J == K + 1>(a[J], lik, lik);
+    CholNUpd<N, K, J + 1>::run(a, lik);
+  }
+};
+template <int N, int K>
+struct CholNUpd<N, K, N> {
+  static __device__ __forceinline__ void run(float (&)[N], float) {}
+};
+template <int N, int K>
+struct CholN {  // lr: the lane's row within its 16-lane DPP row
+  static __device__ __forceinline__ void run(float (&a)[N], float& dinv, int lr) {
+    const float dkk = sqrtf(fmaxf(rbc<K>(a[K]), kMinVal));
+    const float inv = 1.f / dkk;
+    const float lik = lr > K ? a[K] * inv : 0.f;
+    a[K] = lik;
+    dinv = lr == K ? inv : dinv;
+    CholNUpd<N, K, K + 1>::run(a, lik);
+    CholN<N, K + 1>::run(a, dinv, lr);
+  }
+};
+template <int N>
+struct CholN<N, N> {
+  static __device__ __forceinline__ void run(float (&)[N], float&, int) {}
+};
+template <int N, int K, int STEP>
+struct SweepN {
+  static __device__ __forceinline__ void run(const float (&c)[N], float& acc, float dinv) {
+    const float t = acc * dinv;
+    fnmac_bc<K, true>(acc, t, c[K]);
+    SweepN<N, K + STEP, STEP>::run(c, acc, dinv);
+  }
+};
+template <int N, int STEP>
+struct SweepN<N, N, STEP> {
+  static __device__ __forceinline__ void run(const float (&)[N], float&, float) {}
+};
+template <int N, int STEP>
+struct SweepN<N, -1, STEP> {
+  static __device__ __forceinline__ void run(const float (&)[N], float&, float) {}
+};
+// x = A^-1 b for a symmetric A (rows of the dof-major LDS matrix A, stride lda)
+// that is block diagonal by kinematic tree, in the blocked lane layout;
+// b and x are dof-indexed LDS vectors (x may alias b).  Lt: 256-float LDS
+// scratch.  Must be called by all lanes (two barriers).
+__device__ __forceinline__ void blocked_solve(const DevModel* __restrict__ m, const float* A, int lda, const float* bv,
+                                              float* xv, int lane, float* Lt) {
+  if (MPCR_CHOL_LANE_LAUNDER) asm volatile("" : "+v"(lane));
+  const int lr = lane & 15, t = lane >> 4, lb = lane & ~15;
+  const int d = m->blane_dof[lane];
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int dj = m->blane_dof[lb + j];
+    a[j] = (d >= 0 && dj >= 0) ? A[d * lda + dj] : (j == lr ? 1.f : 0.f);
+  }
+  float dinv = 0.f;
+  CholN<8, 0>::run(a, dinv, lr);
+  float acc = d >= 0 ? bv[d] : 0.f;
+  SweepN<8, 0, 1>::run(a, acc, dinv);
+  const float y = acc * dinv;
+  if (lr < 8) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) Lt[t * 64 + j * 8 + lr] = a[j];
+  }
+  sync();
+  float lt[8];
+  {
+    const float4* col = reinterpret_cast<const float4*>(Lt + t * 64 + (lr & 7) * 8);
+    const float4 v0 = col[0], v1 = col[1];
+    lt[0] = v0.x; lt[1] = v0.y; lt[2] = v0.z; lt[3] = v0.w; lt[4] = v1.x; lt[5] = v1.y; lt[6] = v1.z; lt[7] = v1.w;
+  }
+  acc = y;
+  SweepN<8, 7, -1>::run(lt, acc, dinv);
+  const float x = acc * dinv;
+  sync();
+  if (d >= 0) xv[d] = x;
+}
+
 // x = L^-T L^-1 b (lane i: row i of L in l[]); Lt: LDS transpose scratch
 template <int LDL>
 __device__ __forceinline__ float chol16_solve(const float (&l)[16], float dinv, float b, int lane, float* Lt) {
@@ -2265,7 +2356,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     STOP_AT(5)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
-    {
+    if (NVW == 16 && S::CPW == 1 && MPCR_BLOCK_CHOL && m->blk_ok) {
+      // M is block diagonal by kinematic tree: one 8-column chain for all trees
+      if (lane >= nv && lane < NVW) s.qas[lane] = 0.f;
+      blocked_solve(m, &s.M[0][0], S::LD, s.qfs, s.qas, lane, &s.xpos[0][0]);
+    } else {
       float Lm[NVW];
 #pragma unroll
       for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? s.M[lane][j] : 0.f;
@@ -2380,6 +2475,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     STOP_AT(7)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- constraint rows: equality, limits, contacts ------------------------
+    bool coupled = true;  // a constraint row spans two kinematic trees (Newton's H not block diagonal)
     {
       const int ncon = s.ncon;
       const int neq = (m->disableflags & 64) ? 0 : (S::WIDE ? m->neqrow : m->neq);
@@ -2444,6 +2540,14 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         } else {
           for (int r = 0; r < ncr; r++) s.efc_src[o + r] = (3 << 24) | (lane << 4) | r;
         }
+      }
+      if constexpr (!S::WIDE) {
+        bool cross = false;
+        if (lane < keep_con) {
+          const int4 ji = m->pair_jinfo[s.con_pair[lane]];
+          cross = ji.x != 0 && ji.y != 0 && ji.z != ji.w;
+        }
+        coupled = m->eq_cross || hballot<S::CPW>(cross) != 0ull;
       }
       if (lane == 0) s.nefc = nefc;
       sync();
@@ -2875,23 +2979,33 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             for (int k = 0; k < QPL; k++) reinterpret_cast<float4*>(Hs + gi * S::LD)[gq + RPW * k] = hq[k];
             sync();
           }
-          float h[NVW];
-          {
-            const float4* row = reinterpret_cast<const float4*>(Hs + (lane & (NVW - 1)) * S::LD);
-#pragma unroll
-            for (int q = 0; q < NVW / 4; q++) {
-              const float4 v = row[q];
-              h[4 * q] = v.x; h[4 * q + 1] = v.y; h[4 * q + 2] = v.z; h[4 * q + 3] = v.w;
-            }
-          }
           float mg;
-          if constexpr (NVW == 16 && MPCR_DPP_CHOL) {
-            float dinv;
-            chol16(h, dinv, lane);
-            mg = chol16_solve<S::LD>(h, dinv, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
+          if (NVW == 16 && S::CPW == 1 && MPCR_BLOCK_CHOL && m->blk_ok && !coupled) {
+            // no row couples two trees: H is block diagonal like M
+            if (lane < NVW) s.srch[lane] = lane < nv ? grad : 0.f;
+            sync();
+            blocked_solve(m, Hs, S::LD, s.srch, s.srch, lane, &s.gxpos[0][0]);
+            sync();
+            mg = lane < nv ? s.srch[lane] : 0.f;
+            sync();  // srch is rewritten below
           } else {
-            chol_rows(h, lane);
-            mg = chol_solve<NVW, S::LD>(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
+            float h[NVW];
+            {
+              const float4* row = reinterpret_cast<const float4*>(Hs + (lane & (NVW - 1)) * S::LD);
+#pragma unroll
+              for (int q = 0; q < NVW / 4; q++) {
+                const float4 v = row[q];
+                h[4 * q] = v.x; h[4 * q + 1] = v.y; h[4 * q + 2] = v.z; h[4 * q + 3] = v.w;
+              }
+            }
+            if constexpr (NVW == 16 && MPCR_DPP_CHOL) {
+              float dinv;
+              chol16(h, dinv, lane);
+              mg = chol16_solve<S::LD>(h, dinv, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
+            } else {
+              chol_rows(h, lane);
+              mg = chol_solve<NVW, S::LD>(h, lane < nv ? grad : 0.f, lane, &s.gxpos[0][0]);
+            }
           }
           const float search = lane < nv ? -mg : 0.f;
           if (args.dbg && b == 0 && t == H - 1 && it == 0 && lane < NVW) {
