@@ -467,21 +467,34 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
   }
   for (int i = 0; i < m.nv; i++) d.dof_submask[i] = d.dof_body[i] >= 0 ? d.body_submask[d.dof_body[i]] : 0u;
   {  // blocked Cholesky layout: tree t's k-th dof (ascending) at lane 16 t + k
-    int cnt[DX_NTREE] = {0};
-    bool ok = m.nv <= 16;
+    int cnt[DX_NTREE] = {0}, mx = 0;
+    bool ok = true;
     for (int l = 0; l < 64; l++) d.blane_dof[l] = -1;
     for (int i = 0; i < m.nv && ok; i++) {
       const int b = d.dof_body[i], t = b >= 0 ? d.body_tree[b] : -1;
-      if (t < 0 || t >= DX_NTREE || cnt[t] >= 8) { ok = false; break; }
+      if (t < 0 || t >= DX_NTREE || cnt[t] >= 16) { ok = false; break; }
       d.blane_dof[16 * t + cnt[t]++] = i;
+      mx = std::max(mx, cnt[t]);
     }
-    d.blk_ok = ok ? 1 : 0;
+    d.blk_n = !ok ? 0 : (mx <= 8 ? 8 : 16);
+    // rows spanning two trees keep Newton's H dense: equalities (joint: the
+    // two joints' trees; connect: the two bodies', static = none) and tendons
+    auto tree_of_body = [&](int b) { return b > 0 && dmap[b] >= 0 ? d.body_tree[dmap[b]] : -1; };
+    auto cross = [](int t1, int t2) { return t1 >= 0 && t2 >= 0 && t1 != t2; };
     d.eq_cross = 0;
     for (int e = 0; e < m.neq; e++) {
-      if (m.eq_type[e] != MPCR_EQ_JOINT) { d.eq_cross = 1; continue; }
-      const int j1 = m.eq_obj1[e], j2 = m.eq_obj2[e];
-      if (j2 >= 0 && d.body_tree[dmap[m.jnt_bodyid[j1]]] != d.body_tree[dmap[m.jnt_bodyid[j2]]]) d.eq_cross = 1;
+      if (m.eq_type[e] == MPCR_EQ_JOINT) {
+        const int j1 = m.eq_obj1[e], j2 = m.eq_obj2[e];
+        if (j2 >= 0 && cross(tree_of_body(m.jnt_bodyid[j1]), tree_of_body(m.jnt_bodyid[j2]))) d.eq_cross = 1;
+      } else if (m.eq_type[e] == MPCR_EQ_CONNECT) {
+        if (cross(tree_of_body(m.eq_obj1[e]), tree_of_body(m.eq_obj2[e]))) d.eq_cross = 1;
+      } else {
+        d.eq_cross = 1;
+      }
     }
+    for (int t = 0; t < m.nten; t++)
+      if (cross(tree_of_body(m.site_bodyid[m.ten_site[t][0]]), tree_of_body(m.site_bodyid[m.ten_site[t][1]])))
+        d.eq_cross = 1;
   }
   for (int i = 0; i < m.nq; i++) d.qpos_init[i] = (float)m.qpos_init[i];
   for (int i = 0; i < m.nv; i++) d.qvel_init[i] = (float)m.qvel_init[i];

@@ -73,8 +73,8 @@ struct DevModel {
   // blocked Cholesky (narrow kernel): every kinematic tree's dofs (<= 8 each,
   // <= 4 trees) in their own 16-lane DPP row, so M -- block diagonal by tree --
   // and an uncoupled Newton H factor as ntree simultaneous 8-column chains
-  int blk_ok;                    // the layout applies (else the dense 16-wide path)
-  int eq_cross;                  // an equality couples two trees (Newton stays dense)
+  int blk_n;                     // 8 / 16: every tree has <= that many dofs; 0: dense paths only
+  int eq_cross;                  // an equality / tendon row couples two trees (Newton stays dense)
   int blane_dof[64];             // lane 16 tree + k -> dof (-1: pad)
   float dof_armature[DX_NV], dof_damping[DX_NV], dof_invweight0[DX_NV];
 

@@ -433,42 +433,59 @@ template <int N, int STEP>
 struct SweepN<N, -1, STEP> {
   static __device__ __forceinline__ void run(const float (&)[N], float&, float) {}
 };
-// x = A^-1 b for a symmetric A (rows of the dof-major LDS matrix A, stride lda)
-// that is block diagonal by kinematic tree, in the blocked lane layout;
-// b and x are dof-indexed LDS vectors (x may alias b).  Lt: 256-float LDS
-// scratch.  Must be called by all lanes (two barriers).
-__device__ __forceinline__ void blocked_solve(const DevModel* __restrict__ m, const float* A, int lda, const float* bv,
-                                              float* xv, int lane, float* Lt) {
+// x = A^-1 b for a symmetric A that is block diagonal by kinematic tree (tree
+// t's <= N dofs on lanes 16 t ..), elem(d, dj) = A[d][dj]; b and x are
+// dof-indexed LDS vectors (x may alias b).  Lt: 4 N^2-float LDS scratch (it
+// may alias A's storage: every element is read before the first write).  Must
+// be called by all lanes (two barriers).
+template <int N, class F>
+__device__ __forceinline__ void blocked_solve(const DevModel* __restrict__ m, F&& elem, const float* bv, float* xv,
+                                              int lane, float* Lt) {
+  static_assert(N == 8 || N == 16, "blocked Cholesky width");
   if (MPCR_CHOL_LANE_LAUNDER) asm volatile("" : "+v"(lane));
   const int lr = lane & 15, t = lane >> 4, lb = lane & ~15;
   const int d = m->blane_dof[lane];
-  float a[8];
+  float a[N];
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < N; j++) {
     const int dj = m->blane_dof[lb + j];
-    a[j] = (d >= 0 && dj >= 0) ? A[d * lda + dj] : (j == lr ? 1.f : 0.f);
+    a[j] = (d >= 0 && dj >= 0) ? elem(d, dj) : (j == lr ? 1.f : 0.f);
   }
   float dinv = 0.f;
-  CholN<8, 0>::run(a, dinv, lr);
+  CholN<N, 0>::run(a, dinv, lr);
   float acc = d >= 0 ? bv[d] : 0.f;
-  SweepN<8, 0, 1>::run(a, acc, dinv);
+  SweepN<N, 0, 1>::run(a, acc, dinv);
   const float y = acc * dinv;
-  if (lr < 8) {
+  if (lr < N) {
 #pragma unroll
-    for (int j = 0; j < 8; j++) Lt[t * 64 + j * 8 + lr] = a[j];
+    for (int j = 0; j < N; j++) Lt[t * N * N + j * N + lr] = a[j];
   }
   sync();
-  float lt[8];
+  float lt[N];
   {
-    const float4* col = reinterpret_cast<const float4*>(Lt + t * 64 + (lr & 7) * 8);
-    const float4 v0 = col[0], v1 = col[1];
-    lt[0] = v0.x; lt[1] = v0.y; lt[2] = v0.z; lt[3] = v0.w; lt[4] = v1.x; lt[5] = v1.y; lt[6] = v1.z; lt[7] = v1.w;
+    const float4* col = reinterpret_cast<const float4*>(Lt + t * N * N + (lr & (N - 1)) * N);
+#pragma unroll
+    for (int q = 0; q < N / 4; q++) {
+      const float4 v = col[q];
+      lt[4 * q] = v.x; lt[4 * q + 1] = v.y; lt[4 * q + 2] = v.z; lt[4 * q + 3] = v.w;
+    }
   }
   acc = y;
-  SweepN<8, 7, -1>::run(lt, acc, dinv);
+  SweepN<N, N - 1, -1>::run(lt, acc, dinv);
   const float x = acc * dinv;
   sync();
   if (d >= 0) xv[d] = x;
+}
+// the blocked path for a kernel variant of NVW dofs: 8-wide chains in the
+// narrow kernel (trees <= 8 dofs), 16-wide in the dual-arm one (trees <= 16)
+template <int NVW>
+__device__ __forceinline__ bool blk_usable(const DevModel* __restrict__ m) {
+  return MPCR_BLOCK_CHOL && (NVW == 16 ? m->blk_n == 8 : m->blk_n != 0);
+}
+template <int NVW, class F>
+__device__ __forceinline__ void blk_solve(const DevModel* __restrict__ m, F&& elem, const float* bv, float* xv,
+                                          int lane, float* Lt) {
+  blocked_solve<NVW == 16 ? 8 : 16>(m, elem, bv, xv, lane, Lt);
 }
 
 // x = L^-T L^-1 b (lane i: row i of L in l[]); Lt: LDS transpose scratch
@@ -2356,10 +2373,10 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     STOP_AT(5)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- qacc_smooth = M^-1 qfrc_smooth (row-per-lane Cholesky) -------------
-    if (NVW == 16 && S::CPW == 1 && MPCR_BLOCK_CHOL && m->blk_ok) {
-      // M is block diagonal by kinematic tree: one 8-column chain for all trees
+    if (S::CPW == 1 && blk_usable<NVW>(m)) {
+      // M is block diagonal by kinematic tree: one chain for all trees
       if (lane >= nv && lane < NVW) s.qas[lane] = 0.f;
-      blocked_solve(m, &s.M[0][0], S::LD, s.qfs, s.qas, lane, &s.xpos[0][0]);
+      blk_solve<NVW>(m, [&](int i, int j) { return s.M[i][j]; }, s.qfs, s.qas, lane, &s.xpos[0][0]);
     } else {
       float Lm[NVW];
 #pragma unroll
@@ -2541,7 +2558,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           for (int r = 0; r < ncr; r++) s.efc_src[o + r] = (3 << 24) | (lane << 4) | r;
         }
       }
-      if constexpr (!S::WIDE) {
+      {
         bool cross = false;
         if (lane < keep_con) {
           const int4 ji = m->pair_jinfo[s.con_pair[lane]];
@@ -2980,11 +2997,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             sync();
           }
           float mg;
-          if (NVW == 16 && S::CPW == 1 && MPCR_BLOCK_CHOL && m->blk_ok && !coupled) {
+          if (S::CPW == 1 && !coupled && blk_usable<NVW>(m)) {
             // no row couples two trees: H is block diagonal like M
             if (lane < NVW) s.srch[lane] = lane < nv ? grad : 0.f;
             sync();
-            blocked_solve(m, Hs, S::LD, s.srch, s.srch, lane, &s.gxpos[0][0]);
+            blk_solve<NVW>(m, [&](int i, int j) { return Hs[i * S::LD + j]; }, s.srch, s.srch, lane, &s.gxpos[0][0]);
             sync();
             mg = lane < nv ? s.srch[lane] : 0.f;
             sync();  // srch is rewritten below
