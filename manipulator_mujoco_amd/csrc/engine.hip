@@ -654,6 +654,10 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     }
     for (int i = 0; i < m.nv; i++)
       for (int j = 0; j < m.nv; j++) d.impl_D[i][j] = (float)D[(size_t)i * m.nv + j];
+    d.impl_cross = 0;  // a transmission across trees keeps the implicit solve dense
+    for (int i = 0; i < m.nv; i++)
+      for (int j = 0; j < m.nv; j++)
+        if (D[(size_t)i * m.nv + j] != 0.0 && d.body_tree[d.dof_body[i]] != d.body_tree[d.dof_body[j]]) d.impl_cross = 1;
   } else if (m.integrator != MPCR_INT_EULER) {
     return fail(MPCR_EMODEL, "integrator %d not supported (Euler, implicitfast)", m.integrator);
   }

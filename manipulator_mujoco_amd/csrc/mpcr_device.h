@@ -75,6 +75,7 @@ struct DevModel {
   // and an uncoupled Newton H factor as ntree simultaneous 8-column chains
   int blk_n;                     // 8 / 16: every tree has <= that many dofs; 0: dense paths only
   int eq_cross;                  // an equality / tendon row couples two trees (Newton stays dense)
+  int impl_cross;                // implicitfast's D couples two trees (its solve stays dense)
   int blane_dof[64];             // lane 16 tree + k -> dof (-1: pad)
   float dof_armature[DX_NV], dof_damping[DX_NV], dof_invweight0[DX_NV];
 

@@ -1437,6 +1437,24 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
     for (int k = 0; k < 3; k++) s.poly[0][lane][k] = ci[k] + si * hk * Ik[k] + su * hu * Iu[k] + sv * hv * Iv[k];
   }
   int np = 4, cur = 0;
+  // fast path: an incident face wholly inside the reference face's 4 side
+  // planes (an object resting inside a table top) passes every clip unchanged
+  // -- Sutherland-Hodgman keeps each vertex and adds no crossing -- so the 4
+  // sequential clips are skipped for exactly the same polygon
+  bool inside = true;
+  sync();
+  if (lane < 4) {
+    const float P[3] = {s.poly[0][lane][0], s.poly[0][lane][1], s.poly[0][lane][2]};
+#pragma unroll
+    for (int pl = 0; pl < 4; pl++) {  // the clip loop's own dp expression
+      const int ax = (fi + 1 + (pl >> 1)) % 3;
+      const float sgn = (pl & 1) ? -1.f : 1.f;
+      const float Ra[3] = {Rr[ax], Rr[3 + ax], Rr[6 + ax]};
+      const float cra = dot3(cr, Ra);
+      inside = inside && sgn * (dot3(P, Ra) - cra) - hr[ax] <= 0.f;
+    }
+  }
+  if (hballot<S::CPW>(!inside) == 0ull) np = -np;  // marker: skip the clips
   for (int pl = 0; pl < 4 && np > 0; pl++) {
     sync();
     const int ax = (fi + 1 + (pl >> 1)) % 3;
@@ -1469,6 +1487,7 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
     np = tot;
     cur ^= 1;
   }
+  if (np < 0) np = -np;
   sync();
   if (np == 0) return;
   const float hrf = hr[fi];
@@ -3149,13 +3168,21 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 #pragma unroll
         for (int o = NVW; o < S::HL; o <<= 1) qc += __shfl_xor(qc, o);
         const float dt = m->timestep;
-        float Lm[NVW];
+        if (S::CPW == 1 && !m->impl_cross && blk_usable<NVW>(m)) {  // M + dt D block diagonal by tree
+          if (lane < NVW) s.srch[lane] = lane < nv ? s.qfs[lane] + qc : 0.f;
+          sync();
+          blk_solve<NVW>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], s.M[i][j]); }, s.srch, s.srch,
+                         lane, &s.gxpos[0][0]);
+          sync();
+        } else {
+          float Lm[NVW];
 #pragma unroll
-        for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? fmaf(dt, m->impl_D[lane][j], s.M[lane][j]) : 0.f;
-        chol_rows(Lm, lane);
-        const float a = chol_solve<NVW, S::LD>(Lm, lane < nv ? s.qfs[lane] + qc : 0.f, lane, &s.gxpos[0][0]);
-        if (lane < NVW) s.srch[lane] = lane < nv ? a : 0.f;
-        sync();
+          for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? fmaf(dt, m->impl_D[lane][j], s.M[lane][j]) : 0.f;
+          chol_rows(Lm, lane);
+          const float a = chol_solve<NVW, S::LD>(Lm, lane < nv ? s.qfs[lane] + qc : 0.f, lane, &s.gxpos[0][0]);
+          if (lane < NVW) s.srch[lane] = lane < nv ? a : 0.f;
+          sync();
+        }
       }
     }
     // ---- Euler: qvel += dt qacc; integrate qpos; warm start -----------------
