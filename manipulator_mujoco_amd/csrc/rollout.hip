@@ -1842,6 +1842,28 @@ __device__ __forceinline__ void jrows(const S& s, const float* gx, int r0, int s
 #endif
 typedef float mfx4 __attribute__((ext_vector_type(4)));
 typedef float mfx16 __attribute__((ext_vector_type(16)));
+// narrow variant: the chain / subtree sums of the dynamics (CRB, body
+// velocities, cdof_dot, RNE accelerations, bias forces) and the mass matrix as
+// 16 x 16 (x 16) products on the matrix core: a 0/1 (or qvel-weighted) chain
+// mask times per-dof / per-body rows.  v_mfma_f32_16x16x4_f32 is a k-ordered
+// fmaf chain, and the products are the loops' own (qvel x cdof, fvec x cdof),
+// so the results are bitwise the per-lane loops'
+#ifndef MPCR_MFMA_DYN
+#define MPCR_MFMA_DYN 1
+#endif
+// acc + A B over k < 16 (4 instructions): lane l supplies A[l & 15][k] =
+// af(l & 15, k) and B[k][l & 15] = bf(k, l & 15) for its k = 4 s + (l >> 4);
+// register v of lane l then holds row 4 (l >> 4) + v, column l & 15
+template <int KB, class AF, class BF>
+__device__ __forceinline__ mfx4 mm16(AF&& af, BF&& bf, mfx4 acc, int lane) {
+  const int i = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int s4 = 0; s4 < KB; s4++) {
+    const int k = 4 * s4 + kq;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af(i, k), bf(k, i), acc, 0, 0, 0);
+  }
+  return acc;
+}
 // the same for the 32-wide (dual-arm) Newton on v_mfma_f32_32x32x2_f32 (off:
 // measured neutral on C4, 68.3 / 70.4 vs 70.5 / 70.2 ms -- its 32-wide
 // readlane Cholesky, not the Hessian sum, is the cost)
@@ -1949,6 +1971,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 #endif
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
   int status = 0, nefc_sum = 0, nefc_max = 0;
+  // this lane's controlled joint addresses, held across the horizon (read
+  // every step; the per-step model launder would otherwise reload them)
+  const int ctrl_qa = lane < nc ? m->ctrl_qposadr[lane] : 0, ctrl_da = lane < nc ? m->ctrl_dofadr[lane] : 0;
   PROF_DECL
 
   for (int t = 0; t < H; t++) {
@@ -1963,7 +1988,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     if (lane < nc) {
       const float v = vnext;
       if (t + 1 < H) vnext = tdp[lane * H + t + 1];  // next step's, in flight during this one
-      s.qvel[m->ctrl_dofadr[lane]] = v;
+      s.qvel[ctrl_da] = v;
       if (args.layout != 0 && args.thetadot && live) args.thetadot[(size_t)b * nc * H + lane * H + t] = v;
     }
 #else
@@ -1978,7 +2003,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       } else {
         v = args.input[(size_t)bi * nc * H + lane * H + t];
       }
-      s.qvel[m->ctrl_dofadr[lane]] = v;
+      s.qvel[ctrl_da] = v;
       if (args.thetadot && live) args.thetadot[(size_t)b * nc * H + lane * H + t] = v;
     }
 #endif
@@ -2257,6 +2282,64 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     STOP_AT(3)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- CRB, velocity, RNE + gravcomp (subtree sums by bitmask) -----------
+    constexpr bool MFMA_DYN = NVW == 16 && NBW == 16 && S::CPW == 1 && MPCR_MFMA_DYN;
+    float* dscr = &s.xquat[0][0];  // xquat + xmat (256 floats) are dead after the cdof phase
+    if constexpr (MFMA_DYN) {
+      const int mr = lane & 15, kq = lane >> 4;
+      const float* qv = s.qvel;
+      const mfx4 z4 = {0.f, 0.f, 0.f, 0.f};
+      // crb[b] = sum of cinert over b's subtree
+      {
+        const uint32_t sub = mr < nb ? m->body_submask[mr] : 0u;
+        const mfx4 acc = mm16<4>([&](int, int k) { return ((sub >> k) & 1u) ? 1.f : 0.f; },
+                                 [&](int k, int j) { return (k < nb && j < 10) ? s.cinert[k][j] : 0.f; }, z4, lane);
+#pragma unroll
+        for (int v = 0; v < 4; v++)
+          if (4 * kq + v < nb && mr < 10) s.crb[4 * kq + v][mr] = acc[v];
+      }
+      // cvel[b] = sum over b's chain of qvel x cdof; the velocity before each
+      // dof (its velmask) likewise, into the scratch for cdof_dot
+      {
+        const uint32_t bm = mr < nb ? m->body_dofmask[mr] : 0u, vm = mr < nv ? m->dof_velmask[mr] : 0u;
+        mfx4 cv = z4, vv = z4;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+          const int k = 4 * s4 + kq;
+          const float q = k < nv ? qv[k] : 0.f;
+          const float bcd = (k < nv && mr < 6) ? s.cdof[k][mr] : 0.f;
+          cv = __builtin_amdgcn_mfma_f32_16x16x4f32(((bm >> k) & 1u) ? q : 0.f, bcd, cv, 0, 0, 0);
+          vv = __builtin_amdgcn_mfma_f32_16x16x4f32(((vm >> k) & 1u) ? q : 0.f, bcd, vv, 0, 0, 0);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+          if (4 * kq + v < nb && mr < 6) s.cvel[4 * kq + v][mr] = cv[v];
+          if (mr < 6) dscr[(4 * kq + v) * 8 + mr] = vv[v];
+        }
+      }
+      sync();
+      if (lane < nv) {  // cdof_dot = cvel_before x cdof (0 for free translation)
+        float v[6], r[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) v[k] = dscr[lane * 8 + k];
+        cross_motion(r, v, s.cdof[lane]);
+        const bool zero = m->dof_kind[lane] == 2;
+#pragma unroll
+        for (int k = 0; k < 6; k++) s.cdofdot[lane][k] = zero ? 0.f : r[k];
+      }
+      sync();
+      // RNE accelerations: (0, -g) + sum over the chain of qvel x cdof_dot
+      {
+        const uint32_t bm = mr < nb ? m->body_dofmask[mr] : 0u;
+        mfx4 a4;
+#pragma unroll
+        for (int v = 0; v < 4; v++) a4[v] = (mr >= 3 && mr < 6) ? -m->gravity[mr - 3] : 0.f;
+        a4 = mm16<4>([&](int, int k) { return ((bm >> k) & 1u) ? (k < nv ? qv[k] : 0.f) : 0.f; },
+                     [&](int k, int j) { return (k < nv && j < 6) ? s.cdofdot[k][j] : 0.f; }, a4, lane);
+#pragma unroll
+        for (int v = 0; v < 4; v++)
+          if (mr < 6) dscr[128 + (4 * kq + v) * 8 + mr] = a4[v];
+      }
+    } else {
     for (int idx = lane; idx < nb * 10; idx += S::HL) {
       const int bb = idx / 10, k = idx - bb * 10;
       uint32_t sm = m->body_submask[bb];
@@ -2296,6 +2379,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 #pragma unroll
       for (int k = 0; k < 6; k++) s.cdofdot[lane][k] = zero ? 0.f : r[k];
     }
+    }
     sync();
     if (lane < nv) {  // f_i = crb[body(i)] * cdof_i
       float f[6];
@@ -2304,14 +2388,21 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       for (int k = 0; k < 6; k++) s.fvec[lane][k] = f[k];
     }
     if (lane < nb) {  // cfrc_body = I*cacc + v x* (I v) - gravcomp wrench
-      uint32_t dm = m->body_dofmask[lane];
-      float a[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
-      while (dm) {
-        const int d = __builtin_ctz(dm);
-        dm &= dm - 1;
-        const float qd = s.qvel[d];
+      float a[6];
+      if constexpr (MFMA_DYN) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) a[k] = fmaf(s.cdofdot[d][k], qd, a[k]);
+        for (int k = 0; k < 6; k++) a[k] = dscr[128 + lane * 8 + k];
+      } else {
+        uint32_t dm = m->body_dofmask[lane];
+        a[0] = a[1] = a[2] = 0.f;
+        a[3] = -m->gravity[0]; a[4] = -m->gravity[1]; a[5] = -m->gravity[2];
+        while (dm) {
+          const int d = __builtin_ctz(dm);
+          dm &= dm - 1;
+          const float qd = s.qvel[d];
+#pragma unroll
+          for (int k = 0; k < 6; k++) a[k] = fmaf(s.cdofdot[d][k], qd, a[k]);
+        }
       }
       float f[6], iv[6], vf[6], cv[6];
 #pragma unroll
@@ -2346,6 +2437,37 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     STOP_AT(4)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // mass matrix entries (chain-masked) + bias forces
+    if constexpr (MFMA_DYN) {
+      // P = fvec cdof^T (K = 6 in two instructions); M[i][j] = P[i][j] for j on
+      // i's chain, mirrored to M[j][i]; the bias forces' subtree sums of cfrc
+      const int mr = lane & 15, kq = lane >> 4;
+      const mfx4 z4 = {0.f, 0.f, 0.f, 0.f};
+      const mfx4 P = mm16<2>([&](int i, int c) { return (i < nv && c < 6) ? s.fvec[i][c] : 0.f; },
+                             [&](int c, int j) { return (j < nv && c < 6) ? s.cdof[j][c] : 0.f; }, z4, lane);
+      const int j = mr;
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        const int i = 4 * kq + v;
+        if (i < nv && j < nv) {
+          if ((m->dof_chainmask[i] >> j) & 1u) {
+            const float x = i == j ? P[v] + m->dof_armature[i] : P[v];
+            s.M[i][j] = x;
+            s.M[j][i] = x;
+          } else if (!((m->dof_chainmask[j] >> i) & 1u)) {
+            s.M[i][j] = 0.f;
+          }
+        } else {
+          s.M[i][j] = i == j ? 1.f : 0.f;
+        }
+      }
+      const uint32_t sub = mr < nv ? m->dof_submask[mr] : 0u;
+      const mfx4 fb = mm16<4>([&](int, int b) { return ((sub >> b) & 1u) ? 1.f : 0.f; },
+                              [&](int b, int c) { return (b < nb && c < 6) ? s.cfrc[b][c] : 0.f; }, z4, lane);
+#pragma unroll
+      for (int v = 0; v < 4; v++)
+        if (mr < 6) dscr[(4 * kq + v) * 8 + mr] = fb[v];
+      sync();
+    } else {
     for (int idx = lane; idx < NVW * NVW; idx += S::HL) {
       const int i = idx >> S::LOG_NVW, j = idx & (NVW - 1);
       float v = 0.f;
@@ -2363,14 +2485,21 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       }
       s.M[i][j] = v;
     }
+    }
     if (lane < nv) {
+      float f[6];
+      if constexpr (MFMA_DYN) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) f[k] = dscr[lane * 8 + k];
+      } else {
       uint32_t sm = m->dof_submask[lane];
-      float f[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      f[0] = f[1] = f[2] = f[3] = f[4] = f[5] = 0.f;
       while (sm) {
         const int c = __builtin_ctz(sm);
         sm &= sm - 1;
 #pragma unroll
         for (int k = 0; k < 6; k++) f[k] += s.cfrc[c][k];
+      }
       }
       float bias = 0.f;
 #pragma unroll
@@ -3216,7 +3345,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         }
       }
       sync();
-      if (lane < nc && args.theta && live) args.theta[(size_t)b * nc * H + lane * H + t] = s.qpos[m->ctrl_qposadr[lane]];
+      if (lane < nc && args.theta && live) args.theta[(size_t)b * nc * H + lane * H + t] = s.qpos[ctrl_qa];
     }
   }
 
