@@ -1864,11 +1864,11 @@ __device__ __forceinline__ mfx4 mm16(AF&& af, BF&& bf, mfx4 acc, int lane) {
   }
   return acc;
 }
-// the same for the 32-wide (dual-arm) Newton on v_mfma_f32_32x32x2_f32 (off:
-// measured neutral on C4, 68.3 / 70.4 vs 70.5 / 70.2 ms -- its 32-wide
-// readlane Cholesky, not the Hessian sum, is the cost)
+// the same for the 32-wide (dual-arm) Newton on v_mfma_f32_32x32x2_f32
+// (neutral while the 32-wide readlane Cholesky dominated; with the blocked
+// per-tree solve C4 66.2 -> 65.2 ms)
 #ifndef MPCR_MFMA_HESS_W
-#define MPCR_MFMA_HESS_W 0
+#define MPCR_MFMA_HESS_W 1
 #endif
 // The dual-arm variant is compiled for 2 waves/SIMD (<= 256 registers incl.
 // AGPRs; uncapped it took 274 and ran 1 wave/SIMD): with its 21.6 KB image,
