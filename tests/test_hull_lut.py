@@ -1,0 +1,70 @@
+"""The hull support start table (model format v6, `cmodel.hull_luts`) and the
+cube-map cell mapping the oracle and the kernel share (oracle lut_cell /
+rollout.hip lut_cell): every cell names a vertex of its own hull that is
+extreme along the cell centre, and the climb from it reaches the oracle's
+support point (tests/test_oracle.py covers the rollouts)."""
+import numpy as np
+import pytest
+
+from manipulator_mujoco_amd import cmodel, models
+
+
+def lut_cell(l, R=cmodel.LUT_R):
+    """numpy restatement of the oracle's lut_cell (major axis lowest on ties)."""
+    a = np.abs(l)
+    ax = 0 if (a[0] >= a[1] and a[0] >= a[2]) else (1 if a[1] >= a[2] else 2)
+    la = a[ax]
+    if not la > 0:
+        return 0
+    iu = int(np.floor((l[(ax + 1) % 3] / la + 1.0) * 0.5 * R))
+    iv = int(np.floor((l[(ax + 2) % 3] / la + 1.0) * 0.5 * R))
+    iu, iv = min(max(iu, 0), R - 1), min(max(iv, 0), R - 1)
+    return (2 * ax + (1 if l[ax] < 0 else 0)) * R * R + iu * R + iv
+
+
+@pytest.fixture(scope="module")
+def dual_arm():
+    return models.load("dual_arm", 0.05)
+
+
+def test_cell_dirs_map_to_their_own_cells():
+    dirs = cmodel.lut_cell_dirs()
+    assert dirs.shape == (6 * cmodel.LUT_R ** 2, 3)
+    for c in range(0, len(dirs), 7):
+        assert lut_cell(dirs[c]) == c
+
+
+def test_table_layout_and_extremes(dual_arm):
+    m = dual_arm
+    adr, lut = cmodel.hull_luts(m)
+    hulls = np.where((np.asarray(m.geom_hulladr) >= 0) & (np.asarray(m.geom_hullnum) > 0))[0]
+    assert len(hulls) == 14
+    ncell = 6 * cmodel.LUT_R ** 2
+    assert lut.size == ncell * len(hulls)
+    verts = np.asarray(m.hull_vert).reshape(-1, 3)
+    dirs = cmodel.lut_cell_dirs()
+    for g in hulls:
+        a, n = int(m.geom_hulladr[g]), int(m.geom_hullnum[g])
+        cells = lut[adr[g]:adr[g] + ncell]
+        assert ((cells >= a) & (cells < a + n)).all()  # the geom's own hull
+        best = (dirs @ verts[a:a + n].T).max(axis=1)
+        got = np.einsum("ij,ij->i", dirs, verts[cells])
+        assert np.allclose(got, best, rtol=0, atol=1e-12)  # extreme along the cell centre
+    for g in range(int(m.ngeom)):
+        if g not in hulls:
+            assert adr[g] == -1
+
+
+def test_packed_struct_carries_the_table(dual_arm):
+    s = dual_arm.to_struct()
+    adr, lut = cmodel.hull_luts(dual_arm)
+    assert s.version == cmodel.VERSION == 6
+    got_adr = np.ctypeslib.as_array(s.geom_lutadr)[:int(dual_arm.ngeom)]
+    assert (got_adr == adr).all()
+    assert (np.ctypeslib.as_array(s.hull_lut)[:lut.size] == lut).all()
+
+
+def test_models_without_hulls_have_no_table():
+    m = models.load("scene_mjx", 0.05)
+    adr, lut = cmodel.hull_luts(m)
+    assert lut.size == 0 and (adr == -1).all()
