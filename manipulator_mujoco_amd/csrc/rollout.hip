@@ -1598,7 +1598,10 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
 // ---------------------------------------------------------------------------
 // line search point (MJX-style, see oracle)
 
-struct LsPt { float alpha, cost, d0, d1; };
+// cost: complete, or (narrow kernel, full == false) without its constant
+// part q0 (the active rows' 0.5 D jar^2 + the Gauss term), which the bracket
+// never reads: the line search adds it once for the final two points
+struct LsPt { float alpha, cost, d0, d1; bool full; };
 
 // elliptic rows: efc_src = (5 << 24) | (contact << 14) | (pair << 4) | side
 __device__ __forceinline__ bool ell_row(int src) { return (src >> 24) == 5; }
@@ -1630,22 +1633,41 @@ __device__ __forceinline__ LsPt ls_make(float alpha, float q0, float q1, float q
   p.cost = alpha * alpha * q2 + alpha * q1 + q0;
   p.d0 = 2.f * alpha * q2 + q1;
   p.d1 = 2.f * q2 + (q2 == 0.f ? kMinVal : 0.f);
+  p.full = true;
   return p;
 }
 
-template <class S>
+template <class S, bool Q0 = true>
 __device__ __forceinline__ LsPt ls_eval(const S& s, int lane, const float qg[3], float alpha) {
   float q0, q1, q2;
   ls_rows(s, lane, alpha, q0, q1, q2);
-  q0 = hsum<S::CPW>(q0) + qg[0];
+  q0 = Q0 ? hsum<S::CPW>(q0) + qg[0] : 0.f;
   q1 = hsum<S::CPW>(q1) + qg[1];
   q2 = hsum<S::CPW>(q2) + qg[2];
-  return ls_make(alpha, q0, q1, q2);
+  LsPt p = ls_make(alpha, q0, q1, q2);
+  p.full = Q0;
+  return p;
+}
+// the deferred constant parts of two line-search points in one row pass
+template <class S>
+__device__ __forceinline__ void ls_finish(const S& s, int lane, const float qg[3], LsPt& a, LsPt& b) {
+  float qa = 0.f, qb = 0.f;
+  for (int r = lane; r < s.nefc; r += S::HL) {
+    const float jar = s.efc_jar[r], jv = s.efc_jv[r];
+    const bool eq = (s.efc_src[r] >> 24) == 1;
+    const float c0 = 0.5f * s.efc_D[r] * jar * jar;
+    if (eq || jar + a.alpha * jv < 0.f) qa += c0;
+    if (eq || jar + b.alpha * jv < 0.f) qb += c0;
+  }
+  qa = hsum<S::CPW>(qa) + qg[0];
+  qb = hsum<S::CPW>(qb) + qg[0];
+  if (!a.full) { a.cost = a.cost + qa; a.full = true; }
+  if (!b.full) { b.cost = b.cost + qb; b.full = true; }
 }
 
 // three line-search points in one pass over the rows; the 9 reductions are
 // independent so their DPP chains interleave
-template <class S>
+template <class S, bool Q0 = true>
 __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3], float a0, float a1, float a2,
                                          LsPt& p0, LsPt& p1, LsPt& p2) {
   float q[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1663,10 +1685,11 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
     }
   }
 #pragma unroll
-  for (int k = 0; k < 9; k++) q[k] = hsum<S::CPW>(q[k]) + qg[k % 3];
+  for (int k = 0; k < 9; k++) q[k] = (Q0 || k % 3) ? hsum<S::CPW>(q[k]) + qg[k % 3] : 0.f;
   p0 = ls_make(a0, q[0], q[1], q[2]);
   p1 = ls_make(a1, q[3], q[4], q[5]);
   p2 = ls_make(a2, q[6], q[7], q[8]);
+  p0.full = p1.full = p2.full = Q0;
 }
 
 // ---------------------------------------------------------------------------
@@ -3198,7 +3221,8 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             ls_cones3(s, m, lane, al, e);
             ls_add(p0, e[0], e[1], e[2]);
           }
-          LsPt lo = ls_eval(s, lane, qg, p0.alpha - p0.d0 / p0.d1);
+          constexpr bool LSQ0 = S::WIDE;  // narrow: q0 deferred to ls_finish
+          LsPt lo = ls_eval<S, LSQ0>(s, lane, qg, p0.alpha - p0.d0 / p0.d1);
           if (ell_ls) {
             const float al[3] = {lo.alpha, 0.f, 0.f};
             float e[9];
@@ -3221,8 +3245,8 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             // dual arm ran ~20 passes per Newton iteration against ~2.4 in fp64)
             if (fabsf(hi.alpha - lo.alpha) <= 1e-6f * fmaxf(fabsf(lo.alpha), fabsf(hi.alpha))) break;
             LsPt lo_next, hi_next, mid;
-            ls_eval3(s, lane, qg, lo.alpha - lo.d0 / lo.d1, hi.alpha - hi.d0 / hi.d1, 0.5f * (lo.alpha + hi.alpha),
-                     lo_next, hi_next, mid);
+            ls_eval3<S, LSQ0>(s, lane, qg, lo.alpha - lo.d0 / lo.d1, hi.alpha - hi.d0 / hi.d1,
+                              0.5f * (lo.alpha + hi.alpha), lo_next, hi_next, mid);
             if (ell_ls) {
               const float al[3] = {lo_next.alpha, hi_next.alpha, mid.alpha};
               float e[9];
@@ -3241,6 +3265,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             if (s4) hi = mid;
             swap = s1 || s2 || s3 || s4;
           }
+          if constexpr (!LSQ0) ls_finish(s, lane, qg, lo, hi);
           const bool improved = lo.cost < p0.cost || hi.cost < p0.cost;
           const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
           if (args.dbg && b == 0 && t == H - 1 && lane == 0 && it == 0) {
