@@ -73,6 +73,7 @@ struct mpcr_engine {
   float* d_jx = nullptr;         // max_n x (MAXEFC - JL) x LDJ: J rows past the LDS ones
   float* d_td = nullptr;         // (max_n + 1) x nctrl x H joint-velocity table (thetadot not requested)
   short* d_hints = nullptr;      // max_n x NHINT x 2 (dual-arm class): hull-climb starts
+  unsigned* d_pace = nullptr;    // MPCR_PACE_SLOTS: the rollout kernel's per-wave-slot progress (pacing)
   // convex hulls (dual-arm class)
   float4* d_hull_vert = nullptr;
   int2* d_hull_info = nullptr;
@@ -776,6 +777,7 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
                                        : (SmemN::MAXEFC - SmemN::JL + 1) * SmemN::LDJ)) !=
           hipSuccess ||
       hipMalloc(&e->d_hints, sizeof(short) * 2 * (size_t)max_n * (e->wide ? SmemW::NHINT : 1)) != hipSuccess ||
+      hipMalloc(&e->d_pace, sizeof(unsigned) * MPCR_PACE_SLOTS) != hipSuccess ||
       hipMalloc(&e->d_td, sizeof(float) * ((size_t)max_n + 1) * (size_t)(e->host.nctrl > 0 ? e->host.nctrl : 1) *
                               (size_t)horizon) != hipSuccess) {
     mpcr_engine_free(e);
@@ -784,7 +786,8 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
   if (hipMemcpy(e->d_model, &e->dev, sizeof(DevModel), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(e->d_pdot, pdot, sizeof(float) * horizon * nbasis, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(e->d_hints, 0xff, sizeof(short) * 2 * (size_t)max_n * (e->wide ? SmemW::NHINT : 1)) !=
-          hipSuccess) {
+          hipSuccess ||
+      hipMemset(e->d_pace, 0xff, sizeof(unsigned) * MPCR_PACE_SLOTS) != hipSuccess) {
     mpcr_engine_free(e);
     return fail(MPCR_EHIP, "model upload failed");
   }
@@ -807,6 +810,7 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_jx);
   (void)hipFree(e->d_td);
   (void)hipFree(e->d_hints);
+  (void)hipFree(e->d_pace);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
   (void)hipFree(e->d_hull_adjv);
@@ -854,6 +858,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.jx = e->d_jx;
   a.tdscratch = e->d_td;
   a.hints = e->d_hints;
+  a.pace = e->d_pace;
   a.dpar = l.dpar;
   a.state = l.state;
   a.plant = l.plant;
@@ -1135,6 +1140,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   a.jx = e->d_jx;
   a.tdscratch = e->d_td;
   a.hints = e->d_hints;
+  a.pace = e->d_pace;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);
@@ -1142,6 +1148,36 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   HIPCHK(hipMemcpy(phases16, d_prof, 24 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   e->dev.prof = nullptr;
   HIPCHK(hipMemcpy(e->d_model, &e->dev, sizeof(DevModel), hipMemcpyHostToDevice));
+  (void)hipFree(d_prof);
+  return MPCR_OK;
+}
+#endif
+
+#ifdef MPCR_WAVETIME
+// diagnostic build only: per wave (start, end) on the 100 MHz clock, shader
+// cycles, (XCC_ID << 32 | HW_ID) -- 4 u64 per candidate
+extern "C" int mpcr_rollout_wavetime(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
+                                     const float* w, const float* ptgt, const float* qtgt, unsigned long long* out) {
+  HIPCHK(hipSetDevice(e->device));
+  const int nc = e->host.nctrl;
+  const size_t cols = layout == MPCR_LAYOUT_XI ? (size_t)nc * e->nbasis : (size_t)nc * e->H;
+  unsigned long long* d_prof = nullptr;
+  HIPCHK(hipMalloc(&d_prof, 4 * (size_t)n * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(d_prof, 0, 4 * (size_t)n * sizeof(unsigned long long)));
+  HIPCHK(hipMemcpy(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice));
+  RolloutArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.m = e->d_model; a.input = e->d_in; a.pdot = e->d_pdot; a.cost4 = e->d_cost; a.prof = d_prof;
+  a.slot_prev = e->d_slot_prev;
+  a.jx = e->d_jx;
+  a.tdscratch = e->d_td;
+  a.hints = e->d_hints;
+  a.pace = e->d_pace;
+  a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
+  fill_par(a.par, nc, q0, w, ptgt, qtgt);
+  rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, d_prof, 4 * (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(d_prof);
   return MPCR_OK;
 }

@@ -34,6 +34,9 @@ enum { DBG_NCON = 0, DBG_NEFC = 1, DBG_CON = 2, DBG_MAXCON = 32, DBG_ROW = DBG_C
 enum { ST_QPOS = 0, ST_QVEL = DX_NQ, ST_QWS = ST_QVEL + DX_NV, ST_QACC = ST_QWS + DX_NV, ST_EEF = ST_QACC + DX_NV,
        ST_N = ST_EEF + 8 };
 
+// pacing table: (XCC 8 x SE 8 x SH 2 x CU 16 x SIMD 4) groups of 16 wave slots
+constexpr unsigned MPCR_PACE_SLOTS = 8u * 8u * 2u * 16u * 4u * 16u;
+
 struct RolloutArgs {
   const DevModel* m;
   const float* input;
@@ -50,6 +53,9 @@ struct RolloutArgs {
   short* hints;        // n x NHINT x 2: hull-climb start per convex pair and side (dual-arm class)
   unsigned long long* prof;  // per-phase cycles (MPCR_PROFILE builds only)
   float* tdscratch;  // (n + 1) x nctrl x H: the joint-velocity table when thetadot is not requested
+  // per hardware wave slot: the step a resident wave is on (~0u when none),
+  // MPCR_PACE_SLOTS words; the kernel's pacing reads its SIMD's 16 slots
+  unsigned* pace;
   float* dbg;  // parity debugging (mpcr_plant_step_debug): candidate 0's last step, DBG_* layout
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs

@@ -48,6 +48,15 @@ namespace mpcr {
 #define PROF_FLUSH
 #define PROF_COUNT(m, i)
 #endif
+// Pacing (load balance of a one-round launch): at N = 4096 every candidate is
+// resident at once (4 waves per SIMD) and the launch ends with the slowest
+// candidate, ~18 % after the mean one (tools/wavetime.py).  Each wave posts
+// the step it is on in its SIMD's slot group and takes an issue priority
+// equal to the number of its SIMD mates ahead of it, so the waves sharing a
+// SIMD progress together and the SIMD drains when its total work is done.
+#ifndef MPCR_PACE
+#define MPCR_PACE 1
+#endif
 #ifndef MPCR_TD_TABLE
 #define MPCR_TD_TABLE 1
 #endif
@@ -1998,6 +2007,24 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   // every step; the per-step model launder would otherwise reload them)
   const int ctrl_qa = lane < nc ? m->ctrl_qposadr[lane] : 0, ctrl_da = lane < nc ? m->ctrl_dofadr[lane] : 0;
   PROF_DECL
+#if MPCR_PACE
+  unsigned* pace = nullptr;
+  int pace_own = 0;
+  unsigned pace_v = ~0u;
+  if (S::CPW == 1 && args.pace) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID[3:0]
+    const unsigned grp = ((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) *
+                             4u + ((hw >> 4) & 3u);
+    pace = args.pace + grp * 16u;
+    pace_own = (int)(hw & 15u);
+  }
+#endif
+#ifdef MPCR_WAVETIME
+  // diagnostic build: per-wave start / end (constant 100 MHz clock), shader
+  // cycles and the hardware slot the wave ran on (load-balance study)
+  const unsigned long long wt_t0 = __builtin_amdgcn_s_memrealtime(), wt_c0 = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int t = 0; t < H; t++) {
     // Launder the model pointer every step: otherwise the compiler hoists
@@ -2006,6 +2033,12 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     // stay in their phases and hit L1/L2.
     LAUNDER_MODEL();
     if constexpr (!WIDE && MPCR_LANE_LAUNDER) LAUNDER_LANE();
+#if MPCR_PACE
+    if (pace) {  // post this step, read the SIMD mates' (consumed mid-step)
+      if (lane == pace_own) __hip_atomic_store(pace + lane, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < 16) pace_v = __hip_atomic_load(pace + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
     // ---- qvel[:nctrl] = thetadot_t ----------------------------------------------
 #if MPCR_TD_TABLE
     if (lane < nc) {
@@ -2567,6 +2600,15 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 
     STAMP(6);
     STOP_AT(6)
+#if MPCR_PACE
+    if (pace) {  // priority = SIMD mates ahead of this wave (0..3)
+      const int ahead = __popcll(__ballot(lane < 16 && lane != pace_own && pace_v != ~0u && pace_v > (unsigned)t));
+      if (ahead >= 3) __builtin_amdgcn_s_setprio(3);
+      else if (ahead == 2) __builtin_amdgcn_s_setprio(2);
+      else if (ahead == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
     //      slots; active contacts compacted into the list; box-box pairs
@@ -3406,6 +3448,19 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       atomicMin(args.best_key, k64);
     }
   }
+#if MPCR_PACE
+  if (pace && lane == pace_own) __hip_atomic_store(pace + lane, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+#ifdef MPCR_WAVETIME
+  if (lane == 0 && live && args.prof) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), t1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    args.prof[4 * (size_t)b + 0] = wt_t0;
+    args.prof[4 * (size_t)b + 1] = t1;
+    args.prof[4 * (size_t)b + 2] = c1 - wt_c0;
+    args.prof[4 * (size_t)b + 3] = ((unsigned long long)xcc << 32) | hwid;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
