@@ -2011,7 +2011,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   unsigned* pace = nullptr;
   int pace_own = 0;
   unsigned pace_v = ~0u;
-  if (S::CPW == 1 && args.pace) {
+  // narrow kernel only: the dual-arm one runs ~2.3 rounds at 4096 (7 blocks
+  // per CU), the dispatcher backfills, and pacing measured 1.7 % slower there
+  if (!WIDE && S::CPW == 1 && args.pace) {
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID[3:0]
     const unsigned grp = ((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) *

@@ -18,7 +18,16 @@ run() {  # name timeout cmd...
   if fatal $rc; then echo "[session] fatal rc=$rc in $name, stopping"; exit $rc; fi
   return 0
 }
-STEPS=${STEPS:-bench,prof,pmc}
+STEPS=${STEPS:-tests,bench,prof,pmc,wavetime}
+if [[ $STEPS == *tests* ]]; then
+  run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+fi
+if [[ $STEPS == *abdual* ]]; then  # pacing A/B on the dual-arm shard (build_variants/{nopace,pace}.so)
+  i=0
+  for v in nopace pace nopace pace; do
+    i=$((i+1)); MODEL=dual_arm N=4096 H=100 R=3 run ab_dual_${i}_$v 200 python tools/ab_time.py build_variants/$v.so
+  done
+fi
 if [[ $STEPS == *bench* ]]; then
   run bench_c3 300 python bench.py
   run bench_c2 300 python bench.py --config c2
@@ -34,5 +43,8 @@ if [[ $STEPS == *pmc* ]]; then
     i=$((i+1))
     run pmc$i 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
   done
+fi
+if [[ $STEPS == *wavetime* ]]; then
+  N=4096 run wavetime 120 python tools/wavetime.py scene_mjx $OUT/wavetime_c3_4096.json
 fi
 echo "[session] done"
