@@ -207,6 +207,32 @@ int mpcr_cem_update(mpcr_cem* c, const float* xi, int n, const float* cost, int 
                     float lamda, float alpha_mean, float alpha_cov, float reg, float* mean, float* cov, int flags,
                     void* stream);
 
+/* ---- multi-GPU exchange over RCCL / xGMI (SURVEY.md §8b "later":
+   mpcr_comm_init; §8e).  One process (or host thread) per GPU, candidates
+   sharded by rank (rank r rolls out [r n, (r+1) n) with index_base = r n).
+   Replaces the torch.distributed path of manipulator_mujoco_amd/dist.py for
+   hosts without Python; the reference itself is single-device
+   (SBP/mjx_planner.py:395 argmin, :305-310 elites).  RCCL is dlopen'ed at the
+   first call (librccl.so.1). */
+#define MPCR_COMM_ID_BYTES 128
+typedef struct mpcr_comm mpcr_comm;
+/* rank 0 creates the id and hands it to the other ranks out of band */
+int mpcr_comm_unique_id(unsigned char* id_out /* MPCR_COMM_ID_BYTES */);
+int mpcr_comm_init(int rank, int nranks, const unsigned char* id, int device, mpcr_comm** out);
+void mpcr_comm_free(mpcr_comm* c);
+/* in place, device pointer: global MIN of count packed best keys (the
+   rollout's fused key is unsigned-ordered, so this is the global jnp.argmin:
+   NaN first, ties to the lowest global index) */
+int mpcr_comm_allreduce_key(mpcr_comm* c, uint64_t* d_key, int count, void* stream);
+/* rank-major all-gather of count floats per rank (device pointers) */
+int mpcr_comm_allgather(mpcr_comm* c, const float* d_send, float* d_recv, size_t count, void* stream);
+/* sharded elites: local top-kl (kl = min(k, n)) of d_cost[n], their rows
+   (d_xi row | cost) all-gathered into d_rows (nranks x kl x (nv+1)), and
+   d_sel[k] = the global top-k positions in d_rows, in the single-GPU
+   argsort(kind="stable")[:k] order.  Every rank passes the same n, nv, k. */
+int mpcr_comm_gather_elites(mpcr_comm* c, const float* d_cost, const float* d_xi, int n, int nv, int k, float* d_rows,
+                            int* d_sel, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

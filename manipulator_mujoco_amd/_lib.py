@@ -27,10 +27,11 @@ EXPORTS = (
     "mpcr_rollout_cost", "mpcr_argmin", "mpcr_best_key_decode", "mpcr_topk", "mpcr_cem_create", "mpcr_cem_free",
     "mpcr_cem_factor", "mpcr_cem_sample_project", "mpcr_project", "mpcr_cem_update", "mpcr_rollout_cost_dp",
     "mpcr_plant_create", "mpcr_plant_free", "mpcr_plant_set_state", "mpcr_plant_get_state", "mpcr_plant_step",
-    "mpcr_rollout_occupancy",
+    "mpcr_rollout_occupancy", "mpcr_comm_unique_id", "mpcr_comm_init", "mpcr_comm_free", "mpcr_comm_allreduce_key",
+    "mpcr_comm_allgather", "mpcr_comm_gather_elites",
 )
 _VOID = ("mpcr_last_error", "mpcr_model_free", "mpcr_engine_free", "mpcr_best_key_decode", "mpcr_cem_free",
-         "mpcr_plant_free")
+         "mpcr_plant_free", "mpcr_comm_free")
 
 _lib = None
 
@@ -84,6 +85,13 @@ def load():
     lib.mpcr_rollout_occupancy.argtypes = [i, P(i)]
     lib.mpcr_plant_step_debug.argtypes = [vp, P(d), vp, i]
     lib.mpcr_plant_dbg_size.argtypes = []
+    lib.mpcr_comm_unique_id.argtypes = [ctypes.c_char_p]
+    lib.mpcr_comm_init.argtypes = [i, i, ctypes.c_char_p, i, P(vp)]
+    lib.mpcr_comm_free.argtypes = [vp]
+    lib.mpcr_comm_free.restype = None
+    lib.mpcr_comm_allreduce_key.argtypes = [vp, vp, i, vp]
+    lib.mpcr_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
+    lib.mpcr_comm_gather_elites.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
     for name in EXPORTS + ("mpcr_rollout_trace", "mpcr_plant_step_debug", "mpcr_plant_dbg_size"):
         if name not in _VOID:
             getattr(lib, name).restype = i

@@ -25,7 +25,7 @@ UNITS = [(os.path.join(CSRC, "engine.hip"), []),
                                               "-Xarch_device", "-fassociative-math", "-Xarch_device", "-fno-signed-zeros",
                                               "-Xarch_device", "-fno-trapping-math"])]
 SRC = [u for u, _ in UNITS]
-DEPS = SRC + [os.path.join(CSRC, f) for f in ("rollout.h", "cem.hip", "mpcr_device.h")] + [
+DEPS = SRC + [os.path.join(CSRC, f) for f in ("rollout.h", "cem.hip", "comm.hip", "mpcr_device.h")] + [
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mpcr.h", "mpcr_model.h")]
 OUT = os.path.join(HERE, "libmpcr.so")
 ARCH = os.environ.get("MPCR_OFFLOAD_ARCH", "gfx950")

@@ -1454,3 +1454,5 @@ extern "C" int mpcr_cem_update(mpcr_cem* c, const float* xi, int n, const float*
   if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
   return MPCR_OK;
 }
+
+#include "comm.hip"

@@ -144,3 +144,86 @@ def allgather_min(values, group=None):
     a = all_gather(values, group).cpu().numpy()
     return np.where(np.isnan(a).any(axis=0), np.nan, np.nanmin(np.where(np.isnan(a), np.inf, a), axis=0)).astype(
         np.float32)
+
+
+class RcclComm:
+    """The C ABI's own RCCL communicator (``mpcr_comm_*``, include/mpcr.h):
+    the same two exchanges as the torch.distributed functions above, for
+    hosts that embed libmpcr.so without Python.  Device tensors only.
+
+        uid = RcclComm.unique_id()            # rank 0, shared out of band
+        comm = RcclComm(rank, nranks, uid, device)
+    """
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+
+        from . import _lib
+        buf = ctypes.create_string_buffer(RcclComm.ID_BYTES)
+        _lib.check(_lib.load().mpcr_comm_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, rank: int, nranks: int, uid: bytes, device: int = 0):
+        import ctypes
+
+        from . import _lib
+        if len(uid) != self.ID_BYTES:
+            raise ValueError(f"unique id must be {self.ID_BYTES} bytes")
+        self._lib = _lib.load()
+        self.rank, self.nranks, self.device = rank, nranks, device
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.mpcr_comm_init(rank, nranks, uid, device, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.mpcr_comm_free(self.handle)
+            self.handle = None
+
+    __del__ = close
+
+    @staticmethod
+    def _stream(t):
+        import torch
+        return ctypes_ptr(torch.cuda.current_stream(t.device).cuda_stream)
+
+    def allreduce_min_key(self, key_tensor):
+        """In-place global MIN of packed uint64 keys held in an int64 device tensor."""
+        from . import _lib
+        _lib.check(self._lib.mpcr_comm_allreduce_key(self.handle, key_tensor.data_ptr(), key_tensor.numel(),
+                                                     self._stream(key_tensor)))
+        return key_tensor
+
+    def all_gather(self, x):
+        """(nranks, *x.shape) rank-major all-gather of a float32 device tensor."""
+        import torch
+
+        from . import _lib
+        src = x.contiguous()
+        out = torch.empty((self.nranks,) + tuple(src.shape), dtype=torch.float32, device=src.device)
+        _lib.check(self._lib.mpcr_comm_allgather(self.handle, src.data_ptr(), out.data_ptr(), src.numel(),
+                                                 self._stream(src)))
+        return out
+
+    def gather_elites(self, cost, xi, k):
+        """gather_elites above through mpcr_comm_gather_elites: returns
+        (gathered cost, gathered rows, selected positions)."""
+        import torch
+
+        from . import _lib
+        n, nv = xi.shape
+        kl = min(int(k), n)
+        rows = torch.empty((self.nranks * kl, nv + 1), dtype=torch.float32, device=xi.device)
+        sel = torch.empty(int(k), dtype=torch.int32, device=xi.device)
+        c, x = cost.contiguous(), xi.contiguous()
+        _lib.check(self._lib.mpcr_comm_gather_elites(self.handle, c.data_ptr(), x.data_ptr(), n, nv, int(k),
+                                                     rows.data_ptr(), sel.data_ptr(), self._stream(x)))
+        return rows[:, nv].contiguous(), rows[:, :nv].contiguous(), sel
+
+
+def ctypes_ptr(v: int):
+    import ctypes
+    return ctypes.c_void_p(v) if v else None

@@ -138,3 +138,17 @@ def test_mjcf_library_exports_its_header():
     assert names == ["mpcr_mjcf_compile", "mpcr_mjcf_free"]
     for n in names:
         assert hasattr(so, n), n
+
+
+def test_comm_entry_points_fail_cleanly():
+    """mpcr_comm_*: argument errors are EINVAL with a message; creating an id
+    either works (GPU host) or reports RCCL's error (no GPU) -- no crash."""
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    uid = ctypes.create_string_buffer(128)
+    assert lib.mpcr_comm_init(2, 2, uid, 0, ctypes.byref(h)) == -1
+    assert b"bad comm arguments" in lib.mpcr_last_error()
+    assert lib.mpcr_comm_unique_id(None) == -1
+    rc = lib.mpcr_comm_unique_id(uid)
+    assert rc == 0 or (rc == -3 and lib.mpcr_last_error())
+    lib.mpcr_comm_free(None)
