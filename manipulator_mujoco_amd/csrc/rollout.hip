@@ -57,6 +57,10 @@ namespace mpcr {
 #ifndef MPCR_PACE
 #define MPCR_PACE 1
 #endif
+// a mate counts as ahead when it is more than MPCR_PACE_LAG steps ahead
+#ifndef MPCR_PACE_LAG
+#define MPCR_PACE_LAG 0
+#endif
 #ifndef MPCR_TD_TABLE
 #define MPCR_TD_TABLE 1
 #endif
@@ -2604,7 +2608,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     STOP_AT(6)
 #if MPCR_PACE
     if (pace) {  // priority = SIMD mates ahead of this wave (0..3)
-      const int ahead = __popcll(__ballot(lane < 16 && lane != pace_own && pace_v != ~0u && pace_v > (unsigned)t));
+      const int ahead = __popcll(__ballot(lane < 16 && lane != pace_own && pace_v != ~0u && pace_v > (unsigned)t + MPCR_PACE_LAG));
       if (ahead >= 3) __builtin_amdgcn_s_setprio(3);
       else if (ahead == 2) __builtin_amdgcn_s_setprio(2);
       else if (ahead == 1) __builtin_amdgcn_s_setprio(1);
