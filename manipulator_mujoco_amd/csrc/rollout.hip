@@ -61,6 +61,14 @@ namespace mpcr {
 #ifndef MPCR_PACE_LAG
 #define MPCR_PACE_LAG 0
 #endif
+// ablation builds (timing attribution only; results are wrong): skip the
+// capsule-box deepest-point search / the narrow-phase functions in the mask
+#ifndef MPCR_ABL_DEEP
+#define MPCR_ABL_DEEP 0
+#endif
+#ifndef MPCR_ABL_FUNC
+#define MPCR_ABL_FUNC 0
+#endif
 #ifndef MPCR_TD_TABLE
 #define MPCR_TD_TABLE 1
 #endif
@@ -1176,7 +1184,7 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
 #pragma unroll
     for (int c = 0; c < 3; c++) pp[c] = a[c] + ts * dd[c];
     float g = point_box(pp, h, nl, q);
-    if (g <= 1e-6f) {  // on or in the box (penetrating segments land on the surface): the oracle's band
+    if (g <= 1e-6f && !MPCR_ABL_DEEP) {  // on or in the box (penetrating segments land on the surface): the oracle's band
       // deepest point of g(t) = max_k |x_k(t)| - h_k over its kinks
       float gbest = 1e30f, tbest = 0.f;
 #pragma unroll
@@ -2666,9 +2674,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       }
       float dist[4] = {1e30f, 1e30f, 1e30f, 1e30f}, pos[4][3] = {}, nrm[4][3] = {};
       int nsl = 0;
-      if (run && func != 4 && !defer) nsl = narrow_lane(m, s, hx, p, dist, pos, nrm);
+      if (run && func != 4 && !defer && !(MPCR_ABL_FUNC & (1 << func))) nsl = narrow_lane(m, s, hx, p, dist, pos, nrm);
       STAMP(11);
-      const unsigned long long bbm = hballot<S::CPW>(run && func == 4);
+      const unsigned long long bbm = hballot<S::CPW>(run && func == 4 && !(MPCR_ABL_FUNC & 16));
       emit_contacts(m, s, args, b, t, H, valid && func != 4 && !defer, p, nsl, dist, pos, nrm, cost_c);
       STAMP(12);
       if (bbm && !(m->disableflags & 16)) {
