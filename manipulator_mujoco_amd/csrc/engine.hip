@@ -1155,15 +1155,16 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
 
 #ifdef MPCR_WAVETIME
 // diagnostic build only: per wave (start, end) on the 100 MHz clock, shader
-// cycles, (XCC_ID << 32 | HW_ID) -- 4 u64 per candidate
+// cycles, (XCC_ID << 32 | HW_ID) -- 4 u64 per candidate; then per candidate
+// (line-search passes << 32 | Newton iterations, convex flush chunks)
 extern "C" int mpcr_rollout_wavetime(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
                                      const float* w, const float* ptgt, const float* qtgt, unsigned long long* out) {
   HIPCHK(hipSetDevice(e->device));
   const int nc = e->host.nctrl;
   const size_t cols = layout == MPCR_LAYOUT_XI ? (size_t)nc * e->nbasis : (size_t)nc * e->H;
   unsigned long long* d_prof = nullptr;
-  HIPCHK(hipMalloc(&d_prof, 4 * (size_t)n * sizeof(unsigned long long)));
-  HIPCHK(hipMemset(d_prof, 0, 4 * (size_t)n * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&d_prof, 6 * (size_t)n * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(d_prof, 0, 6 * (size_t)n * sizeof(unsigned long long)));
   HIPCHK(hipMemcpy(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice));
   RolloutArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1177,7 +1178,7 @@ extern "C" int mpcr_rollout_wavetime(mpcr_engine* e, const float* input, int lay
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(out, d_prof, 4 * (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, d_prof, 6 * (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   (void)hipFree(d_prof);
   return MPCR_OK;
 }

@@ -947,19 +947,26 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   return true;
 }
 
-// argmax step with the oracle's relative tie band (oracle beats()): near-ties
-// resolve to the lowest vertex index in both
 __device__ __forceinline__ bool beats(float v, float best) { return v > best + 1e-4f * fabsf(best) + 1e-12f; }
+__device__ __forceinline__ bool near_max(float v, float mx) { return v >= mx - (1e-4f * fabsf(mx) + 1e-12f); }
+__device__ __forceinline__ float wmax(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
 
-// plane - mesh manifold, MJX's plane_convex (oracle col_plane_mesh): called
-// once the climb found a penetrating vertex (depth > 0).  Candidate set: hull
-// vertices penetrating by more than max(0, depth - 1 mm); a = first, b =
-// farthest from a, c = farthest from line ab, d = farthest from edge bc or ac
-// (bc on ties); repeated picks stay empty.  Passes 2-4 scan [a, last member].
+// Plane-mesh manifold (MJX plane_convex / _manifold_points, the oracle's
+// col_plane_mesh), wave-cooperative: every lane calls it with the same pair
+// (mesh g, plane normal n through xp, penetration depth) and lane q receives
+// the contacts.  The hull's vertices are scanned 64 at a time -- a first /
+// last ballot for the penetrating set, then per pick a wave max and a ballot
+// for its first index within the tie band (near_max, as the oracle) -- instead
+// of four serial per-lane scans (a 2691-vertex hull touching the table made a
+// handful of dual-arm candidates 3x slower than the rest).
 template <class S>
-__device__ __noinline__ int plane_mesh_manifold(const DevModel* __restrict__ m, const S& s, int g, const float n[3],
-                                                const float* xp, float depth, float dist[4], float pos[4][3],
-                                                float nrm[4][3]) {
+__device__ __noinline__ void plane_mesh_manifold_wave(const DevModel* __restrict__ m, const S& s, int g,
+                                                      const float n[3], const float* xp, float depth, int q, int lane,
+                                                      float dist[4], float pos[4][3], float nrm[4][3], int& nsl) {
   const float* R = s.gxmat[g];
   const float* xg = s.gxpos[g];
   float nl[3], pl[3];
@@ -971,35 +978,55 @@ __device__ __noinline__ int plane_mesh_manifold(const DevModel* __restrict__ m, 
   const float4* __restrict__ hv = m->hull_vert;
   auto sup = [&](const float4& v) { return (pl[0] - v.x) * nl[0] + (pl[1] - v.y) * nl[1] + (pl[2] - v.z) * nl[2]; };
   int ia = -1, il = -1;
-  for (int i = v0; i < v1; i++) {
-    if (sup(hv[i]) > thr) {
-      if (ia < 0) ia = i;
-      il = i;
+  for (int base = v0; base < v1; base += WAVE) {
+    const int i = base + lane;
+    const unsigned long long bm = __ballot(i < v1 && sup(hv[i < v1 ? i : v0]) > thr);
+    if (bm) {
+      if (ia < 0) ia = base + __builtin_ctzll(bm);
+      il = base + 63 - __builtin_clzll(bm);
     }
   }
-  if (ia < 0) return 1;  // the climb's vertex alone (threshold rounding)
-  const float4 a = hv[ia];
-  int ib = ia, ic = ia;
-  float best = -1.f;
-  for (int i = ia; i <= il; i++) {
-    const float4 v = hv[i];
-    if (!(sup(v) > thr)) continue;
-    const float e = (a.x - v.x) * (a.x - v.x) + (a.y - v.y) * (a.y - v.y) + (a.z - v.z) * (a.z - v.z);
-    if (beats(e, best)) { best = e; ib = i; }
+  if (ia < 0) {  // the climb's vertex alone (threshold rounding): lane q keeps it
+    if (lane == q) nsl = 1;
+    return;
   }
+  // max of e over the penetrating set, then its first index within the band
+  auto pick = [&](auto&& ef, float& mx) {
+    float lm = -1.f;
+    for (int base = ia; base <= il; base += WAVE) {
+      const int i = base + lane;
+      if (i <= il) {
+        const float4 v = hv[i];
+        if (sup(v) > thr) lm = fmaxf(lm, ef(v));
+      }
+    }
+    mx = wmax(lm);
+    for (int base = ia; base <= il; base += WAVE) {
+      const int i = base + lane;
+      bool hit = false;
+      if (i <= il) {
+        const float4 v = hv[i];
+        hit = sup(v) > thr && near_max(ef(v), mx);
+      }
+      const unsigned long long bm = __ballot(hit);
+      if (bm) return base + __builtin_ctzll(bm);
+    }
+    return ia;  // unreachable: the maximum itself is within the band
+  };
+  const float4 a = hv[ia];
+  float mx;
+  const int ib = pick([&](const float4& v) {
+    return (a.x - v.x) * (a.x - v.x) + (a.y - v.y) * (a.y - v.y) + (a.z - v.z) * (a.z - v.z);
+  }, mx);
   const float4 b = hv[ib];
   float ab[3];
   {
     const float amb[3] = {a.x - b.x, a.y - b.y, a.z - b.z};
     cross(ab, nl, amb);
   }
-  best = -1.f;
-  for (int i = ia; i <= il; i++) {
-    const float4 v = hv[i];
-    if (!(sup(v) > thr)) continue;
-    const float e = fabsf((a.x - v.x) * ab[0] + (a.y - v.y) * ab[1] + (a.z - v.z) * ab[2]);
-    if (beats(e, best)) { best = e; ic = i; }
-  }
+  const int ic = pick([&](const float4& v) {
+    return fabsf((a.x - v.x) * ab[0] + (a.y - v.y) * ab[1] + (a.z - v.z) * ab[2]);
+  }, mx);
   const float4 c = hv[ic];
   float ac[3], bc[3];
   {
@@ -1007,35 +1034,34 @@ __device__ __noinline__ int plane_mesh_manifold(const DevModel* __restrict__ m, 
     cross(ac, nl, amc);
     cross(bc, nl, bmc);
   }
-  float bbp = -1.f, bap = -1.f;
-  int ibp = ia, iap = ia;
-  for (int i = ia; i <= il; i++) {
-    const float4 v = hv[i];
-    if (!(sup(v) > thr)) continue;
-    const float e1 = fabsf((b.x - v.x) * bc[0] + (b.y - v.y) * bc[1] + (b.z - v.z) * bc[2]);
-    const float e2 = fabsf((a.x - v.x) * ac[0] + (a.y - v.y) * ac[1] + (a.z - v.z) * ac[2]);
-    if (beats(e1, bbp)) { bbp = e1; ibp = i; }
-    if (beats(e2, bap)) { bap = e2; iap = i; }
-  }
+  float bbp, bap;
+  const int ibp = pick([&](const float4& v) {
+    return fabsf((b.x - v.x) * bc[0] + (b.y - v.y) * bc[1] + (b.z - v.z) * bc[2]);
+  }, bbp);
+  const int iap = pick([&](const float4& v) {
+    return fabsf((a.x - v.x) * ac[0] + (a.y - v.y) * ac[1] + (a.z - v.z) * ac[2]);
+  }, bap);
   const int idx[4] = {ia, ib, ic, beats(bap, bbp) ? iap : ibp};
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     bool dup = false;
 #pragma unroll
     for (int t = 0; t < k; t++) dup |= idx[t] == idx[k];
-    dist[k] = 1e30f;
-    if (dup) continue;
     const float4 v = hv[idx[k]];
     const float l[3] = {v.x, v.y, v.z};
     float w[3];
     mv(w, R, l);
     const float d = -sup(v);
-    dist[k] = d;
+    if (lane == q) {
+      dist[k] = dup ? 1e30f : d;
 #pragma unroll
-    for (int e = 0; e < 3; e++) { pos[k][e] = w[e] + xg[e] - 0.5f * d * n[e]; nrm[k][e] = n[e]; }
+      for (int e = 0; e < 3; e++) { pos[k][e] = w[e] + xg[e] - 0.5f * d * n[e]; nrm[k][e] = n[e]; }
+    }
   }
-  return 4;
+  if (lane == q) nsl = 4;
 }
+
+constexpr int kPendingManifold = -4;  // narrow_lane: plane-mesh pair awaiting plane_mesh_manifold_wave
 
 // per-lane narrow phase for plane/capsule/box-vs-capsule pairs (box-box is
 // wave-cooperative, below).  out: dist[4], pos[4][3], nrm[4][3]
@@ -1270,8 +1296,8 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
       dist[0] = d;
 #pragma unroll
       for (int c = 0; c < 3; c++) { pos[0][c] = q[c] - 0.5f * d * n[c]; nrm[0][c] = n[c]; }
-      if (d < 0.f && m->geom_type[g2] == 7) return plane_mesh_manifold(m, s, g2, n, x1, -d, dist, pos, nrm);
-      return 1;
+      // a penetrating mesh: the caller runs the wave-cooperative manifold
+      return (d < 0.f && m->geom_type[g2] == 7) ? kPendingManifold : 1;
     }
   }
   return 0;
@@ -1930,6 +1956,42 @@ __device__ __forceinline__ mfx4 mm16(AF&& af, BF&& bf, mfx4 acc, int lane) {
 #define MPCR_ROLLOUT_ATTR
 #endif
 
+// 32-wide: acc += sum over constraint rows, two per v_mfma_f32_32x32x2_f32
+// (lane (gi, gq) supplies A = J[r0 + gq][gi] and B = bf(r, A)).  Rows < JL
+// come from LDS; the HBM-slab rows (heavily constrained candidates: 100+
+// rows) are read four row pairs at a time with the loads issued together,
+// instead of one dependent flat load per instruction.  Same MFMAs in the same
+// row order (pairs wholly past nefc skipped): bitwise the single loop.
+template <class S, class BF>
+__device__ __forceinline__ mfx16 mfma_rows32(const S& s, const float* gx, int nefc, int gi, int gq, BF&& bf,
+                                             mfx16 acc) {
+  static_assert(S::JL % 2 == 0, "a row pair never straddles the LDS / slab boundary");
+  const int n1 = nefc < S::JL ? nefc : S::JL;
+  for (int r0 = 0; r0 < n1; r0 += 2) {
+    const int r = r0 + gq;
+    const bool ok = r < nefc;
+    const float a = ok ? s.J[r][gi] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, ok ? bf(r, a) : 0.f, acc, 0, 0, 0);
+  }
+  if constexpr (S::JL < S::MAXEFC) {
+    for (int r0 = S::JL; r0 < nefc; r0 += 8) {
+      float a[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int r = r0 + 2 * u + gq;
+        a[u] = r < nefc ? gx[(r - S::JL) * S::LDJ + gi] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int r = r0 + 2 * u + gq;
+        if (r0 + 2 * u < nefc)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], r < nefc ? bf(r, a[u]) : 0.f, acc, 0, 0, 0);
+      }
+    }
+  }
+  return acc;
+}
+
 template <int NVW, int NBW, int NGW, bool WIDE>
 __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / SmemN::CPW) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
@@ -2038,6 +2100,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   // diagnostic build: per-wave start / end (constant 100 MHz clock), shader
   // cycles and the hardware slot the wave ran on (load-balance study)
   const unsigned long long wt_t0 = __builtin_amdgcn_s_memrealtime(), wt_c0 = __builtin_amdgcn_s_memtime();
+  unsigned wt_newton = 0, wt_ls = 0, wt_cvx = 0;  // Newton iterations, line-search passes, convex flush chunks
 #endif
 
   for (int t = 0; t < H; t++) {
@@ -2692,12 +2755,24 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         if (s.ncvx > S::CVXN - WAVE || (k + 1) * S::HL >= m->npair) {  // flush (pair order is kept)
           const int nc = s.ncvx;
           for (int i0 = 0; i0 < nc; i0 += S::HL) {
+#ifdef MPCR_WAVETIME
+            wt_cvx++;
+#endif
             const bool v = i0 + lane < nc;
             const int pc = v ? s.cvx[i0 + lane] : 0;
             float cd[4] = {1e30f, 1e30f, 1e30f, 1e30f}, cp[4][3] = {}, cn[4][3] = {};
-            const int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn, (args.dbg && b == 0 && t == H - 1) ? args.dbg
-                                                                                                     : nullptr)
-                                : 0;
+            int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn, (args.dbg && b == 0 && t == H - 1) ? args.dbg
+                                                                                               : nullptr)
+                          : 0;
+            for (unsigned long long pm = __ballot(cn_sl == kPendingManifold); pm; pm &= pm - 1) {
+              const int q = __builtin_ctzll(pm);  // penetrating plane-mesh pairs, one at a time, all lanes
+              const int pq = __shfl(pc, q);
+              const float dq = __shfl(cd[0], q);
+              const int gp = m->pair_g1[pq];
+              const float* Rp = s.gxmat[gp];
+              const float nq[3] = {Rp[2], Rp[5], Rp[8]};
+              plane_mesh_manifold_wave(m, s, m->pair_g2[pq], nq, s.gxpos[gp], -dq, q, lane, cd, cp, cn, cn_sl);
+            }
             STAMP(17);
             emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c);
             STAMP(18);
@@ -3050,6 +3125,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 #ifdef MPCR_PROFILE
           prof_acc[15] += 1;  // Newton iterations (low half of the counter, not cycles)
 #endif
+#ifdef MPCR_WAVETIME
+          wt_newton++;
+#endif
           // Ma, jar, cost at the current qacc; per-row force and active D
           const float ma = lane < nv ? dotN<NVW>(s.M[lane], s.qacc) : 0.f;
           float cc = 0.f;
@@ -3120,12 +3198,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             mfx16 gacc;
 #pragma unroll
             for (int v = 0; v < 16; v++) gacc[v] = 0.f;
-            for (int r0 = 0; r0 < nefc; r0 += 2) {
-              const int r = r0 + gq;
-              const bool ok = r < nefc;
-              const float a = ok ? jrow_ptr(s, gx, r)[gi] : 0.f;
-              gacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, ok ? s.efc_f[r] : 0.f, gacc, 0, 0, 0);
-            }
+            gacc = mfma_rows32(s, gx, nefc, gi, gq, [&](int r, float) { return s.efc_f[r]; }, gacc);
             float* qcs = s.srch;  // free until this iteration's search direction
             if (gi == 0) {
 #pragma unroll
@@ -3171,12 +3244,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
               for (int k = 0; k < QPL; k++) {
                 acc[4 * k] = hq[k].x; acc[4 * k + 1] = hq[k].y; acc[4 * k + 2] = hq[k].z; acc[4 * k + 3] = hq[k].w;
               }
-              for (int r0 = 0; r0 < nefc; r0 += 2) {
-                const int r = r0 + gq;
-                const bool ok = r < nefc;
-                const float a = ok ? jrow_ptr(s, gx, r)[gi] : 0.f;
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, ok ? s.efc_Da[r] * a : 0.f, acc, 0, 0, 0);
-              }
+              acc = mfma_rows32(s, gx, nefc, gi, gq, [&](int r, float a) { return s.efc_Da[r] * a; }, acc);
 #pragma unroll
               for (int k = 0; k < QPL; k++) hq[k] = make_float4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
             } else {
@@ -3292,6 +3360,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             if (!swap) break;
 #ifdef MPCR_PROFILE
             prof_acc[15] += 1ull << 32;  // line-search passes (high half of the counter)
+#endif
+#ifdef MPCR_WAVETIME
+            wt_ls++;
 #endif
             if (args.dbg && b == 0 && t == H - 1 && lane == 0 && it == 0) args.dbg[DBG_INFO + 5] = (float)ls;
             if (lo.d0 < 0.f && lo.d0 > -gtol) break;
@@ -3473,6 +3544,8 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     args.prof[4 * (size_t)b + 1] = t1;
     args.prof[4 * (size_t)b + 2] = c1 - wt_c0;
     args.prof[4 * (size_t)b + 3] = ((unsigned long long)xcc << 32) | hwid;
+    args.prof[4 * (size_t)args.n + 2 * (size_t)b] = ((unsigned long long)wt_ls << 32) | wt_newton;
+    args.prof[4 * (size_t)args.n + 2 * (size_t)b + 1] = wt_cvx;
   }
 #endif
 }

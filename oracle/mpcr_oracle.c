@@ -1238,11 +1238,13 @@ static void col_convex(const mpcr_model_t* m, odata* d, int pair, int g1, int g2
   set_contact(out, -depth, pos, n);
 }
 
-/* argmax with a relative tie band: a later candidate replaces the best only
-   if it beats it by more than 1e-4 of its magnitude, so near-ties (symmetric
-   hulls, fp32 vs fp64 rounding) resolve to the lowest vertex index in the
-   oracle and the kernel alike */
+/* argmax with a relative tie band, independent of scan order: the lowest
+   index whose value lies within 1e-4 of the maximum's magnitude (+1e-12), so
+   near-ties (symmetric hulls, fp32 vs fp64 rounding) resolve to the lowest
+   vertex index in the oracle and the kernel alike (the kernel evaluates it as
+   a wave max and a ballot over 64 vertices at a time) */
 static int beats(double v, double best) { return v > best + 1e-4 * fabs(best) + 1e-12; }
+static int near_max(double v, double mx) { return v >= mx - (1e-4 * fabs(mx) + 1e-12); }
 
 /* plane - mesh: MJX's plane_convex manifold (mujoco-mjx 3.3.1,
    mjx/_src/collision_convex.py plane_convex + _manifold_points; MJX is the
@@ -1250,7 +1252,7 @@ static int beats(double v, double best) { return v > best + 1e-4 * fabs(best) + 
    that penetrate the plane and lie within 1 mm of the deepest one form the
    candidate set; of those: a = the first, b = the farthest from a, c = the
    farthest from the line ab (in the plane), d = the farthest from the edges
-   bc / ac.  Repeated picks are inactive (dist 1 in MJX, 1e30 here); every
+   bc / ac ("farthest": near_max's lowest index within the tie band).  Repeated picks are inactive (dist 1 in MJX, 1e30 here); every
    contact carries the plane normal and sits half-way through the
    penetration.  No penetrating vertex: slot 0 reports the deepest vertex's
    (non-negative) distance, slots 1-3 stay empty -- the restatement for
@@ -1289,39 +1291,42 @@ static void col_plane_mesh(const mpcr_model_t* m, odata* d, int pair, int gp, in
   }
   const double* a = m->hull_vert[ia];
   int ib = ia, ic = ia, id = ia;
-  double best = -1;
-  for (int i = ia; i <= ilast; i++) {
-    if (!(SUP(i) > thr)) continue;
-    const double* v = m->hull_vert[i];
-    double e = (a[0] - v[0]) * (a[0] - v[0]) + (a[1] - v[1]) * (a[1] - v[1]) + (a[2] - v[2]) * (a[2] - v[2]);
-    if (beats(e, best)) { best = e; ib = i; }
-  }
+  /* each pick: the maximum over the candidate set, then its first index
+     within the tie band (near_max) */
+#define PICK(EXPR, OUT)                                                  \
+  do {                                                                   \
+    double mx_ = -1;                                                     \
+    for (int i = ia; i <= ilast; i++) {                                  \
+      if (!(SUP(i) > thr)) continue;                                     \
+      const double* v = m->hull_vert[i];                                 \
+      const double e = (EXPR);                                           \
+      if (e > mx_) mx_ = e;                                              \
+    }                                                                    \
+    for (int i = ia; i <= ilast; i++) {                                  \
+      if (!(SUP(i) > thr)) continue;                                     \
+      const double* v = m->hull_vert[i];                                 \
+      if (near_max((EXPR), mx_)) { OUT = i; break; }                     \
+    }                                                                    \
+    best_ = mx_;                                                         \
+  } while (0)
+  double best_;
+  PICK((a[0] - v[0]) * (a[0] - v[0]) + (a[1] - v[1]) * (a[1] - v[1]) + (a[2] - v[2]) * (a[2] - v[2]), ib);
   const double* b = m->hull_vert[ib];
   double amb[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]}, ab[3];
   cross3(ab, nl, amb);
-  best = -1;
-  for (int i = ia; i <= ilast; i++) {
-    if (!(SUP(i) > thr)) continue;
-    const double* v = m->hull_vert[i];
-    double e = fabs((a[0] - v[0]) * ab[0] + (a[1] - v[1]) * ab[1] + (a[2] - v[2]) * ab[2]);
-    if (beats(e, best)) { best = e; ic = i; }
-  }
+  PICK(fabs((a[0] - v[0]) * ab[0] + (a[1] - v[1]) * ab[1] + (a[2] - v[2]) * ab[2]), ic);
   const double* c = m->hull_vert[ic];
   double amc[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]}, bmc[3] = {b[0] - c[0], b[1] - c[1], b[2] - c[2]};
   double ac[3], bc[3];
   cross3(ac, nl, amc);
   cross3(bc, nl, bmc);
   /* MJX takes the argmax of concat(dist_bp, dist_ap): the bc edge wins ties */
-  double bbp = -1, bap = -1;
   int ibp = ia, iap = ia;
-  for (int i = ia; i <= ilast; i++) {
-    if (!(SUP(i) > thr)) continue;
-    const double* v = m->hull_vert[i];
-    double e1 = fabs((b[0] - v[0]) * bc[0] + (b[1] - v[1]) * bc[1] + (b[2] - v[2]) * bc[2]);
-    double e2 = fabs((a[0] - v[0]) * ac[0] + (a[1] - v[1]) * ac[1] + (a[2] - v[2]) * ac[2]);
-    if (beats(e1, bbp)) { bbp = e1; ibp = i; }
-    if (beats(e2, bap)) { bap = e2; iap = i; }
-  }
+  PICK(fabs((b[0] - v[0]) * bc[0] + (b[1] - v[1]) * bc[1] + (b[2] - v[2]) * bc[2]), ibp);
+  const double bbp = best_;
+  PICK(fabs((a[0] - v[0]) * ac[0] + (a[1] - v[1]) * ac[1] + (a[2] - v[2]) * ac[2]), iap);
+  const double bap = best_;
+#undef PICK
   id = beats(bap, bbp) ? iap : ibp;
   const int idx[4] = {ia, ib, ic, id};
   for (int s = 0; s < 4; s++) {

@@ -42,6 +42,9 @@ def main():
     q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
     xi = proj(torch.tensor(np.random.default_rng(20250632).normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32)),
               proj.boundary(q0, np.zeros(6), np.zeros(6), n), 10).numpy()
+    if os.environ.get("SUBSET"):  # profile chosen candidates of the batch only (comma-separated indices)
+        xi = np.ascontiguousarray(xi[[int(i) for i in os.environ["SUBSET"].split(",")]])
+        n = xi.shape[0]
     e = Engine(m, H, n, Pd)
     ph = (ctypes.c_ulonglong * 24)()
     f = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731

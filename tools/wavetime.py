@@ -53,11 +53,18 @@ def main():
     e = Engine(m, H, n, Pd)
     f = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
     w, pt, qt = np.array([20, 3, 80.]), np.array([-0.3, -0.3, 0.5]), np.array([0, 1, 0, 0.])
-    buf = np.zeros((n, 4), np.uint64)
+    buf = np.zeros((n, 6), np.uint64)  # (n, 4) times / slots, then (n, 2) work counters
     for _ in range(3):  # warm; the last launch is analysed
         _lib.check(lib.mpcr_rollout_wavetime(e.handle, xi.ctypes.data, MPCR_LAYOUT_XI, n,
                                              q0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), f(w), f(pt), f(qt),
                                              buf.ctypes.data))
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")  # per-candidate rows: max (bits 2-7), sum (8-)
+    e.rollout_cost(torch.tensor(xi, device="cuda"), MPCR_LAYOUT_XI, q0, w, pt, qt, status=st)
+    sv = st.cpu().numpy()
+    rows_mean, rows_max = (sv >> 8) / H, (sv >> 2) & 63
+    work = buf.reshape(-1)[4 * n:].reshape(n, 2)
+    buf = buf.reshape(-1)[:4 * n].reshape(n, 4)
+    newton, lsp, cvx = (work[:, 0] & 0xffffffff).astype(float), (work[:, 0] >> 32).astype(float), work[:, 1].astype(float)
     t0, t1, cyc = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64), buf[:, 2].astype(np.float64)
     base = t0.min()
     s, e_ = (t0 - base) * 0.01, (t1 - base) * 0.01  # us (100 MHz)
@@ -85,11 +92,24 @@ def main():
                         "max": float(per_simd_end.max())},
         "simd_cycles_cv": float(per_simd_cyc.std() / per_simd_cyc.mean()),
         "xccs": sorted({k[0] for k in keys}), "cus": len({k[:4] for k in keys}),
+        "work_per_step": {"newton": float(newton.mean() / H), "ls_passes": float(lsp.mean() / H),
+                          "convex_chunks": float(cvx.mean() / H)},
+        "corr_cycles": {"newton": float(np.corrcoef(cyc, newton)[0, 1]) if newton.std() > 0 else None,
+                        "ls_passes": float(np.corrcoef(cyc, lsp)[0, 1]) if lsp.std() > 0 else None,
+                        "convex_chunks": float(np.corrcoef(cyc, cvx)[0, 1]) if cvx.std() > 0 else None},
+        "slowest": [{"cand": int(i), "Mcycles": round(cyc[i] / 1e6, 1), "newton": int(newton[i]), "ls": int(lsp[i]),
+                     "cvx": int(cvx[i])} for i in np.argsort(-cyc)[:6]],
+        "corr_cycles_rows": {"mean": float(np.corrcoef(cyc, rows_mean)[0, 1]), "max": float(np.corrcoef(cyc, rows_max)[0, 1])},
+        "rows_slowest_vs_all": {"slowest_mean_rows": float(rows_mean[np.argsort(-cyc)[:40]].mean()),
+                                "all_mean_rows": float(rows_mean.mean()),
+                                "slowest_max_rows": float(rows_max[np.argsort(-cyc)[:40]].mean()),
+                                "all_max_rows": float(rows_max.mean())},
+        "median_work": {"newton": float(np.median(newton)), "ls": float(np.median(lsp)), "cvx": float(np.median(cvx))},
     }
     print(json.dumps(res, indent=1))
     if out:
         json.dump(res, open(out, "w"), indent=1)
-        np.save(out.replace(".json", ".npy"), buf)
+        np.save(out.replace(".json", ".npy"), np.concatenate([buf, work], axis=1))
 
 
 if __name__ == "__main__":
