@@ -32,6 +32,8 @@ def main():
         build.compile_lib(SO, ["-DMPCR_WAVETIME"])
         print(SO)
         return
+    import torch
+    torch.cuda.init()  # torch's HIP runtime first: loading libmpcr first would bind both to ROCm's
     _lib.LIB_PATH = SO
     lib = _lib.load()
     vp, P_ = ctypes.c_void_p, ctypes.POINTER
