@@ -44,6 +44,13 @@ if [[ $STEPS == *pmc* ]]; then
     run pmc$i 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
   done
 fi
+if [[ $STEPS == *c5* ]]; then
+  run c5_dual 300 python tools/bench_mpc.py --model dual_arm --ticks 30
+  run c5_planner 200 python tools/bench_mpc.py --model planner_scene --ticks 30
+fi
+if [[ $STEPS == *phase* ]]; then  # needs libmpcr_prof.so (python tools/phase_profile.py --build, CPU container)
+  run phase_c4 200 env N=4096 H=100 python tools/phase_profile.py dual_arm $OUT/phase_c4.json
+fi
 if [[ $STEPS == *wavetime* ]]; then
   N=4096 run wavetime 120 python tools/wavetime.py scene_mjx $OUT/wavetime_c3_4096.json
 fi
