@@ -61,6 +61,20 @@ namespace mpcr {
 #ifndef MPCR_PACE_LAG
 #define MPCR_PACE_LAG 0
 #endif
+// where the mates' progress read at the step start is consumed: 0 before the
+// collision phase (mid-step), 1 at the next step's start, 2 before Newton
+#ifndef MPCR_PACE_AT
+#define MPCR_PACE_AT 0
+#endif
+#define PACE_SETPRIO() \
+  if (pace) {  /* priority = SIMD mates ahead of this wave (0..3) */ \
+  const int ahead = __popcll(__ballot(lane < 16 && lane != pace_own && pace_v != ~0u && pace_v > (unsigned)t + MPCR_PACE_LAG)); \
+  if (ahead >= 3) __builtin_amdgcn_s_setprio(3); \
+  else if (ahead == 2) __builtin_amdgcn_s_setprio(2); \
+  else if (ahead == 1) __builtin_amdgcn_s_setprio(1); \
+  else __builtin_amdgcn_s_setprio(0); \
+  }
+
 // ablation builds (timing attribution only; results are wrong): skip the
 // capsule-box deepest-point search / the narrow-phase functions in the mask
 #ifndef MPCR_ABL_DEEP
@@ -2110,6 +2124,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     // stay in their phases and hit L1/L2.
     LAUNDER_MODEL();
     if constexpr (!WIDE && MPCR_LANE_LAUNDER) LAUNDER_LANE();
+#if MPCR_PACE && MPCR_PACE_AT == 1
+    PACE_SETPRIO();  // the previous step's read, against this step
+#endif
 #if MPCR_PACE
     if (pace) {  // post this step, read the SIMD mates' (consumed mid-step)
       if (lane == pace_own) __hip_atomic_store(pace + lane, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2677,14 +2694,8 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 
     STAMP(6);
     STOP_AT(6)
-#if MPCR_PACE
-    if (pace) {  // priority = SIMD mates ahead of this wave (0..3)
-      const int ahead = __popcll(__ballot(lane < 16 && lane != pace_own && pace_v != ~0u && pace_v > (unsigned)t + MPCR_PACE_LAG));
-      if (ahead >= 3) __builtin_amdgcn_s_setprio(3);
-      else if (ahead == 2) __builtin_amdgcn_s_setprio(2);
-      else if (ahead == 1) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
+#if MPCR_PACE && MPCR_PACE_AT == 0
+    PACE_SETPRIO();
 #endif
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
@@ -3067,6 +3078,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 
     STAMP(8);
     STOP_AT(8)
+#if MPCR_PACE && MPCR_PACE_AT == 2
+    PACE_SETPRIO();
+#endif
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- Newton solver (primal), MJX-style line search ------------------------
     {
