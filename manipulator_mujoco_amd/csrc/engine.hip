@@ -74,6 +74,7 @@ struct mpcr_engine {
   float* d_td = nullptr;         // (max_n + 1) x nctrl x H joint-velocity table (thetadot not requested)
   short* d_hints = nullptr;      // max_n x NHINT x 2 (dual-arm class): hull-climb starts
   unsigned* d_pace = nullptr;    // MPCR_PACE_SLOTS: the rollout kernel's per-wave-slot progress (pacing)
+  float* d_mslab = nullptr;      // (max_n + 1) x NVW x LD: the dual-arm class's mass matrices
   // convex hulls (dual-arm class)
   float4* d_hull_vert = nullptr;
   int2* d_hull_info = nullptr;
@@ -778,6 +779,8 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
           hipSuccess ||
       hipMalloc(&e->d_hints, sizeof(short) * 2 * (size_t)max_n * (e->wide ? SmemW::NHINT : 1)) != hipSuccess ||
       hipMalloc(&e->d_pace, sizeof(unsigned) * MPCR_PACE_SLOTS) != hipSuccess ||
+      hipMalloc(&e->d_mslab, sizeof(float) * ((size_t)max_n + 1) * (e->wide ? SmemW::NVW * SmemW::LD : 1)) !=
+          hipSuccess ||
       hipMalloc(&e->d_td, sizeof(float) * ((size_t)max_n + 1) * (size_t)(e->host.nctrl > 0 ? e->host.nctrl : 1) *
                               (size_t)horizon) != hipSuccess) {
     mpcr_engine_free(e);
@@ -811,6 +814,7 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_td);
   (void)hipFree(e->d_hints);
   (void)hipFree(e->d_pace);
+  (void)hipFree(e->d_mslab);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
   (void)hipFree(e->d_hull_adjv);
@@ -859,6 +863,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.tdscratch = e->d_td;
   a.hints = e->d_hints;
   a.pace = e->d_pace;
+  a.mslab = e->d_mslab;
   a.dpar = l.dpar;
   a.state = l.state;
   a.plant = l.plant;
@@ -1141,6 +1146,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   a.tdscratch = e->d_td;
   a.hints = e->d_hints;
   a.pace = e->d_pace;
+  a.mslab = e->d_mslab;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);
@@ -1174,6 +1180,7 @@ extern "C" int mpcr_rollout_wavetime(mpcr_engine* e, const float* input, int lay
   a.tdscratch = e->d_td;
   a.hints = e->d_hints;
   a.pace = e->d_pace;
+  a.mslab = e->d_mslab;
   a.layout = layout; a.n = n; a.H = e->H; a.nbasis = e->nbasis;
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);

@@ -56,6 +56,7 @@ struct RolloutArgs {
   // per hardware wave slot: the step a resident wave is on (~0u when none),
   // MPCR_PACE_SLOTS words; the kernel's pacing reads its SIMD's 16 slots
   unsigned* pace;
+  float* mslab;  // (n + 1) x NVW x LD: the mass matrix of the dual-arm class (SmemT::M_SLAB)
   float* dbg;  // parity debugging (mpcr_plant_step_debug): candidate 0's last step, DBG_* layout
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs
@@ -101,7 +102,10 @@ struct __align__(16) SmemT {
   alignas(16) float srch[NVW];  // Newton search direction
   float com[DX_NTREE][4];
   float cdof[NVW][WIDE ? 6 : 8];
-  alignas(16) float M[NVW][LD];
+  // the dual-arm class keeps M in a per-candidate HBM slab (RolloutArgs::mslab,
+  // L2-resident): 4.6 KB less LDS -> 8 blocks per CU instead of 7
+  static constexpr bool M_SLAB = NVW_ == 32;
+  alignas(16) float M[M_SLAB ? 1 : NVW][LD];
   alignas(16) float gxpos[NGW][4];   // gxpos+gxmat (dead during Newton) double as the
   float gxmat[NGW][12];  // Hessian solve's LDS scratch (NGW*16 >= NVW*LD)
   float cprev[CPREV_GLOBAL ? 1 : DX_NSLOT];  // previous-step masked slot distances (cost_c)
@@ -184,8 +188,10 @@ static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU
 #endif
 // Dual-arm image: J rows past 40 in the HBM slab, cost history and hull-climb
 // hints in HBM (the class has no robot-masked slots), the convex-pair list
-// inside the J rows, 6-float cdof rows: 21.6 KB -> 7 blocks per CU (was
-// 32.3 KB, 4); the kernel is compiled for 2 waves/SIMD (<= 256 VGPRs).
+// inside the J rows, 6-float cdof rows, the mass matrix in an HBM slab:
+// 17.2 KB -> 8 blocks per CU (21.7 KB / 7 before the M slab; 32.3 KB / 4
+// before the J slab); the kernel is compiled for 2 waves/SIMD (<= 256 VGPRs),
+// so 8 blocks per CU is also its register limit.
 #ifndef MPCR_W_JL
 #define MPCR_W_JL 40
 #endif
@@ -197,7 +203,7 @@ static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD + SmemN::NVW, "Hessian +
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 static_assert(SmemW::JL * SmemW::LDJ >= SmemW::CVXN, "convex-pair list inside the J rows");
 #if !defined(MPCR_N_LDS_UNCHECKED)
-static_assert(sizeof(SmemW) <= 152448 / 7, "dual-arm LDS image must fit 7 blocks per CU");
+static_assert(sizeof(SmemW) <= 152448 / 8, "dual-arm LDS image must fit 8 blocks per CU");
 #endif
 
 

@@ -2024,6 +2024,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   const int nv = m->nv, nb = m->nbody, nc = m->nctrl;
   float* const gx = S::JL < S::MAXEFC ? args.jx + (size_t)b * (S::MAXEFC - S::JL) * S::LDJ : nullptr;
   short* const hx = S::WIDE ? args.hints + (size_t)b * S::NHINT * 2 : nullptr;
+  // mass-matrix rows: LDS, or the candidate's HBM slab (dual-arm class)
+  float* const mrow0 = S::M_SLAB ? args.mslab + (size_t)b * NVW * S::LD : nullptr;
+#define MR(i) (S::M_SLAB ? mrow0 + (i) * S::LD : s.M[S::M_SLAB ? 0 : (i)])
 
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
   //      (plant mode: the caller's state, no init_pos override)
@@ -2601,13 +2604,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         if (i < nv && j < nv) {
           if ((m->dof_chainmask[i] >> j) & 1u) {
             const float x = i == j ? P[v] + m->dof_armature[i] : P[v];
-            s.M[i][j] = x;
-            s.M[j][i] = x;
+            MR(i)[j] = x;
+            MR(j)[i] = x;
           } else if (!((m->dof_chainmask[j] >> i) & 1u)) {
-            s.M[i][j] = 0.f;
+            MR(i)[j] = 0.f;
           }
         } else {
-          s.M[i][j] = i == j ? 1.f : 0.f;
+          MR(i)[j] = i == j ? 1.f : 0.f;
         }
       }
       const uint32_t sub = mr < nv ? m->dof_submask[mr] : 0u;
@@ -2633,7 +2636,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       } else if (i == j) {
         v = 1.f;
       }
-      s.M[i][j] = v;
+      MR(i)[j] = v;
     }
     }
     if (lane < nv) {
@@ -2674,11 +2677,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     if (S::CPW == 1 && blk_usable<NVW>(m)) {
       // M is block diagonal by kinematic tree: one chain for all trees
       if (lane >= nv && lane < NVW) s.qas[lane] = 0.f;
-      blk_solve<NVW>(m, [&](int i, int j) { return s.M[i][j]; }, s.qfs, s.qas, lane, &s.xpos[0][0]);
+      blk_solve<NVW>(m, [&](int i, int j) { return MR(i)[j]; }, s.qfs, s.qas, lane, &s.xpos[0][0]);
     } else {
       float Lm[NVW];
 #pragma unroll
-      for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? s.M[lane][j] : 0.f;
+      for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? MR(lane)[j] : 0.f;
       // the dynamics region (xpos..fvec) is dead once M is assembled
       float x;
       if constexpr (NVW == 16 && MPCR_DPP_CHOL) {
@@ -3090,7 +3093,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         // warm start: the better of qacc_warmstart and qacc_smooth
         if (!(m->disableflags & 4)) {
           // (the Gauss term of qacc_smooth itself is (M a_s - f_s)'(a_s - a_s) = 0)
-          const float maw = lane < nv ? dotN<NVW>(s.M[lane], s.qws) : 0.f;
+          const float maw = lane < nv ? dotN<NVW>(MR(lane), s.qws) : 0.f;
           const float gw = lane < nv ? (maw - s.qfs[lane]) * (s.qws[lane] - s.qas[lane]) : 0.f;
           float cw = 0.f, cs = 0.f;
           for (int r = lane; r < nefc; r += S::HL) {
@@ -3143,7 +3146,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           wt_newton++;
 #endif
           // Ma, jar, cost at the current qacc; per-row force and active D
-          const float ma = lane < nv ? dotN<NVW>(s.M[lane], s.qacc) : 0.f;
+          const float ma = lane < nv ? dotN<NVW>(MR(lane), s.qacc) : 0.f;
           float cc = 0.f;
           for (int r = lane; r < nefc; r += S::HL) {
             const float jar = jdot(s, gx, r, s.qacc) - s.efc_aref[r];
@@ -3188,7 +3191,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             // H[gi][4 gq ..], the same products in the same row order as the
             // VALU build (the MFMA is a k-ordered fmaf chain), so H is
             // bitwise the VALU one
-            const float4 m4 = reinterpret_cast<const float4*>(s.M[gi])[gq];
+            const float4 m4 = reinterpret_cast<const float4*>(MR(gi))[gq];
             mfx4 hacc = {m4.x, m4.y, m4.z, m4.w};
             mfx4 gacc = {0.f, 0.f, 0.f, 0.f};
             for (int r0 = 0; r0 < nefc; r0 += 4) {
@@ -3247,7 +3250,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             constexpr int QPL = NVW / 4 / RPW;
             float4 hq[QPL];
 #pragma unroll
-            for (int k = 0; k < QPL; k++) hq[k] = reinterpret_cast<const float4*>(s.M[gi])[gq + RPW * k];
+            for (int k = 0; k < QPL; k++) hq[k] = reinterpret_cast<const float4*>(MR(gi))[gq + RPW * k];
             if constexpr (MFMA_HESS_W) {
               // J^T D J on v_mfma_f32_32x32x2_f32: accumulator register 4k + e of
               // lane (gi, gq) is H[gi][4 (gq + 2k) + e] in the transposed view --
@@ -3342,7 +3345,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
           if (lane < NVW) s.srch[lane] = search;
           sync();
           // Mv, jv, quadratic coefficients
-          const float mvv = lane < nv ? dotN<NVW>(s.M[lane], s.srch) : 0.f;
+          const float mvv = lane < nv ? dotN<NVW>(MR(lane), s.srch) : 0.f;
           for (int r = lane; r < nefc; r += S::HL) s.efc_jv[r] = jdot(s, gx, r, s.srch);
           const float sn = sqrtf(hsum<S::CPW>(search * search));
           const float gtol = m->tolerance * m->ls_tolerance * sn * m->meaninertia * (float)(nv > 1 ? nv : 1);
@@ -3466,13 +3469,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
         if (S::CPW == 1 && !m->impl_cross && blk_usable<NVW>(m)) {  // M + dt D block diagonal by tree
           if (lane < NVW) s.srch[lane] = lane < nv ? s.qfs[lane] + qc : 0.f;
           sync();
-          blk_solve<NVW>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], s.M[i][j]); }, s.srch, s.srch,
+          blk_solve<NVW>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], MR(i)[j]); }, s.srch, s.srch,
                          lane, &s.gxpos[0][0]);
           sync();
         } else {
           float Lm[NVW];
 #pragma unroll
-          for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? fmaf(dt, m->impl_D[lane][j], s.M[lane][j]) : 0.f;
+          for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? fmaf(dt, m->impl_D[lane][j], MR(lane)[j]) : 0.f;
           chol_rows(Lm, lane);
           const float a = chol_solve<NVW, S::LD>(Lm, lane < nv ? s.qfs[lane] + qc : 0.f, lane, &s.gxpos[0][0]);
           if (lane < NVW) s.srch[lane] = lane < nv ? a : 0.f;
@@ -3563,6 +3566,8 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   }
 #endif
 }
+
+#undef MR
 
 // ---------------------------------------------------------------------------
 // launchers (the host side lives in another translation unit)
