@@ -57,6 +57,12 @@ namespace mpcr {
 #ifndef MPCR_PACE
 #define MPCR_PACE 1
 #endif
+// pacing in the dual-arm kernel too: 1.7 % slower at 7 blocks per CU (2.3
+// backfilled rounds), ~0.8 % faster at 8 (C4 4096 x 100: 33.6-34.0 vs
+// 34.1 ms; 8192 x 50: 30.35-30.45 vs 30.57-30.79 ms)
+#ifndef MPCR_W_PACE
+#define MPCR_W_PACE 1
+#endif
 // a mate counts as ahead when it is more than MPCR_PACE_LAG steps ahead
 #ifndef MPCR_PACE_LAG
 #define MPCR_PACE_LAG 0
@@ -2102,9 +2108,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   unsigned* pace = nullptr;
   int pace_own = 0;
   unsigned pace_v = ~0u;
-  // narrow kernel only: the dual-arm one runs ~2.3 rounds at 4096 (7 blocks
-  // per CU), the dispatcher backfills, and pacing measured 1.7 % slower there
-  if (!WIDE && S::CPW == 1 && args.pace) {
+  if ((!WIDE || MPCR_W_PACE) && S::CPW == 1 && args.pace) {
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID[3:0]
     const unsigned grp = ((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) *
