@@ -116,12 +116,27 @@ def pmc_valu(path, n, H, flops_step):
     return rec
 
 
-def _host_cpu():
-    """(usable host cores, machine cpu count, model name)."""
+def _cgroup_cpus():
+    """The cgroup v2 CPU quota in CPUs (cpu.max "quota period"), or None."""
     try:
-        usable = len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
+def _host_cpu():
+    """(usable host cores, machine cpu count, model name, affinity cores, cgroup
+    quota).  Usable = the CPUs this process may run on AND the cgroup lets it
+    use: the GPU box's affinity mask shows the whole machine (256) while its
+    cgroup quota is the box's share."""
+    try:
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        usable = os.cpu_count() or 1
+        aff = os.cpu_count() or 1
+    quota = _cgroup_cpus()
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -131,19 +146,21 @@ def _host_cpu():
                     break
     except OSError:
         pass
-    return usable, os.cpu_count() or 1, model
+    return usable, os.cpu_count() or 1, model, aff, quota
 
 
-def cpu_baseline(m, xi, H, Pd, threads, reps=5):
-    """The fp64 scalar C oracle (oracle/mpcr_oracle.c, a restatement of the
-    reference's rollout + cost, SBP/mjx_planner.py:123-124) on host threads:
-    pool started and model converted before the clock; median of `reps`
-    timed repetitions of the rollout compute only.  Returns rollouts/s."""
+def cpu_baseline(m, xi, H, Pd, threads, reps=5, precision="fp32"):
+    """The scalar C oracle (oracle/mpcr_oracle.c, a restatement of the
+    reference's rollout + cost, SBP/mjx_planner.py:123-124; precision "fp32"
+    = oracle_f32.c, every double as float, the reference's own precision) on
+    host threads: pool started and model converted before the clock; median
+    of `reps` timed repetitions of the rollout compute only.  Returns
+    rollouts/s."""
     import oracle
     oracle.build()
     n = xi.shape[0]
     td = np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
-    run = oracle.Runner(m, threads, Q0, W, PT, QT)
+    run = oracle.Runner(m, threads, Q0, W, PT, QT, precision=precision)
     run.rollout(td[: max(1, min(n, threads))])  # warm-up (page in, first-touch)
     ts = []
     for _ in range(reps):
@@ -165,15 +182,22 @@ def main():
                     help="weak: --n candidates per GPU; strong: --n candidates in total, split over the GPUs")
     ap.add_argument("--exchange", choices=("key", "elite"), default=None,
                     help="per-step selection: best-key MIN all-reduce, or also the CEM elite exchange")
-    ap.add_argument("--n", type=int, default=None, help="candidates (per GPU for weak, total for strong)")
+    # --candidates: torch.distributed.run's argparse takes a bare "--n" after the
+    # script name for an abbreviation of its own options
+    ap.add_argument("--candidates", "--n", dest="n", type=int, default=None,
+                    help="candidates (per GPU for weak, total for strong)")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--model", default=None)
     ap.add_argument("--cpu-sample", type=int, default=2048)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the usable host cores, at most 16")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every usable host core (affinity mask capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-contact-report", action="store_true")
     ap.add_argument("--pmc", default=None, help="rocprofv3 FETCH/WRITE CSV of this workload")
     ap.add_argument("--pmc-sq", default=None, help="rocprofv3 SQ counter CSV of this workload")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N > 1: nccl (= RCCL over xGMI, one GPU per rank) or gloo (host-staged; ranks may share "
+                         "a GPU, device = local rank mod the visible GPUs: rehearses the multi-rank path on one GPU)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.model = args.model or cfg["model"]
@@ -214,27 +238,41 @@ def main():
     cpu_rec = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # host-core baseline before the process initialises the GPU
-        usable, ncpu, model = _host_cpu()
-        threads = args.cpu_threads or min(16, usable)
+        usable, ncpu, model, aff, quota = _host_cpu()
+        threads = args.cpu_threads or usable
         sample = xi_host[: args.cpu_sample].numpy()
-        vp, reps = cpu_baseline(m, sample, H, Pd, threads)
-        v1, _ = cpu_baseline(m, sample[: max(32, args.cpu_sample // 16)], H, Pd, 1)
-        cpu_rec = {"value": round(vp, 1), "unit": "rollouts/s", "cores": threads, "kind": "port",
-                   "sample": f"{sample.shape[0]} of the same {args.config.upper()} candidates x {H} steps; fp64 "
-                             f"scalar C restatement of the reference rollout + cost (oracle/mpcr_oracle.c, not "
-                             f"CPU-MJX), {threads} threads, median of {len(reps)} timed repetitions (pool and model "
-                             f"set up before the clock); 1 thread: {v1:.1f} rollouts/s",
-                   "precision": "fp64", "one_core": round(v1, 1), "reps": reps,
-                   "host": {"usable_cores": usable, "nproc": ncpu, "cpu_model": model}}
+        one = sample[: max(32, args.cpu_sample // 16)]
+        v32, reps = cpu_baseline(m, sample, H, Pd, threads, precision="fp32")
+        v32_1, _ = cpu_baseline(m, one, H, Pd, 1, precision="fp32")
+        v64, reps64 = cpu_baseline(m, sample, H, Pd, threads, precision="fp64")
+        v64_1, _ = cpu_baseline(m, one, H, Pd, 1, precision="fp64")
+        cpu_rec = {"value": round(v32, 1), "unit": "rollouts/s", "cores": threads, "kind": "port",
+                   "sample": f"{sample.shape[0]} of the same {args.config.upper()} candidates x {H} steps; fp32 "
+                             f"scalar C restatement of the reference rollout + cost (oracle/oracle_f32.c = "
+                             f"oracle/mpcr_oracle.c in float, not CPU-MJX), {threads} threads = every usable core "
+                             f"(affinity {aff}, cgroup quota {quota}), median of {len(reps)} timed repetitions "
+                             f"(pool and model set up before the clock); 1 thread: {v32_1:.1f} rollouts/s; fp64 "
+                             f"build: {v64:.1f} ({threads} threads), {v64_1:.1f} (1 thread)",
+                   "precision": "fp32", "one_core": round(v32_1, 1), "reps": reps,
+                   "fp64": {"value": round(v64, 1), "one_core": round(v64_1, 1), "reps": reps64},
+                   "host": {"usable_cores": usable, "affinity_cores": aff, "cgroup_cpu_quota": quota, "nproc": ncpu,
+                            "cpu_model": model}}
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"local rank {local} has no GPU of its own ({ndev} visible); use --backend gloo to share")
+    gpu = local % max(ndev, 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     backend = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         backend = dist.get_backend()
     xi = xi_host.to(dev)
-    eng = Engine(m, H, n, Pd, device=local)
+    eng = Engine(m, H, n, Pd, device=gpu)
     cost4 = torch.empty((n, 4), dtype=torch.float32, device=dev)
     theta = torch.empty((n, 6 * H), dtype=torch.float32, device=dev)
     thetadot = torch.empty((n, 6 * H), dtype=torch.float32, device=dev)
@@ -242,6 +280,8 @@ def main():
     status = torch.zeros(n, dtype=torch.int32, device=dev)
     n_elite = int(0.05 * n_total)
     topk_fn = (lambda c, k: topk(eng, c, k))
+
+    elites = {}
 
     def step(ev=None):
         if ev is not None:
@@ -253,14 +293,17 @@ def main():
         if args.exchange == "elite":
             c = cost4[:, 0].contiguous()
             if world > 1:
-                md.gather_elites(c, xi, n_elite, topk_fn)
+                g_cost, _, sel = md.gather_elites(c, xi, n_elite, topk_fn)
+                elites["cost"] = g_cost.index_select(0, sel.long())
             else:
-                topk_fn(c, n_elite)
+                elites["cost"] = c.index_select(0, topk_fn(c, n_elite).long())
+            elites["count"] = elites.get("count", 0) + 1
         if world > 1:
             md.allreduce_min_key(key)
 
     for _ in range(args.warmup):
         step()
+    elites["count"] = 0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -317,6 +360,7 @@ def main():
                        "candidates_per_gpu": n, "horizon": H, "global_batch": n_total,
                        "parallelism": f"dp{world} (candidate shards; {args.exchange} exchange)",
                        "world_size_seen": world, "backend": backend or "single process",
+                       "gpus_visible": ndev,
                        "exchange": "8-byte RCCL MIN all-reduce of the best key" + (
                            "; local top-E + RCCL all-gather of (xi, cost) rows + global top-E"
                            if args.exchange == "elite" else "")},
@@ -331,6 +375,14 @@ def main():
             "best": {"index": idx, "cost": best}, "truncated_candidates": trunc,
             "mean_constraint_rows": round(nefc_mean, 2),
         }
+        if traffic is not None:
+            rec["roofline"]["traffic_over_algorithmic"] = round(traffic / hbm_launch, 3)
+        if "cost" in elites:
+            ec = elites["cost"].double().cpu().numpy()
+            # the global top-E of the last timed step: equal to one GPU's on the
+            # same global batch (tests/test_gpu_bench.py)
+            rec["elites"] = {"k": n_elite, "exchanges_timed": elites["count"], "cost_sum": float(ec.sum()),
+                             "first": [float(x) for x in ec[:4]]}
         if valu is not None:
             rec["roofline"]["valu"] = valu
         if contact is not None:

@@ -213,7 +213,10 @@ int mpcr_cem_update(mpcr_cem* c, const float* xi, int n, const float* cost, int 
    Replaces the torch.distributed path of manipulator_mujoco_amd/dist.py for
    hosts without Python; the reference itself is single-device
    (SBP/mjx_planner.py:395 argmin, :305-310 elites).  RCCL is dlopen'ed at the
-   first call (librccl.so.1). */
+   first call (librccl.so.1).  A communicator is single-stream, like an RCCL
+   communicator: mpcr_comm_gather_elites stages the local elites in scratch
+   owned by the comm, so calls on one comm must be ordered on one stream (or
+   use one comm per stream). */
 #define MPCR_COMM_ID_BYTES 128
 typedef struct mpcr_comm mpcr_comm;
 /* rank 0 creates the id and hands it to the other ranks out of band */

@@ -87,7 +87,14 @@ def compile_mjcf_lib(out: str = MJCF_OUT) -> str:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if force or not os.path.exists(MJCF_OUT) or os.path.getmtime(MJCF_OUT) < os.path.getmtime(MJCF_SRC):
-        compile_mjcf_lib()
+        # optional: libmpcr.so dlopens it only for .xml model paths and reports
+        # "MJCF compiler unavailable" at run time when it is missing (a host
+        # without Python headers or a shared libpython still builds the engine)
+        try:
+            compile_mjcf_lib()
+        except (subprocess.CalledProcessError, OSError) as e:
+            print(f"warning: libmpcr_mjcf.so not built ({e}); mpcr_model_load of .xml paths will be unavailable",
+                  file=sys.stderr)
     if not force and os.path.exists(OUT):
         mt = os.path.getmtime(OUT)
         if all(os.path.getmtime(d) <= mt for d in DEPS):

@@ -637,9 +637,16 @@ __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
 // only moves to a neighbour beating the current vertex by more than kSupBand
 // metres along the unit direction (coplanar vertices are ties, the first in
 // list order wins).
-constexpr float kSupTie = 1e-6f;
-constexpr float kSupBand = 1e-5f;
+#ifndef MPCR_SUP_BAND
+#define MPCR_SUP_BAND 1e-5f  // the oracle's SUP_BAND (experiments: tools/build_variant.py -DMPCR_SUP_BAND=...)
+#endif
+#ifndef MPCR_SUP_TIE
+#define MPCR_SUP_TIE 1e-6f  // < 0: MuJoCo's mju_sign (only an exact zero is a tie)
+#endif
+constexpr float kSupTie = MPCR_SUP_TIE;
+constexpr float kSupBand = MPCR_SUP_BAND;
 __device__ __forceinline__ float tie_sign(float lk, float ln) {
+  if (kSupTie < 0.f) return lk > 0.f ? 1.f : (lk < 0.f ? -1.f : 0.f);
   return fabsf(lk) < kSupTie * ln ? 0.f : (lk >= 0.f ? 1.f : -1.f);
 }
 
@@ -712,7 +719,7 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
     if (type == 3) p[2] += tie_sign(l[2], ln) * sz[1];
   } else if (type == 5) {  // cylinder
     const float r = sqrtf(l[0] * l[0] + l[1] * l[1]);
-    if (r > kSupTie * ln) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
+    if (r > fmaxf(kSupTie, 0.f) * ln) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
     p[2] = tie_sign(l[2], ln) * sz[1];
   } else if (type == 6) {  // box
     p[0] = tie_sign(l[0], ln) * sz[0];

@@ -24,9 +24,13 @@ _LIB = None
 
 
 def build(force: bool = False) -> str:
+    """liboracle.so (fp64, the checker) and liboracle_f32.so (the same source
+    in float: bench.py's cpu_baseline and the parity bar's fp32 probe)."""
     path = os.path.join(_HERE, "liboracle.so")
-    src = os.path.join(_HERE, "mpcr_oracle.c")
-    if force or not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("mpcr_oracle.c", "oracle_f32.c")]
+    outs = [path, os.path.join(_HERE, "liboracle_f32.so")]
+    newest = max(os.path.getmtime(f) for f in srcs)
+    if force or any(not os.path.exists(o) or os.path.getmtime(o) < newest for o in outs):
         subprocess.check_call(["make", "-s", "-C", _HERE], stdout=subprocess.DEVNULL)
     return path
 
@@ -48,7 +52,89 @@ def lib():
         _LIB.oracle_model_size.restype = ctypes.c_int
         _LIB.oracle_cone_eval.argtypes = [ctypes.c_double] + [dp] * 4 + [ctypes.c_double] + [dp] * 4
         _LIB.oracle_cone_eval.restype = ctypes.c_int
+        _LIB.oracle_set_floor.argtypes = [ctypes.c_int, ctypes.c_double]
     return _LIB
+
+
+FLOOR_DEFAULTS = (1e-6, 1e-5, 1e-6, 1e-5)  # Newton, support band, support tie, MPR tol (mpcr_oracle.c g_floor)
+
+
+def _both():
+    return (lib(), lib_f32())
+
+
+class exact:
+    """Context manager: run the oracle (fp64 and fp32 builds) with the rules
+    of the EXACT_* mask MuJoCo-exact (no kernel-matching floors, bands or
+    tolerances; oracle_set_exact in mpcr_oracle.c) and, optionally, the
+    other rules at the given values (``floors``: Newton floor, support band,
+    support tie (< 0: mju_sign), MPR tolerance).  Global to the libraries:
+    not for concurrent callers."""
+
+    def __init__(self, mask=31, floors=None):
+        self.mask = int(mask)  # EXACT_* bits of mpcr_oracle.c; 31 = every rule
+        self.floors = floors
+
+    def __enter__(self):
+        self.prev = lib().oracle_get_exact()
+        for L in _both():
+            L.oracle_set_exact(self.mask)
+            if self.floors is not None:
+                for k, v in enumerate(self.floors):
+                    L.oracle_set_floor(k, float(v))
+        return self
+
+    def __exit__(self, *exc):
+        for L in _both():
+            L.oracle_set_exact(self.prev)
+            if self.floors is not None:
+                for k, v in enumerate(FLOOR_DEFAULTS):
+                    L.oracle_set_floor(k, float(v))
+        return False
+
+
+_LIB32 = None
+
+
+def lib_f32():
+    """The fp32 build (oracle_f32.c: every double of the oracle as float) --
+    bench.py's cpu_baseline only; the parity checker is the fp64 build."""
+    global _LIB32
+    if _LIB32 is None:
+        build()
+        _LIB32 = ctypes.CDLL(os.path.join(_HERE, "liboracle_f32.so"))
+        fp = ctypes.POINTER(ctypes.c_float)
+        _LIB32.oracle_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, fp, fp, fp, fp, fp, fp,
+                                          fp, fp, fp, ctypes.POINTER(ctypes.c_int), ctypes.c_float,
+                                          ctypes.c_uint, ctypes.c_int]
+        _LIB32.oracle_rollout.restype = ctypes.c_int
+        _LIB32.oracle_set_floor.argtypes = [ctypes.c_int, ctypes.c_float]  # double is float in that build
+    return _LIB32
+
+
+def _f32_type(t):
+    if t is ctypes.c_double:
+        return ctypes.c_float
+    if isinstance(t, type) and issubclass(t, ctypes.Array):
+        return _f32_type(t._type_) * t._length_
+    return t
+
+
+def struct_f32(model):
+    """The compiled model as the fp32 build's struct: the same header with
+    float fields (oracle_f32.c), values rounded from the fp64 struct."""
+    s = model.to_struct()
+    F = type("mpcr_model_f32_t", (ctypes.Structure,),
+             {"_fields_": [(n, _f32_type(t)) for n, t in type(s)._fields_]})
+    f = F()
+    for n, t in type(s)._fields_:
+        v = getattr(s, n)
+        if isinstance(v, ctypes.Array):
+            np.ctypeslib.as_array(getattr(f, n))[...] = np.ctypeslib.as_array(v)
+        else:
+            setattr(f, n, v)
+    f.nbytes = ctypes.sizeof(F)
+    return f
 
 
 def _p(a):
@@ -73,7 +159,7 @@ def rollout(model, thetadot, q0, w, ptgt, qtgt, want_theta=True, want_slots=Fals
     theta = np.zeros((n, nc * H)) if want_theta else None
     slots = np.zeros((n, H, max(model.nslot, 1))) if want_slots else None
     eef = np.zeros((n, H, 7)) if want_eef else None
-    info = np.zeros((n, 2), dtype=np.int32)
+    info = np.zeros((n, 3), dtype=np.int32)
     q0 = np.ascontiguousarray(q0, dtype=np.float64)
     w = np.ascontiguousarray(w, dtype=np.float64)
     pt = np.ascontiguousarray(ptgt, dtype=np.float64)
@@ -99,7 +185,8 @@ def rollout(model, thetadot, q0, w, ptgt, qtgt, want_theta=True, want_slots=Fals
     if st < 0:
         raise RuntimeError(f"oracle_rollout failed ({st})")
     # maxrows / maxcon: the busiest step's constraint rows / active contacts
-    out = dict(cost4=cost4, theta=theta, status=st, maxrows=info[:, 0], maxcon=info[:, 1])
+    # nneg: the integer #{c < 0} count inside cost_c (SBP/mjx_planner.py:296)
+    out = dict(cost4=cost4, theta=theta, status=st, maxrows=info[:, 0], maxcon=info[:, 1], nneg=info[:, 2])
     if want_slots:
         out["slots"] = slots[:, :, :model.nslot]
     if want_eef:
@@ -113,26 +200,30 @@ class Runner:
     model converted before the clock, each call is only the C rollouts
     (ctypes drops the GIL, so the threads run the C code concurrently)."""
 
-    def __init__(self, model, workers, q0, w, ptgt, qtgt):
+    def __init__(self, model, workers, q0, w, ptgt, qtgt, precision="fp64"):
         from concurrent.futures import ThreadPoolExecutor
         self.model, self.workers = model, max(1, int(workers))
-        self.s = model.to_struct()
-        self.L = lib()
-        self.args = [np.ascontiguousarray(x, dtype=np.float64) for x in (q0, w, ptgt, qtgt)]
+        self.dt = np.float32 if precision == "fp32" else np.float64
+        self.s = struct_f32(model) if precision == "fp32" else model.to_struct()
+        self.L = lib_f32() if precision == "fp32" else lib()
+        ct = ctypes.c_float if precision == "fp32" else ctypes.c_double
+        self.p = lambda a: None if a is None else a.ctypes.data_as(ctypes.POINTER(ct))  # noqa: E731
+        self.args = [np.ascontiguousarray(x, dtype=self.dt) for x in (q0, w, ptgt, qtgt)]
         self.ex = ThreadPoolExecutor(self.workers)
         list(self.ex.map(lambda i: i, range(self.workers)))  # start every thread now
 
     def rollout(self, td):
-        td = np.ascontiguousarray(td, dtype=np.float64)
+        td = np.ascontiguousarray(td, dtype=self.dt)
         n, H = td.shape[0], td.shape[1] // self.model.nctrl
-        cost4 = np.zeros((n, 4))
+        cost4 = np.zeros((n, 4), dtype=self.dt)
         cuts = np.linspace(0, n, min(self.workers, n) + 1).astype(int)
         q0, w, pt, qt = self.args
+        p = self.p
 
         def run(i):
             a, b = cuts[i], cuts[i + 1]
-            return self.L.oracle_rollout(ctypes.byref(self.s), int(b - a), H, _p(td[a:b]), _p(q0), _p(w), _p(pt),
-                                         _p(qt), _p(cost4[a:b]), None, None, None, None, 0.0, 0, 0)
+            return self.L.oracle_rollout(ctypes.byref(self.s), int(b - a), H, p(td[a:b]), p(q0), p(w), p(pt),
+                                         p(qt), p(cost4[a:b]), None, None, None, None, 0.0, 0, 0)
 
         st = list(self.ex.map(run, range(len(cuts) - 1)))
         if min(st) < 0:

@@ -919,9 +919,44 @@ static void col_box_box(const odata* d, int ga, int gb, const double* ha, const 
    segment) centre, 0, instead of the sign of rounding noise; the hull climb
    only moves to a neighbour that beats the current vertex by more than
    SUP_BAND metres (coplanar vertices are ties) */
-#define SUP_TIE 1e-6
-#define SUP_BAND 1e-5
-static double tie_sign(double lk, double ln) { return fabs(lk) < SUP_TIE * ln ? 0.0 : (lk >= 0 ? 1.0 : -1.0); }
+#define SUP_TIE_K 1e-6
+#define SUP_BAND_K 1e-5
+/* MuJoCo-exact mode (oracle_set_exact(1)): every kernel-matching
+   floor, band and tolerance of this file is switched off -- strict support
+   maxima, exact argmax picks, ccd_tolerance 1e-6, MuJoCo's own Newton stop
+   test and line search without the 1e-6 bracket floor -- so the effect of
+   those rules on parity can be measured instead of assumed
+   (tests/test_gpu_parity.py::test_parity_vs_mujoco_exact_oracle).  A global
+   switch: set it before a run, not while one is in flight. */
+static int g_exact = 0; /* bit mask of the rules run MuJoCo-exact (EXACT_* below); 0 = the kernel's */
+#define EXACT_NEWTON 1  /* Newton stop without the 1e-6 relative improvement floor */
+#define EXACT_LS 2      /* line search without the 1e-6 relative bracket floor */
+#define EXACT_MPR 4     /* MPR gap tolerance = ccd_tolerance 1e-6 */
+#define EXACT_SUP 8     /* strict support maxima (no tie band / axis tie) */
+#define EXACT_PICK 16   /* manifold / box picks by exact argmax */
+void oracle_set_exact(int mask) { g_exact = mask; }
+int oracle_get_exact(void) { return g_exact; }
+/* the kernel's values of the rules (oracle_set_floor: experiments that size
+   them against the exact mode) */
+static double g_floor[4] = {1e-6 /* Newton */, SUP_BAND_K, SUP_TIE_K, 1e-5 /* MPR */};
+void oracle_set_floor(int which, double v) { if (which >= 0 && which < 4) g_floor[which] = v; }
+#define SUP_TIE ((g_exact & EXACT_SUP) ? 0.0 : g_floor[2])
+#define SUP_BAND ((g_exact & EXACT_SUP) ? 0.0 : g_floor[1])
+static __thread long g_tie_stats[8]; /* diagnostic: |l_k| / |l| of the support axis ties (oracle_tie_stats) */
+void oracle_tie_stats(long* out, int reset) {
+  if (out) memcpy(out, g_tie_stats, sizeof(g_tie_stats));
+  if (reset) memset(g_tie_stats, 0, sizeof(g_tie_stats));
+}
+static double tie_sign(double lk, double ln) {
+  if (fabs(lk) < 1e-6 * ln) {
+    const double r = fabs(lk) / (ln > 0 ? ln : 1);
+    g_tie_stats[r == 0 ? 0 : r < 1e-15 ? 1 : r < 1e-12 ? 2 : r < 1e-9 ? 3 : 4]++;
+  }
+  /* exact: MuJoCo's mju_sign (0 for an exactly zero component, as
+     mjccd_support's box / capsule / cylinder cases) */
+  if ((g_exact & EXACT_SUP) || g_floor[2] < 0) return lk > 0 ? 1.0 : (lk < 0 ? -1.0 : 0.0);
+  return fabs(lk) < g_floor[2] * ln ? 0.0 : (lk >= 0 ? 1.0 : -1.0);
+}
 
 /* world support point of geom g along dir (any length); *hint: hull vertex the
    previous query on this geom ended at (-1: none), where the climb starts */
@@ -971,7 +1006,7 @@ static void support_rel(const mpcr_model_t* m, const odata* d, int g, const doub
     }
     case MPCR_GEOM_CYLINDER: {
       double r = sqrt(l[0] * l[0] + l[1] * l[1]);
-      if (r > SUP_TIE * ln) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
+      if (r > fmax(SUP_TIE, 0.0) * ln) { p[0] = sz[0] * l[0] / r; p[1] = sz[0] * l[1] / r; }
       p[2] = tie_sign(l[2], ln) * sz[1];
       break;
     }
@@ -1023,7 +1058,7 @@ typedef struct { double v[3], a[3], b[3]; } mpt; /* v = a - b */
    at 1e-6 that decided a visible share of the dual arm's rollouts
    differently in the kernel and here, at 1e-5 it rarely does; the depth it
    leaves is within 1e-5 m of converged (both sides use the same value) */
-#define MPR_TOL 1e-5
+#define MPR_TOL ((g_exact & EXACT_MPR) ? 1e-6 : g_floor[3]) /* MuJoCo's ccd_tolerance in the exact mode */
 #define MPR_ITER 50
 /* zero tests in metres (the kernel's kMprEps): lengths below 1.2e-7 m, two
    vectors parallel when one passes within it of the other's line, a point on
@@ -1243,8 +1278,8 @@ static void col_convex(const mpcr_model_t* m, odata* d, int pair, int g1, int g2
    near-ties (symmetric hulls, fp32 vs fp64 rounding) resolve to the lowest
    vertex index in the oracle and the kernel alike (the kernel evaluates it as
    a wave max and a ballot over 64 vertices at a time) */
-static int beats(double v, double best) { return v > best + 1e-4 * fabs(best) + 1e-12; }
-static int near_max(double v, double mx) { return v >= mx - (1e-4 * fabs(mx) + 1e-12); }
+static int beats(double v, double best) { return v > best + ((g_exact & EXACT_PICK) ? 0.0 : 1e-4 * fabs(best) + 1e-12); }
+static int near_max(double v, double mx) { return v >= mx - ((g_exact & EXACT_PICK) ? 0.0 : 1e-4 * fabs(mx) + 1e-12); }
 
 /* plane - mesh: MJX's plane_convex manifold (mujoco-mjx 3.3.1,
    mjx/_src/collision_convex.py plane_convex + _manifold_points; MJX is the
@@ -1786,7 +1821,7 @@ static void solve(const mpcr_model_t* m, odata* d) {
        improvement within 1e-6 of the cost ends the solve): the same rule on
        both sides, so neither iterates where the other cannot */
     if (it >= m->iterations || scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance ||
-        prev_cost - cost <= 1e-6 * fabs(cost))
+        (!(g_exact & EXACT_NEWTON) && prev_cost - cost <= g_floor[0] * fabs(cost)))
       break;
     for (int i = 0; i < nv; i++)
       for (int j = 0; j < nv; j++) {
@@ -1853,7 +1888,7 @@ static void solve(const mpcr_model_t* m, odata* d) {
       if (lo.d0 < 0 && lo.d0 > -gtol) break;
       if (hi.d0 > 0 && hi.d0 < gtol) break;
       /* the kernel's bracket floor: closed to 1e-6 relative */
-      if (fabs(hi.alpha - lo.alpha) <= 1e-6 * fmax(fabs(lo.alpha), fabs(hi.alpha))) break;
+      if (!(g_exact & EXACT_LS) && fabs(hi.alpha - lo.alpha) <= 1e-6 * fmax(fabs(lo.alpha), fabs(hi.alpha))) break;
       lspt lo_next = ls_eval(d, qg, jar, jv, lo.alpha - lo.d0 / lo.d1);
       lspt hi_next = ls_eval(d, qg, jar, jv, hi.alpha - hi.d0 / hi.d1);
       lspt mid = ls_eval(d, qg, jar, jv, 0.5 * (lo.alpha + hi.alpha));
@@ -2087,7 +2122,9 @@ int oracle_ls_inputs(const mpcr_model_t* m, const double* qpos, const double* qv
      cost4    : n x 4 (cost, cost_g, cost_r, cost_c)
      theta    : n x (nctrl*H) joint-major post-step qpos (nullable)
      slots    : n x H x nslot masked contact distances (nullable)
-     eef      : n x H x 7 (tcp pos, hande quat) (nullable)              */
+     eef      : n x H x 7 (tcp pos, hande quat) (nullable)
+     info     : n x 3 ints (busiest step's rows, its active contacts, and
+                the integer #{c < 0} term of cost_c, SBP/mjx_planner.py:296) */
 int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, const double* q0,
                    const double* w, const double* ptgt, const double* qtgt, double* cost4, double* theta,
                    double* slots, double* eef, int* info, double noise, unsigned seed,
@@ -2108,7 +2145,7 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
     memcpy(d->qvel, m->qvel_init, sizeof(double) * m->nv);
     for (int j = 0; j < nc; j++) d->qpos[m->ctrl_qposadr[j]] = q0[j];
     double cg = 0, cr = 0, cc = 0;
-    int maxrows = 0, maxact = 0;
+    int maxrows = 0, maxact = 0, nneg = 0;
     const double* td = thetadot + (size_t)b * nc * H;
     for (int t = 0; t < H; t++) {
       for (int j = 0; j < nc; j++) d->qvel[m->ctrl_dofadr[j]] = td[j * H + t];
@@ -2139,7 +2176,7 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
         for (int s = 0; s < m->pair_ncon[pi]; s++) {
           double c = d->con[m->pair_conadr[pi] + s].dist;
           if (slots) slots[((size_t)b * H + t) * m->nslot + sa + s] = c;
-          if (c < 0) cc += 1;
+          if (c < 0) { cc += 1; nneg++; }
           if (t > 0) {
             double g = cprev[sa + s] * (1 - 0.005) - c; /* y = 0.005, :287-291 */
             if (g > 0) cc += g;
@@ -2162,7 +2199,7 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
     cost4[4 * b + 1] = cg;
     cost4[4 * b + 2] = cr;
     cost4[4 * b + 3] = cc;
-    if (info) { info[2 * b] = maxrows; info[2 * b + 1] = maxact; }
+    if (info) { info[3 * b] = maxrows; info[3 * b + 1] = maxact; info[3 * b + 2] = nneg; }
   }
   free(cprev);
   free(d);

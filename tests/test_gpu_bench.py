@@ -1,0 +1,51 @@
+"""bench.py's own multi-rank code path (it had never run with
+world > 1).  Two ranks share the box's one GPU over gloo (RCCL refuses two
+ranks on one device): torch.distributed.run launches bench.py exactly as the
+driver does for N > 1, with --backend gloo; the global batch is fixed
+(--scaling strong), so the reduced best key and the global top-E of the
+elite exchange must equal a one-process run over the same batch."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMMON = ["--config", "c3", "--scaling", "strong", "--candidates", "512", "--steps", "2", "--warmup", "1",
+          "--exchange", "elite", "--no-cpu-baseline", "--no-contact-report"]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_equal_one_gpu():
+    one = _run([sys.executable, "bench.py"] + COMMON)
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                "--backend", "gloo"] + COMMON)
+    assert one["config"]["world_size_seen"] == 1
+    assert two["config"]["world_size_seen"] == 2 and two["config"]["backend"] == "gloo"
+    assert two["n_gpus"] == 2 and two["config"]["candidates_per_gpu"] == 256
+    # the global best (8-byte key MIN all-reduce) and the global top-E of the
+    # elite exchange (local top-E, all-gather, global top-E), both in the timed step
+    assert two["best"] == one["best"], (one["best"], two["best"])
+    assert two["elites"]["k"] == one["elites"]["k"] == int(0.05 * 512)
+    assert two["elites"]["exchanges_timed"] == 2
+    assert two["elites"]["cost_sum"] == one["elites"]["cost_sum"]
+    assert two["elites"]["first"] == one["elites"]["first"]

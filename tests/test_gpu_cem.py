@@ -267,3 +267,21 @@ def test_cem_iteration_parity(torch_cuda):
     x_e, idx, c_e = cem_np.ellite(cost, xs, 0.05)
     m_ref, _ = cem_np.mean_cov(c_e, mean0, 10 * np.eye(p.nvar), x_e)
     assert np.abs(out[6] - m_ref).max() < 1e-3 * max(1.0, np.abs(m_ref).max())
+    # the selected candidate's cost components best_cost_g / _r / _c
+    # (SBP/mjx_planner.py:395-402) against the oracle's at the same index, to
+    # 1e-4 or the candidate's own conditioning (8 fp32-sized probes)
+    k = np.where((out[7][-1] == out[4].T.reshape(-1)).all(axis=1))[0]
+    assert k.size >= 1
+    i = int(k[0])
+    W3 = np.array([20.0, 3.0, 80.0])
+    ref = o["cost4"][i]
+    sens = np.zeros(4)
+    for sd in range(1, 9):
+        b = oracle.rollout(p.model, td[i:i + 1], Q0, W3, PT, QT, want_theta=False, noise=1e-6, seed=sd)["cost4"][0]
+        sens = np.maximum(sens, np.abs(b - ref) / np.maximum(np.abs(ref), 1e-12))
+    got = np.array([out[0][-1], out[1], out[2], out[3]], dtype=np.float64)
+    for c in range(4):
+        if ref[c] == 0 and got[c] == 0:
+            continue
+        rel = abs(got[c] - ref[c]) / max(abs(ref[c]), 1e-12)
+        assert rel < max(1e-4, 2 * sens[c]), (c, got, ref, sens)

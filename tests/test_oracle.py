@@ -118,3 +118,52 @@ def test_box_settles_on_table(all_models):
         qpos, qvel, ws = r["qpos"], r["qvel"], r["qacc_warmstart"]
     assert abs(qpos[a + 2] - 0.525) < 0.01, qpos[a:a + 3]
     assert np.abs(qvel[8:14]).max() < 0.05
+
+
+def _cost_batch(m, n=8, H=20, seed=3):
+    rng = np.random.default_rng(seed)
+    t = np.arange(H) * 0.05
+    td = (rng.uniform(-0.6, 0.6, (n, 6, 1)) * np.sin(rng.uniform(0.2, 2, (n, 6, 1)) * t)).reshape(n, 6 * H)
+    return td, np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0]), np.array([20.0, 3.0, 80.0]), \
+        np.array([-0.3, -0.3, 0.5]), np.array([0.0, 1.0, 0.0, 0.0])
+
+
+def test_integer_collision_count_is_the_slot_count(all_models):
+    """info's #{c < 0} (SBP/mjx_planner.py:296) is the number of negative
+    masked-slot distances over the horizon."""
+    m = all_models["scene_mjx"]
+    td, q0, w, pt, qt = _cost_batch(m)
+    out = oracle.rollout(m, td, q0, w, pt, qt, want_slots=True)
+    np.testing.assert_array_equal(out["nneg"], (out["slots"] < 0).sum(axis=(1, 2)))
+
+
+def test_exact_mode_switches_and_restores(all_models):
+    """The MuJoCo-exact mode (no kernel-matching floors / bands) is a global
+    switch that the context manager restores; contact-free costs agree with
+    the default mode to the Newton floor's size."""
+    m = all_models["scene_mjx"]
+    td, q0, w, pt, qt = _cost_batch(m, n=4)
+    a = oracle.rollout(m, td, q0, w, pt, qt)["cost4"]
+    with oracle.exact():
+        assert oracle.lib().oracle_get_exact() == 31
+        b = oracle.rollout(m, td, q0, w, pt, qt)["cost4"]
+    assert oracle.lib().oracle_get_exact() == 0
+    assert np.all(np.isfinite(b))
+    assert np.median(np.abs(a - b) / np.maximum(np.abs(a), 1e-12)) < 1e-3
+
+
+def test_fp32_build_tracks_fp64(all_models):
+    """oracle_f32.c (bench.py's cpu_baseline at the reference's fp32) computes
+    the same costs as the fp64 checker to fp32 accuracy on a smooth batch."""
+    m = all_models["ur5e_hande_mjx"]
+    td, q0, w, pt, qt = _cost_batch(m, n=6, H=16, seed=5)
+    r64 = oracle.Runner(m, 2, q0, w, pt, qt, precision="fp64")
+    r32 = oracle.Runner(m, 2, q0, w, pt, qt, precision="fp32")
+    try:
+        c64, c32 = r64.rollout(td), r32.rollout(td)
+    finally:
+        r64.close()
+        r32.close()
+    assert c32.dtype == np.float32
+    rel = np.abs(c32[:, 0] - c64[:, 0]) / np.abs(c64[:, 0])
+    assert np.median(rel) < 1e-4, rel

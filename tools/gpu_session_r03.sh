@@ -1,0 +1,75 @@
+#!/bin/bash
+# Round-3 measurement session on one MI355X: bench lines (C3 default, C2,
+# C4 with the elite exchange, C3 strong-scaling mode on 1 GPU), the rocprofv3
+# kernel-trace summary of the default bench command, and the PMC passes
+# (FETCH_SIZE, WRITE_SIZE, SQ instruction counters) -- each pass its own run.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/r03
+mkdir -p $OUT
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "[session] $name: $*"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[session] $name rc=$rc"; tail -3 "$OUT/$name.log"
+  if fatal $rc; then echo "[session] fatal rc=$rc in $name, stopping"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-tests,bench,prof,pmc,wavetime}
+if [[ $STEPS == *host* ]]; then  # the box's CPU share: cgroup quota, affinity, nproc
+  { cat /sys/fs/cgroup/cpu.max 2>/dev/null; nproc; python -c "import os; print(len(os.sched_getaffinity(0)), os.cpu_count())"; \
+    grep -m1 "model name" /proc/cpuinfo; env | grep -E "OMP|MAX_JOBS" ; } > $OUT/host.log 2>&1
+fi
+if [[ $STEPS == *tests* ]]; then
+  MPCR_PARITY_LOG=$OUT/parity.jsonl run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+fi
+if [[ $STEPS == *abdual* ]]; then  # pacing A/B on the dual-arm shard (build_variants/{nopace,pace}.so)
+  i=0
+  for v in nopace pace nopace pace; do
+    i=$((i+1)); MODEL=dual_arm N=4096 H=100 R=3 run ab_dual_${i}_$v 200 python tools/ab_time.py build_variants/$v.so
+  done
+fi
+if [[ $STEPS == *triage* ]]; then  # parity triage: which candidates miss, then the per-step replay of them
+  run triage_c3 300 python tools/parity_triage.py scene_mjx 4096 50 3 c3
+  run diag_c3 300 python tools/diag_parity.py scene_mjx 4096 50 3 $(cat gpurun_out/triage_c3.txt)
+  run triage_c2 300 python tools/parity_triage.py ur5e_hande_mjx 1024 50 2 c2
+  run triage_c4 600 python tools/parity_triage.py dual_arm 4096 100 4 c4
+fi
+if [[ $STEPS == *exact* ]]; then  # the kernel against the MuJoCo-exact oracle (no kernel-matching floors)
+  ORACLE_EXACT=1 run exact_c2 300 python tools/parity_triage.py ur5e_hande_mjx 1024 50 2 c2_exact
+  ORACLE_EXACT=1 run exact_c3 300 python tools/parity_triage.py scene_mjx 4096 50 3 c3_exact
+  ORACLE_EXACT=1 run exact_c4 600 python tools/parity_triage.py dual_arm 4096 100 4 c4_exact
+fi
+if [[ $STEPS == *mrank* ]]; then
+  run mrank 400 python -u -m pytest tests/test_gpu_bench.py -v --timeout 300 --timeout-method thread
+fi
+if [[ $STEPS == *bench* ]]; then
+  run bench_c3 300 python bench.py
+  run bench_c2 300 python bench.py --config c2
+  run bench_c4 300 python bench.py --config c4 --no-cpu-baseline --steps 5 --warmup 1
+  run bench_c3_strong 300 python bench.py --scaling strong --no-cpu-baseline
+fi
+if [[ $STEPS == *prof* ]]; then
+  run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 10 --warmup 2
+fi
+if [[ $STEPS == *pmc* ]]; then
+  i=0
+  for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    run pmc$i 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
+  done
+fi
+if [[ $STEPS == *c5* ]]; then
+  run c5_dual 300 python tools/bench_mpc.py --model dual_arm --ticks 30
+  run c5_planner 200 python tools/bench_mpc.py --model planner_scene --ticks 30
+fi
+if [[ $STEPS == *phase* ]]; then  # needs libmpcr_prof.so (python tools/phase_profile.py --build, CPU container)
+  run phase_c4 200 env N=4096 H=100 python tools/phase_profile.py dual_arm $OUT/phase_c4.json
+fi
+if [[ $STEPS == *wavetime* ]]; then
+  N=4096 run wavetime 120 python tools/wavetime.py scene_mjx $OUT/wavetime_c3_4096.json
+fi
+echo "[session] done"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B timing of build_variants/*.so (interleaved) + one SQ latency-level PMC pass
 # on the first variant.  Diagnostic.
-set -u
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/lat
@@ -9,7 +9,7 @@ mkdir -p $OUT
 for round in 1 2; do
   for v in "$@"; do
     R=20 timeout -k 10 120 python tools/ab_time.py build_variants/$v.so 2>&1 | grep -v amdgpu.ids
-    rc=$?; case $rc in 124|134|137|139) exit $rc;; esac
+    rc=${PIPESTATUS[0]}; case $rc in 124|134|137|139) exit $rc;; esac
   done
 done
 if [ -n "${PMC:-}" ]; then
