@@ -621,7 +621,7 @@ __device__ __forceinline__ float point_box(const float p[3], const float h[3], f
 // (libccd MPR; one penetration contact per pair)
 
 #ifndef MPCR_MPR_TOL
-#define MPCR_MPR_TOL 1e-5f  // the oracle's MPR_TOL (see there: not MuJoCo's 1e-6)
+#define MPCR_MPR_TOL 1e-6f  // MuJoCo's ccd_tolerance (round 3; 1e-5 before)
 #endif
 #ifndef MPCR_MPR_ITER
 #define MPCR_MPR_ITER 50
@@ -633,12 +633,12 @@ __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
 
 // Ties in the support mapping resolve as in the oracle's support(): a box /
 // capsule / cylinder axis with |l_k| < kSupTie |l| contributes 0 (its face or
-// segment centre) instead of the sign of rounding noise, and the hull climb
-// only moves to a neighbour beating the current vertex by more than kSupBand
-// metres along the unit direction (coplanar vertices are ties, the first in
-// list order wins).
+// segment centre: MuJoCo's mju_sign(0) = 0, widened to the fp32 rounding of a
+// component that is exactly zero in fp64), and the hull climb moves to the
+// neighbour that beats the current vertex the most (strictly; kSupBand > 0
+// would make it the first within that many metres).
 #ifndef MPCR_SUP_BAND
-#define MPCR_SUP_BAND 1e-5f  // the oracle's SUP_BAND (experiments: tools/build_variant.py -DMPCR_SUP_BAND=...)
+#define MPCR_SUP_BAND 0.f  // MuJoCo's strict climb (round 3; 1e-5 before)
 #endif
 #ifndef MPCR_SUP_TIE
 #define MPCR_SUP_TIE 1e-6f  // < 0: MuJoCo's mju_sign (only an exact zero is a tie)

@@ -56,7 +56,8 @@ def lib():
     return _LIB
 
 
-FLOOR_DEFAULTS = (1e-6, 1e-5, 1e-6, 1e-5)  # Newton, support band, support tie, MPR tol (mpcr_oracle.c g_floor)
+FLOOR_DEFAULTS = (1e-6, 0.0, 1e-6, 1e-5)  # Newton, support band, support tie, MPR tol (mpcr_oracle.c g_floor)
+DEFAULT_EXACT = 1 | 2 | 4  # mpcr_oracle.c g_exact: MuJoCo's Newton / line-search stop, ccd_tolerance
 
 
 def _both():

@@ -916,19 +916,22 @@ static void col_box_box(const odata* d, int ga, int gb, const double* ha, const 
    previous query on this geom ended at (-1: none), where the climb starts */
 /* ties in the support mapping resolve the same way in fp32 and fp64: a box /
    capsule / cylinder axis with |l_k| < SUP_TIE |l| contributes its face (or
-   segment) centre, 0, instead of the sign of rounding noise; the hull climb
-   only moves to a neighbour that beats the current vertex by more than
-   SUP_BAND metres (coplanar vertices are ties) */
+   segment) centre, 0 (MuJoCo's mju_sign(0) = 0, widened to the fp32 rounding
+   of a component that is exactly zero in fp64); the hull climb moves to the
+   neighbour that beats the current vertex the most (strictly: MuJoCo's), or,
+   with a band > 0 (oracle_set_floor(1, b)), to the first within b metres */
 #define SUP_TIE_K 1e-6
-#define SUP_BAND_K 1e-5
-/* MuJoCo-exact mode (oracle_set_exact(1)): every kernel-matching
-   floor, band and tolerance of this file is switched off -- strict support
-   maxima, exact argmax picks, ccd_tolerance 1e-6, MuJoCo's own Newton stop
-   test and line search without the 1e-6 bracket floor -- so the effect of
-   those rules on parity can be measured instead of assumed
-   (tests/test_gpu_parity.py::test_parity_vs_mujoco_exact_oracle).  A global
-   switch: set it before a run, not while one is in flight. */
-static int g_exact = 0; /* bit mask of the rules run MuJoCo-exact (EXACT_* below); 0 = the kernel's */
+#define SUP_BAND_K 1e-5 /* the round-2 band, kept for the experiments */
+/* Which rules run MuJoCo-exact: a bit mask of EXACT_* below, set
+   by oracle_set_exact; the others run at the kernel's values (oracle_set_floor).
+   The default is MuJoCo's Newton stop test, its line search, ccd_tolerance
+   1e-6 and strict support maxima; two fp32-robust rules stay the kernel's:
+   the support-axis tie above (EXACT_SUP: mju_sign) and the manifold picks
+   among near-equal candidates (EXACT_PICK: exact argmax -- a resting flat
+   face has exactly coplanar vertices, whose fp32 values tie by rounding).
+   Global: set before a run, not while one is in flight.  DESIGN.md §Parity
+   lists what each rule moves. */
+static int g_exact = 1 | 2 | 4;
 #define EXACT_NEWTON 1  /* Newton stop without the 1e-6 relative improvement floor */
 #define EXACT_LS 2      /* line search without the 1e-6 relative bracket floor */
 #define EXACT_MPR 4     /* MPR gap tolerance = ccd_tolerance 1e-6 */
@@ -938,7 +941,7 @@ void oracle_set_exact(int mask) { g_exact = mask; }
 int oracle_get_exact(void) { return g_exact; }
 /* the kernel's values of the rules (oracle_set_floor: experiments that size
    them against the exact mode) */
-static double g_floor[4] = {1e-6 /* Newton */, SUP_BAND_K, SUP_TIE_K, 1e-5 /* MPR */};
+static double g_floor[4] = {1e-6 /* Newton */, 0.0 /* support band: strict climb */, SUP_TIE_K, 1e-5 /* MPR */};
 void oracle_set_floor(int which, double v) { if (which >= 0 && which < 4) g_floor[which] = v; }
 #define SUP_TIE ((g_exact & EXACT_SUP) ? 0.0 : g_floor[2])
 #define SUP_BAND ((g_exact & EXACT_SUP) ? 0.0 : g_floor[1])

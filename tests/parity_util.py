@@ -27,7 +27,8 @@ Then
   3 binomial sigma + 1 %;
 * median error at fp32 level;
 * the selection (SBP/mjx_planner.py:395 argmin): the GPU's pick has the
-  oracle's minimum cost to within both candidates' conditioning, the GPU's
+  oracle's minimum cost to within both candidates' conditioning (probes A,
+  B and F), the GPU's
   cost of its pick is within its conditioning of the oracle's, and the
   indices agree unless the oracle's own best two are that close.
 """
@@ -117,7 +118,7 @@ def check(m, g_cost, o, sens, label="", strict_well=True):
     bw = max(stats["probe_b_well_miss"], stats["probe_f_well_miss"]) / max(nw, 1)
     stats["well_miss_allowed"] = float((bw + _sigma3(bw, nw)) * max(nw, 1))
     ig, io = int(np.argmin(g)), int(np.argmin(oc))
-    ug, uo = max(TOL, sens[ig], pb[ig]), max(TOL, sens[io], pb[io])
+    ug, uo = max(TOL, sens[ig], pb[ig], pf[ig]), max(TOL, sens[io], pb[io], pf[io])
     stats.update(sel_gpu=ig, sel_oracle=io, sel_rel=float(rel[ig]), sel_gap=float((oc[ig] - oc[io]) / abs(oc[io])))
     _log(label, stats)
     assert not strict_well or stats["well_miss"] <= stats["well_miss_allowed"], (

@@ -138,16 +138,16 @@ def test_integer_collision_count_is_the_slot_count(all_models):
 
 
 def test_exact_mode_switches_and_restores(all_models):
-    """The MuJoCo-exact mode (no kernel-matching floors / bands) is a global
-    switch that the context manager restores; contact-free costs agree with
-    the default mode to the Newton floor's size."""
+    """The MuJoCo-exact mode (every rule MuJoCo's, the support-axis tie by
+    mju_sign too, exact argmax picks) is a global switch that the context
+    manager restores."""
     m = all_models["scene_mjx"]
     td, q0, w, pt, qt = _cost_batch(m, n=4)
     a = oracle.rollout(m, td, q0, w, pt, qt)["cost4"]
     with oracle.exact():
         assert oracle.lib().oracle_get_exact() == 31
         b = oracle.rollout(m, td, q0, w, pt, qt)["cost4"]
-    assert oracle.lib().oracle_get_exact() == 0
+    assert oracle.lib().oracle_get_exact() == oracle.DEFAULT_EXACT
     assert np.all(np.isfinite(b))
     assert np.median(np.abs(a - b) / np.maximum(np.abs(a), 1e-12)) < 1e-3
 

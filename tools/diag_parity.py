@@ -83,7 +83,7 @@ def main():
         rec["steps"] = steps
         worst = sorted(steps, key=lambda s: -s["qacc_err"] / s["qacc_scale"])[:4]
         # the worst step in detail: contacts that differ between the plant and the oracle
-        tw = worst[0]["t"]
+        tw = int(os.environ.get("DIAG_STEP", worst[0]["t"]))  # DIAG_STEP: inspect that step instead
         qpos = np.array(m.qpos_init[:m.nq], dtype=np.float64)
         qpos[qa] = pu.Q0
         qvel = np.array(m.qvel_init[:m.nv], dtype=np.float64)

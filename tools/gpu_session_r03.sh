@@ -46,6 +46,20 @@ fi
 if [[ $STEPS == *mrank* ]]; then
   run mrank 400 python -u -m pytest tests/test_gpu_bench.py -v --timeout 300 --timeout-method thread
 fi
+if [[ $STEPS == *share* ]]; then  # one rank's share of C4 / C5 at 1..8 GPUs, timed on one GPU
+  for nh in "8192 50" "4096 50" "2048 50" "1024 50" "4096 100" "2048 100" "1024 100"; do
+    set -- $nh
+    MODEL=dual_arm N=$1 H=$2 R=5 run share_dual_${1}x$2 300 python tools/ab_time.py manipulator_mujoco_amd/libmpcr.so
+  done
+  for n in 4096 2048 1024 512; do
+    N=$n R=20 run share_c3_$n 200 python tools/ab_time.py manipulator_mujoco_amd/libmpcr.so
+  done
+  N=1024 MODEL=ur5e_hande_mjx R=20 run share_c2_1024 200 python tools/ab_time.py manipulator_mujoco_amd/libmpcr.so
+fi
+if [[ $STEPS == *micro* ]]; then
+  run micro_build 120 hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -o /tmp/valu_rate tools/micro/valu_rate.hip
+  run micro_valu 60 /tmp/valu_rate
+fi
 if [[ $STEPS == *bench* ]]; then
   run bench_c3 300 python bench.py
   run bench_c2 300 python bench.py --config c2
@@ -61,6 +75,9 @@ if [[ $STEPS == *pmc* ]]; then
     i=$((i+1))
     run pmc$i 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
   done
+fi
+if [[ $STEPS == *lat* ]]; then  # memory-latency levels of the rollout kernel (C3 bench command)
+  run pmc_lat 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_SMEM SQ_INST_LEVEL_LDS SQ_WAIT_ANY --output-format csv -d $OUT/pmc_lat -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
 fi
 if [[ $STEPS == *c5* ]]; then
   run c5_dual 300 python tools/bench_mpc.py --model dual_arm --ticks 30

@@ -31,9 +31,11 @@ from test_gpu_parity import projected_xi  # noqa: E402
 def main():
     name, n, H, seed = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     label = sys.argv[5] if len(sys.argv) > 5 else f"{name}_{n}x{H}"
-    # ORACLE_EXACT=1: every rule MuJoCo-exact; ORACLE_MASK / ORACLE_FLOORS
-    # ("newton,band,tie,mpr"): a kernel variant's rules (tools/build_variant.py)
-    mask = 31 if os.environ.get("ORACLE_EXACT") == "1" else int(os.environ.get("ORACLE_MASK", "0"))
+    # ORACLE_EXACT=1: every rule MuJoCo-exact (support tie by mju_sign too);
+    # ORACLE_MASK / ORACLE_FLOORS ("newton,band,tie,mpr"): a kernel variant's
+    # rules (tools/build_variant.py); default: the oracle's defaults
+    import oracle
+    mask = 31 if os.environ.get("ORACLE_EXACT") == "1" else int(os.environ.get("ORACLE_MASK", oracle.DEFAULT_EXACT))
     floors = os.environ.get("ORACLE_FLOORS")
     floors = [float(x) for x in floors.split(",")] if floors else None
     m = models.load(name, 0.05)

@@ -25,4 +25,5 @@ done
 for v in v_base v_exact; do
   R=20 step time_c3_$v 200 python tools/ab_time.py build_variants/$v.so
 done
+step valu_rate 60 tools/micro/valu_rate
 echo "[tol] done"
