@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 #define MPCR_MODEL_MAGIC   0x4d504352u /* 'MPCR' */
-#define MPCR_MODEL_VERSION 6
+#define MPCR_MODEL_VERSION 7
 
 #define MPCR_MAX_BODY   48
 #define MPCR_MAX_JNT    40
@@ -40,6 +40,10 @@ extern "C" {
 #define MPCR_MAX_HULLA  49152 /* hull-graph adjacency entries */
 #define MPCR_LUT_R      16    /* support start table: 6 cube faces x R x R cells per hull */
 #define MPCR_MAX_HULLLUT (24 * 6 * MPCR_LUT_R * MPCR_LUT_R) /* 24 hulls */
+#define MPCR_MAX_FACE   12288 /* polygon faces of the polyhedron-pair hulls and boxes */
+#define MPCR_MAX_FACEV  49152 /* face polygon vertex entries (<= MPCR_FACE_MAXV each) */
+#define MPCR_MAX_VFACE  65536 /* vertex -> incident face entries */
+#define MPCR_FACE_MAXV  16    /* vertices kept per face polygon */
 #define MPCR_MAX_TEN    4    /* spatial (site-site) tendons with limits */
 
 /* joint types (MuJoCo mjtJoint) */
@@ -257,6 +261,24 @@ typedef struct mpcr_model_t {
      query's hint if that beats it by the tie band) */
   int32_t geom_lutadr[MPCR_MAX_GEOM]; /* first cell, -1: no hull          */
   int32_t hull_lut[MPCR_MAX_HULLLUT];  /* global vertex index per cell     */
+
+  /* v7: polygon faces of the hulls and boxes of polyhedron pairs (mesh-mesh,
+     box-mesh): the face-clipping contact manifold
+     (mujoco-mjx 3.3.1 convex_convex: a reference face, the incident face
+     clipped to it, up to 4 points).  Coplanar hull triangles are merged;
+     vertices counter-clockwise about the outward normal, at most
+     MPCR_FACE_MAXV kept per face; every vertex lists the faces it lies on. */
+  int32_t nface, nfacev, nvface, pad6;
+  int32_t geom_faceadr[MPCR_MAX_GEOM]; /* first face, -1: none             */
+  int32_t geom_facenum[MPCR_MAX_GEOM];
+  int32_t geom_cornadr[MPCR_MAX_GEOM]; /* a box's 8 corners in hull_vert (bit k: + side of axis k), -1 */
+  int32_t face_vadr[MPCR_MAX_FACE];
+  int32_t face_vnum[MPCR_MAX_FACE];
+  int32_t face_vert[MPCR_MAX_FACEV];   /* global hull_vert indices         */
+  int32_t vert_faceadr[MPCR_MAX_HULLV];
+  int32_t vert_facenum[MPCR_MAX_HULLV];
+  int32_t vert_face[MPCR_MAX_VFACE];   /* global face indices              */
+  double face_plane[MPCR_MAX_FACE][4]; /* outward normal, offset: n.x = offset on the face (geom frame) */
 } mpcr_model_t;
 
 #ifdef __cplusplus

@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 
 MAGIC = 0x4D504352
-VERSION = 6
+VERSION = 7
 
 MAX_BODY, MAX_JNT, MAX_DOF, MAX_NQ = 48, 40, 32, 48
 MAX_GEOM, MAX_SITE, MAX_PAIR, MAX_EQ = 128, 24, 768, 8
@@ -20,6 +20,7 @@ MAX_HULLV, MAX_HULLA = 8192, 49152
 MAX_TEN = 4
 LUT_R = 16
 MAX_HULLLUT = 24 * 6 * LUT_R * LUT_R
+MAX_FACE, MAX_FACEV, MAX_VFACE, FACE_MAXV = 12288, 49152, 65536, 16
 
 COL_PLANE_CAPSULE, COL_PLANE_BOX, COL_CAPSULE_CAPSULE, COL_CAPSULE_BOX, COL_BOX_BOX = 0, 1, 2, 3, 4
 COL_PLANE_SPHERE, COL_SPHERE_SPHERE, COL_SPHERE_CAPSULE, COL_SPHERE_BOX = 5, 6, 7, 8
@@ -106,12 +107,18 @@ class mpcr_model_t(ctypes.Structure):
         ("ten_solimp", _a(_d, MAX_TEN, 5)), ("ten_margin", _a(_d, MAX_TEN)),
         ("ten_invweight0", _a(_d, MAX_TEN)),
         ("geom_lutadr", _a(_i, MAX_GEOM)), ("hull_lut", _a(_i, MAX_HULLLUT)),
+        ("nface", _i), ("nfacev", _i), ("nvface", _i), ("pad6", _i),
+        ("geom_faceadr", _a(_i, MAX_GEOM)), ("geom_facenum", _a(_i, MAX_GEOM)), ("geom_cornadr", _a(_i, MAX_GEOM)),
+        ("face_vadr", _a(_i, MAX_FACE)), ("face_vnum", _a(_i, MAX_FACE)), ("face_vert", _a(_i, MAX_FACEV)),
+        ("vert_faceadr", _a(_i, MAX_HULLV)), ("vert_facenum", _a(_i, MAX_HULLV)), ("vert_face", _a(_i, MAX_VFACE)),
+        ("face_plane", _a(_d, MAX_FACE, 4)),
     ]
 
 
 _LIMITS = dict(nbody=MAX_BODY, njnt=MAX_JNT, nv=MAX_DOF, nq=MAX_NQ, ngeom=MAX_GEOM,
                nsite=MAX_SITE, npair=MAX_PAIR, neq=MAX_EQ, nslot=MAX_SLOT, nctrl=MAX_CTRL, nu=MAX_ACT,
-               nhullv=MAX_HULLV, nhulla=MAX_HULLA, nten=MAX_TEN)
+               nhullv=MAX_HULLV, nhulla=MAX_HULLA, nten=MAX_TEN, nface=MAX_FACE, nfacev=MAX_FACEV,
+               nvface=MAX_VFACE)
 
 # struct field -> Model attribute (when the names differ)
 _ALIASES = {}
@@ -177,8 +184,10 @@ def pack(m) -> mpcr_model_t:
     scalars = ("nbody", "njnt", "nq", "nv", "ngeom", "nsite", "npair", "neq", "ncon", "nslot",
                "nctrl", "hande_body", "tcp_site", "iterations", "ls_iterations", "disableflags",
                "ntree", "timestep", "tolerance", "ls_tolerance", "impratio", "meaninertia")
-    for k in ("nu", "nhullv", "nhulla", "integrator", "cone", "nten"):
+    for k in ("nu", "nhullv", "nhulla", "integrator", "cone", "nten", "nface", "nfacev", "nvface"):
         setattr(s, k, int(getattr(m, k, 0)))
+    for k in ("geom_faceadr", "geom_cornadr"):  # -1: no faces / corners (models without polyhedron pairs)
+        np.ctypeslib.as_array(getattr(s, k))[:] = -1
     for k in ("viscosity", "density"):
         setattr(s, k, float(getattr(m, k, 0.0)))
     for k in scalars:
@@ -188,7 +197,8 @@ def pack(m) -> mpcr_model_t:
     for name, _ in mpcr_model_t._fields_:
         if name in scalars or name.startswith("pad") or name in ("magic", "version", "nbytes", "gravity",
                                                                  "integrator", "cone", "nu", "nhullv",
-                                                                 "nhulla", "nten", "viscosity", "density"):
+                                                                 "nhulla", "nten", "viscosity", "density",
+                                                                 "nface", "nfacev", "nvface"):
             continue
         attr = _ALIASES.get(name, name)
         if hasattr(m, attr):

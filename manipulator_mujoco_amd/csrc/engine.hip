@@ -81,6 +81,12 @@ struct mpcr_engine {
   float4* d_hull_adjv = nullptr;
   float4* d_hull_head = nullptr;
   float4* d_hull_lut = nullptr;
+  // polygon faces (polyhedron-pair manifold)
+  float4* d_face_plane = nullptr;
+  int2* d_face_vinfo = nullptr;
+  int* d_face_vert = nullptr;
+  int2* d_vert_finfo = nullptr;
+  int* d_vert_face = nullptr;
   bool wide = false;  // kernel variant: rollout_kernel<32, 32, 72, true>
 };
 
@@ -167,6 +173,34 @@ static int check_model(const mpcr_model_t& m) {
     for (int g : {m.pair_geom1[p], m.pair_geom2[p]})
       if (m.geom_type[g] == MPCR_GEOM_MESH && m.geom_hulladr[g] < 0)
         return fail(MPCR_EMODEL, "mesh geom %d in a pair has no convex hull", g);
+  // polygon faces (v7): every index the manifold follows stays in its table
+  if (m.nface < 0 || m.nface > MPCR_MAX_FACE || m.nfacev < 0 || m.nfacev > MPCR_MAX_FACEV || m.nvface < 0 ||
+      m.nvface > MPCR_MAX_VFACE)
+    return fail(MPCR_EMODEL, "model faces exceed blob capacity");
+  for (int g = 0; g < m.ngeom; g++) {
+    if (m.geom_faceadr[g] >= 0 && m.geom_faceadr[g] + m.geom_facenum[g] > m.nface)
+      return fail(MPCR_EMODEL, "geom %d faces outside the face table", g);
+    if (m.geom_cornadr[g] >= 0 && (m.geom_type[g] != MPCR_GEOM_BOX || m.geom_cornadr[g] + 8 > m.nhullv))
+      return fail(MPCR_EMODEL, "geom %d box corners outside the vertex table", g);
+    if (m.geom_faceadr[g] >= 0 && m.geom_type[g] == MPCR_GEOM_BOX && m.geom_cornadr[g] < 0)
+      return fail(MPCR_EMODEL, "box geom %d has faces but no corners", g);
+  }
+  for (int f = 0; f < m.nface; f++)
+    if (m.face_vadr[f] < 0 || m.face_vnum[f] < 3 || m.face_vnum[f] > MPCR_FACE_MAXV ||
+        m.face_vadr[f] + m.face_vnum[f] > m.nfacev)
+      return fail(MPCR_EMODEL, "face %d polygon outside the face-vertex table", f);
+  for (int k = 0; k < m.nfacev; k++)
+    if (m.face_vert[k] < 0 || m.face_vert[k] >= m.nhullv) return fail(MPCR_EMODEL, "bad face vertex entry");
+  if (m.nface > 0)
+    for (int v = 0; v < m.nhullv; v++)
+      if (m.vert_faceadr[v] < 0 || m.vert_faceadr[v] + m.vert_facenum[v] > m.nvface)
+        return fail(MPCR_EMODEL, "hull vertex %d face list outside the table", v);
+  for (int k = 0; k < m.nvface; k++)
+    if (m.vert_face[k] < 0 || m.vert_face[k] >= m.nface) return fail(MPCR_EMODEL, "bad vertex face entry");
+  for (int p = 0; p < m.npair; p++)  // a polyhedron pair's geoms carry faces
+    if (m.pair_func[p] == MPCR_COL_CONVEX && m.pair_ncon[p] == 4)
+      for (int g : {m.pair_geom1[p], m.pair_geom2[p]})
+        if (m.geom_faceadr[g] < 0) return fail(MPCR_EMODEL, "polyhedron-pair geom %d has no faces", g);
   return MPCR_OK;
 }
 
@@ -517,6 +551,8 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.geom_hulladr[i] = m.geom_hulladr[g];
     d.geom_hullnum[i] = m.geom_hullnum[g];
     d.geom_lutadr[i] = m.geom_lutadr[g];
+    d.geom_faceadr[i] = m.geom_faceadr[g];
+    d.geom_cornadr[i] = m.geom_cornadr[g];
     for (int k = 0; k < 3; k++) d.geom_size[i][k] = (float)m.geom_size[g][k];
     if (dmap[b] >= 0) {
       d.geom_body[i] = dmap[b];
@@ -758,6 +794,35 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     }
     e->dev.hull_lut = e->d_hull_lut;
   }
+  if (e->host.nface > 0) {  // polygon faces + vertex incidence, pointed to by the device model
+    const mpcr_model_t& h = e->host;
+    std::vector<float4> fp(h.nface);
+    std::vector<int2> fv(h.nface), vf(h.nhullv);
+    for (int f = 0; f < h.nface; f++) {
+      fp[f] = make_float4((float)h.face_plane[f][0], (float)h.face_plane[f][1], (float)h.face_plane[f][2],
+                          (float)h.face_plane[f][3]);
+      fv[f] = make_int2(h.face_vadr[f], h.face_vnum[f]);
+    }
+    for (int v = 0; v < h.nhullv; v++) vf[v] = make_int2(h.vert_faceadr[v], h.vert_facenum[v]);
+    if (hipMalloc(&e->d_face_plane, sizeof(float4) * fp.size()) != hipSuccess ||
+        hipMalloc(&e->d_face_vinfo, sizeof(int2) * fv.size()) != hipSuccess ||
+        hipMalloc(&e->d_face_vert, sizeof(int) * h.nfacev) != hipSuccess ||
+        hipMalloc(&e->d_vert_finfo, sizeof(int2) * vf.size()) != hipSuccess ||
+        hipMalloc(&e->d_vert_face, sizeof(int) * h.nvface) != hipSuccess ||
+        hipMemcpy(e->d_face_plane, fp.data(), sizeof(float4) * fp.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_face_vinfo, fv.data(), sizeof(int2) * fv.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_face_vert, h.face_vert, sizeof(int) * h.nfacev, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_vert_finfo, vf.data(), sizeof(int2) * vf.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_vert_face, h.vert_face, sizeof(int) * h.nvface, hipMemcpyHostToDevice) != hipSuccess) {
+      mpcr_engine_free(e);
+      return fail(MPCR_ENOMEM, "face upload failed");
+    }
+    e->dev.face_plane = e->d_face_plane;
+    e->dev.face_vinfo = e->d_face_vinfo;
+    e->dev.face_vert = e->d_face_vert;
+    e->dev.vert_finfo = e->d_vert_finfo;
+    e->dev.vert_face = e->d_vert_face;
+  }
   const int nc = e->host.nctrl;
   const size_t in_cols = (size_t)nc * (horizon > nbasis ? horizon : nbasis);
   if (hipMalloc(&e->d_model, sizeof(DevModel)) != hipSuccess ||
@@ -815,6 +880,11 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_hints);
   (void)hipFree(e->d_pace);
   (void)hipFree(e->d_mslab);
+  (void)hipFree(e->d_face_plane);
+  (void)hipFree(e->d_face_vinfo);
+  (void)hipFree(e->d_face_vert);
+  (void)hipFree(e->d_vert_finfo);
+  (void)hipFree(e->d_vert_face);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
   (void)hipFree(e->d_hull_adjv);

@@ -127,6 +127,14 @@ struct DevModel {
   unsigned long long* prof;  // wave-level event counters (MPCR_PROFILE builds; else null)
   const float4* hull_head;  // per vertex its first 8 neighbour records as hull_adjv, padded with NaN records:
                             // a climb round addresses them from the vertex index alone (no hull_info load)
+  // polygon faces of polyhedron-pair geoms (mesh-mesh / box-mesh manifold) ----
+  int geom_faceadr[DX_NG];   // first face, -1: none
+  int geom_cornadr[DX_NG];   // a box's 8 corners in hull_vert (bit k: + side of axis k), -1: none
+  const float4* face_plane;  // outward normal xyz | offset (n . x = offset), geom frame
+  const int2* face_vinfo;    // (first face_vert entry, count <= MPCR_FACE_MAXV)
+  const int* face_vert;      // hull_vert indices, counter-clockwise about the normal
+  const int2* vert_finfo;    // per hull vertex: (first vert_face entry, count)
+  const int* vert_face;      // face indices
 
   int ctrl_qposadr[DX_NCTRL], ctrl_dofadr[DX_NCTRL];
 

@@ -10,6 +10,7 @@
 #include <type_traits>
 
 #include "mpcr_device.h"
+#include "../../include/mpcr_model.h"  // MPCR_FACE_MAXV (the face polygon cap)
 
 namespace mpcr {
 
@@ -92,6 +93,7 @@ struct __align__(16) SmemT {
   static constexpr int NQW = WIDE ? DX_NQ : 24, NEQP = WIDE ? DX_NEQ : 1, NACT = WIDE ? DX_NU : 1;
   static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
   static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
+  static constexpr int PMAXW = 2 * MPCR_FACE_MAXV + 2;  // clipped incident face: <= its vertices + one per side plane
   // ---- persistent across the step ----
   float qpos[NQW];
   alignas(16) float qvel[NVW];
@@ -132,7 +134,10 @@ struct __align__(16) SmemT {
     struct {
       union {
         alignas(16) float J[JL][LDJ];  // constraint rows .. Newton
-        int cvx[CVXN];                  // collision: the compacted convex-pair list
+        struct {                        // collision:
+          int cvx[CVXN];                // the compacted convex-pair list
+          alignas(16) float polyw[2][WIDE ? PMAXW : 1][4];  // polyhedron-manifold clip polygon (double buffered)
+        };
       };
       float efc_D[MAXEFC];
       float efc_aref[MAXEFC];
@@ -196,12 +201,13 @@ static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU
 #define MPCR_W_JL 40
 #endif
 #ifndef MPCR_W_MAXACT
-#define MPCR_W_MAXACT 32
+#define MPCR_W_MAXACT 40  // the polyhedron manifold's 4 contacts per face pair: <= 39 in a 1024 x 100 C4 batch
 #endif
 using SmemW = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT>;
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD + SmemN::NVW, "Hessian + J^T f scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
-static_assert(SmemW::JL * SmemW::LDJ >= SmemW::CVXN, "convex-pair list inside the J rows");
+static_assert(SmemW::JL * SmemW::LDJ * 4 >= SmemW::CVXN * 4 + 2 * SmemW::PMAXW * 16 + 16,
+              "convex-pair list and clip polygon inside the J rows");
 #if !defined(MPCR_N_LDS_UNCHECKED)
 static_assert(sizeof(SmemW) <= 152448 / 8, "dual-arm LDS image must fit 8 blocks per CU");
 #endif

@@ -1089,6 +1089,245 @@ __device__ __noinline__ void plane_mesh_manifold_wave(const DevModel* __restrict
 }
 
 constexpr int kPendingManifold = -4;  // narrow_lane: plane-mesh pair awaiting plane_mesh_manifold_wave
+constexpr int kPendingPoly = -5;      // narrow_lane: polyhedron pair hit by MPR, awaiting poly_manifold_wave
+
+// hull vertex index of geom g's support point along dir (world): the mesh
+// climb from hint (the pair's, read only), or the box corner (+ side on an
+// exactly zero component) -- the oracle's support_vertex
+template <class S>
+__device__ __forceinline__ int support_vertex(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
+                                              int hint) {
+  if (m->geom_type[g] == 6) {
+    float l[3];
+    mtv(l, s.gxmat[g], dir);
+    return m->geom_cornadr[g] + (l[0] >= 0.f ? 1 : 0) + (l[1] >= 0.f ? 2 : 0) + (l[2] >= 0.f ? 4 : 0);
+  }
+  float p[3];
+  support_geom(m, s, g, dir, p, hint);
+  return hint;
+}
+
+// world outward normal of face f of geom g and its plane offset relative to
+// c (nw . (x - c) = off on the face)
+template <class S>
+__device__ __forceinline__ void face_rel(const DevModel* __restrict__ m, const S& s, int g, int f, const float* c,
+                                         float nw[3], float& off) {
+  const float4 fp = m->face_plane[f];
+  const float nl[3] = {fp.x, fp.y, fp.z};
+  mv(nw, s.gxmat[g], nl);
+  off = fp.w + nw[0] * (s.gxpos[g][0] - c[0]) + nw[1] * (s.gxpos[g][1] - c[1]) + nw[2] * (s.gxpos[g][2] - c[2]);
+}
+
+// hull vertex v of geom g relative to c
+template <class S>
+__device__ __forceinline__ void vert_rel(const DevModel* __restrict__ m, const S& s, int g, int v, const float* c,
+                                         float w[3]) {
+  const float4 hv = m->hull_vert[v];
+  const float l[3] = {hv.x, hv.y, hv.z};
+  mv(w, s.gxmat[g], l);
+  w[0] += s.gxpos[g][0] - c[0]; w[1] += s.gxpos[g][1] - c[1]; w[2] += s.gxpos[g][2] - c[2];
+}
+
+// Polyhedron pairs (mesh-mesh, box-mesh): the face-clipping manifold
+// (mujoco-mjx 3.3.1 convex_convex; the oracle's poly_manifold, same rules and
+// orders), wave-cooperative: every lane calls it with the same pair and MPR's
+// normal n (g1 -> g2) / depth, lane q receives up to 4 contacts (nsl = 4) or
+// keeps MPR's single one (nsl = 1: an edge axis carries the contact).  One
+// lane per candidate reference face (the faces on both support vertices) with
+// its own support query for the SAT separation, one lane per candidate
+// incident face, Sutherland-Hodgman against the reference face's side planes
+// with one lane per polygon vertex and scan compaction (as box_box_wave), the
+// _manifold_points picks as wave maxima.  Coordinates relative to g2's
+// centre, as MPR's.
+template <class S>
+__device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, S& s, const short* hints, int p,
+                                                const float n[3], float depth, int q, int lane, float dist[4],
+                                                float pos[4][3], float nrm[4][3], int& nsl) {
+  const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
+  const float c[3] = {s.gxpos[g2][0], s.gxpos[g2][1], s.gxpos[g2][2]};
+  const int hw = reinterpret_cast<const int*>(hints)[p - m->cvx_base];
+  const int h0 = (int)(short)(hw & 0xffff), h1 = hw >> 16;
+  // support vertices: lane 0 of g1 along n, lane 1 of g2 along -n
+  int sv = 0;
+  if (lane < 2) {
+    const float sg = lane ? -1.f : 1.f;
+    const float d[3] = {sg * n[0], sg * n[1], sg * n[2]};
+    sv = support_vertex(m, s, lane ? g2 : g1, d, lane ? h1 : h0);
+  }
+  const int s1 = __shfl(sv, 0), s2 = __shfl(sv, 1);
+  const int2 i1 = m->vert_finfo[s1], i2 = m->vert_finfo[s2];
+  const int c1 = min(i1.y, WAVE), c2 = min(i2.y, WAVE - c1), nc = c1 + c2;
+  // candidate reference faces: SAT separation along each outward normal
+  float sep = -3e38f;
+  int fid = -1;
+  if (lane < nc) {
+    const bool two = lane >= c1;
+    const int g = two ? g2 : g1, go = two ? g1 : g2;
+    fid = m->vert_face[two ? i2.x + lane - c1 : i1.x + lane];
+    float nw[3], off, pt[3];
+    face_rel(m, s, g, fid, c, nw, off);
+    const float mn[3] = {-nw[0], -nw[1], -nw[2]};
+    int h = two ? h0 : h1;
+    support_geom(m, s, go, mn, pt, h, c);
+    sep = nw[0] * pt[0] + nw[1] * pt[1] + nw[2] * pt[2] - off;
+  }
+  const float mx = wmax(sep);
+  const unsigned long long bm = __ballot(lane < nc && near_max(sep, mx));
+  const int kb = bm ? __builtin_ctzll(bm) : 0;
+  const float bsep = __shfl(sep, kb);
+  if (!bm || -bsep > 1.05f * depth + 1e-5f) {  // an edge axis: MPR's single contact
+    if (lane == q) nsl = 1;
+    return;
+  }
+  const int fr = __shfl(fid, kb);
+  const bool rtwo = kb >= c1;
+  const int gr = rtwo ? g2 : g1, gi = rtwo ? g1 : g2;
+  float nr[3], offr;
+  face_rel(m, s, gr, fr, c, nr, offr);
+  // incident face: the most anti-parallel face on gi's support vertex along -nr
+  int si = 0;
+  if (lane == 0) {
+    const float d[3] = {-nr[0], -nr[1], -nr[2]};
+    si = support_vertex(m, s, gi, d, rtwo ? h0 : h1);
+  }
+  si = __shfl(si, 0);
+  const int2 ii = m->vert_finfo[si];
+  const int ci = min(ii.y, WAVE);
+  float al = -3e38f;
+  int finc = -1;
+  if (lane < ci) {
+    finc = m->vert_face[ii.x + lane];
+    const float4 fp = m->face_plane[finc];
+    const float nl[3] = {fp.x, fp.y, fp.z};
+    float nw[3];
+    mv(nw, s.gxmat[gi], nl);
+    al = -(nw[0] * nr[0] + nw[1] * nr[1] + nw[2] * nr[2]);
+  }
+  const float mxa = wmax(al);
+  const unsigned long long bma = __ballot(lane < ci && near_max(al, mxa));
+  if (!bma) {
+    if (lane == q) nsl = 1;
+    return;
+  }
+  const int fi = __shfl(finc, __builtin_ctzll(bma));
+  // reference polygon (lane k: vertex k and its edge's outward side-plane
+  // normal), incident polygon into the clip buffer
+  const int2 fri = m->face_vinfo[fr], fii = m->face_vinfo[fi];
+  const int nrv = fri.y, ninc = fii.y;
+  float A[3] = {0.f, 0.f, 0.f}, sn[3];
+  if (lane < nrv) vert_rel(m, s, gr, m->face_vert[fri.x + lane], c, A);
+  {
+    const int ln = lane + 1 >= nrv ? 0 : lane + 1;
+    const float ed[3] = {__shfl(A[0], ln) - A[0], __shfl(A[1], ln) - A[1], __shfl(A[2], ln) - A[2]};
+    cross(sn, ed, nr);
+  }
+  if (lane < ninc) {
+    float w[3];
+    vert_rel(m, s, gi, m->face_vert[fii.x + lane], c, w);
+    s.polyw[0][lane][0] = w[0]; s.polyw[0][lane][1] = w[1]; s.polyw[0][lane][2] = w[2];
+  }
+  sync();
+  int np = ninc, cur = 0;
+  for (int e = 0; e < nrv && np > 0; e++) {
+    const float Ae[3] = {__shfl(A[0], e), __shfl(A[1], e), __shfl(A[2], e)};
+    const float se[3] = {__shfl(sn[0], e), __shfl(sn[1], e), __shfl(sn[2], e)};
+    float P[3] = {0.f, 0.f, 0.f}, Q[3] = {0.f, 0.f, 0.f}, dp = 0.f, dq = 0.f;
+    int e0 = 0, e1 = 0;
+    if (lane < np) {
+      const int k2 = lane + 1 == np ? 0 : lane + 1;
+#pragma unroll
+      for (int k = 0; k < 3; k++) { P[k] = s.polyw[cur][lane][k]; Q[k] = s.polyw[cur][k2][k]; }
+      dp = se[0] * (P[0] - Ae[0]) + se[1] * (P[1] - Ae[1]) + se[2] * (P[2] - Ae[2]);
+      dq = se[0] * (Q[0] - Ae[0]) + se[1] * (Q[1] - Ae[1]) + se[2] * (Q[2] - Ae[2]);
+      e0 = dp <= 0.f;
+      e1 = (dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f);
+    }
+    int tot;
+    const int o = wscan_excl(e0 + e1, tot);
+    if (e0 && o < S::PMAXW) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) s.polyw[cur ^ 1][o][k] = P[k];
+    }
+    if (e1 && o + e0 < S::PMAXW) {
+      const float wgt = dp / (dp - dq);
+#pragma unroll
+      for (int k = 0; k < 3; k++) s.polyw[cur ^ 1][o + e0][k] = P[k] + wgt * (Q[k] - P[k]);
+    }
+    np = min(tot, S::PMAXW);
+    cur ^= 1;
+    sync();
+  }
+  // the clipped points below the reference plane
+  float P[3] = {0.f, 0.f, 0.f}, dk = 3e38f;
+  bool keep = false;
+  if (lane < np) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) P[k] = s.polyw[cur][lane][k];
+    dk = nr[0] * P[0] + nr[1] * P[1] + nr[2] * P[2] - offr;
+    keep = dk < m->pair_margin[p];
+  }
+  const unsigned long long km = __ballot(keep);
+  const int nk = __popcll(km);
+  sync();  // the clip buffer is free for the next pair
+  if (nk == 0) {
+    if (lane == q) nsl = 1;
+    return;
+  }
+  int idx[4] = {-1, -1, -1, -1};
+  if (nk <= 4) {
+    unsigned long long r = km;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (r) { idx[j] = __builtin_ctzll(r); r &= r - 1; }
+    }
+  } else {
+    // _manifold_points: a = the first, b = the farthest from a, c = the
+    // farthest from line ab, d = the farthest from edge bc or ac
+    auto pick = [&](float e, float& mxv) {
+      mxv = wmax(keep ? e : -1.f);
+      return __builtin_ctzll(__ballot(keep && near_max(e, mxv)));
+    };
+    const int ia = __builtin_ctzll(km);
+    const float a[3] = {__shfl(P[0], ia), __shfl(P[1], ia), __shfl(P[2], ia)};
+    float mxv;
+    const int ib = pick((a[0] - P[0]) * (a[0] - P[0]) + (a[1] - P[1]) * (a[1] - P[1]) + (a[2] - P[2]) * (a[2] - P[2]),
+                        mxv);
+    const float b[3] = {__shfl(P[0], ib), __shfl(P[1], ib), __shfl(P[2], ib)};
+    float ab[3];
+    {
+      const float amb[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+      cross(ab, nr, amb);
+    }
+    const int ic = pick(fabsf((a[0] - P[0]) * ab[0] + (a[1] - P[1]) * ab[1] + (a[2] - P[2]) * ab[2]), mxv);
+    const float cc[3] = {__shfl(P[0], ic), __shfl(P[1], ic), __shfl(P[2], ic)};
+    float ac[3], bc[3];
+    {
+      const float amc[3] = {a[0] - cc[0], a[1] - cc[1], a[2] - cc[2]}, bmc[3] = {b[0] - cc[0], b[1] - cc[1], b[2] - cc[2]};
+      cross(ac, nr, amc);
+      cross(bc, nr, bmc);
+    }
+    float bbp, bap;
+    const int ibp = pick(fabsf((b[0] - P[0]) * bc[0] + (b[1] - P[1]) * bc[1] + (b[2] - P[2]) * bc[2]), bbp);
+    const int iap = pick(fabsf((a[0] - P[0]) * ac[0] + (a[1] - P[1]) * ac[1] + (a[2] - P[2]) * ac[2]), bap);
+    idx[0] = ia; idx[1] = ib; idx[2] = ic; idx[3] = beats(bap, bbp) ? iap : ibp;
+  }
+  const float sg = rtwo ? -1.f : 1.f;  // contact normal g1 -> g2
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    bool dup = idx[j] < 0;
+#pragma unroll
+    for (int t = 0; t < j; t++) dup |= idx[t] == idx[j];
+    const int L = idx[j] < 0 ? 0 : idx[j];
+    const float Pj[3] = {__shfl(P[0], L), __shfl(P[1], L), __shfl(P[2], L)};
+    const float dj = __shfl(dk, L);
+    if (lane == q) {
+      dist[j] = dup ? 1e30f : dj;
+#pragma unroll
+      for (int e = 0; e < 3; e++) { pos[j][e] = Pj[e] - 0.5f * dj * nr[e] + c[e]; nrm[j][e] = sg * nr[e]; }
+    }
+  }
+  if (lane == q) nsl = 4;
+}
 
 // per-lane narrow phase for plane/capsule/box-vs-capsule pairs (box-box is
 // wave-cooperative, below).  out: dist[4], pos[4][3], nrm[4][3]
@@ -1312,8 +1551,60 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
         dist[0] = -depth;
 #pragma unroll
         for (int c = 0; c < 3; c++) { pos[0][c] = pp[c]; nrm[0][c] = n[c]; }
+        // a penetrating polyhedron pair: the caller runs the face-clipping manifold
+        if (m->pair_ncon[p] == 4 && depth > 0.f) return kPendingPoly;
       }
       return 1;
+    }
+    if (func == 10 && m->pair_ncon[p] == 4 && m->geom_type[g2] == 5) {
+      // plane - cylinder: MuJoCo's mjc_PlaneCylinder (the oracle's
+      // col_plane_cylinder): deepest rim point, the far cap's on that side,
+      // two near-cap rim points 120 degrees either side of the first
+      const float n[3] = {R1[2], R1[5], R1[8]};
+      float ax[3] = {R2[2], R2[5], R2[8]}, vec[3];
+      float prjaxis = dot3(n, ax);
+      if (prjaxis > 0.f) { ax[0] = -ax[0]; ax[1] = -ax[1]; ax[2] = -ax[2]; prjaxis = -prjaxis; }
+      const float dist0 = n[0] * (x2[0] - x1[0]) + n[1] * (x2[1] - x1[1]) + n[2] * (x2[2] - x1[2]);
+#pragma unroll
+      for (int c = 0; c < 3; c++) vec[c] = ax[c] * prjaxis - n[c];
+      const float len = sqrtf(dot3(vec, vec));
+      if (len < kMinVal) { vec[0] = R2[0]; vec[1] = R2[3]; vec[2] = R2[6]; }
+      else { const float il = 1.f / len; vec[0] *= il; vec[1] *= il; vec[2] *= il; }
+#pragma unroll
+      for (int c = 0; c < 3; c++) { vec[c] *= s2[0]; ax[c] *= s2[1]; }
+      const float prjvec = dot3(vec, n);
+      prjaxis *= s2[1];
+      const float margin = m->pair_margin[p];
+      float d = dist0 + prjaxis + prjvec;
+      dist[0] = d;
+#pragma unroll
+      for (int c = 0; c < 3; c++) { pos[0][c] = x2[c] + vec[c] + ax[c] - 0.5f * d * n[c]; nrm[0][c] = n[c]; }
+      if (d <= margin) {
+        d = dist0 - prjaxis + prjvec;
+        if (d <= margin) {
+          dist[1] = d;
+#pragma unroll
+          for (int c = 0; c < 3; c++) { pos[1][c] = x2[c] + vec[c] - ax[c] - 0.5f * d * n[c]; nrm[1][c] = n[c]; }
+        }
+        d = dist0 + prjaxis - 0.5f * prjvec;
+        if (d <= margin) {
+          float v1[3];
+          cross(v1, vec, ax);
+          const float l1 = sqrtf(dot3(v1, v1));
+          const float sc = l1 > 0.f ? s2[0] * 0.8660254037844386f / l1 : 0.f;
+#pragma unroll
+          for (int k = 0; k < 2; k++) {
+            const float sv = k ? -sc : sc;
+            dist[2 + k] = d;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+              pos[2 + k][c] = x2[c] + sv * v1[c] + ax[c] - 0.5f * vec[c] - 0.5f * d * n[c];
+              nrm[2 + k][c] = n[c];
+            }
+          }
+        }
+      }
+      return 4;
     }
     if (func == 10) {  // plane - convex: deepest support point
       float n[3] = {R1[2], R1[5], R1[8]}, nn[3] = {-R1[2], -R1[5], -R1[8]}, q[3];
@@ -2797,6 +3088,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
               const float* Rp = s.gxmat[gp];
               const float nq[3] = {Rp[2], Rp[5], Rp[8]};
               plane_mesh_manifold_wave(m, s, m->pair_g2[pq], nq, s.gxpos[gp], -dq, q, lane, cd, cp, cn, cn_sl);
+            }
+            for (unsigned long long pm = __ballot(cn_sl == kPendingPoly); pm; pm &= pm - 1) {
+              const int q = __builtin_ctzll(pm);  // penetrating polyhedron pairs, one at a time, all lanes
+              const int pq = __shfl(pc, q);
+              const float dq = __shfl(cd[0], q);
+              const float nq[3] = {__shfl(cn[0][0], q), __shfl(cn[0][1], q), __shfl(cn[0][2], q)};
+              poly_manifold_wave(m, s, hx, pq, nq, -dq, q, lane, cd, cp, cn, cn_sl);
             }
             STAMP(17);
             emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c);

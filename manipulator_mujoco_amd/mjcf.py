@@ -771,6 +771,10 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
                                 f"({geoms[a]['name']!r}, {geoms[bb]['name']!r})")
             func, ncon = fn
             ga, gb = geoms[a], geoms[bb]
+            if func == cmodel.COL_CONVEX and {ga["type"], gb["type"]} <= {6, 7}:
+                ncon = 4  # a polyhedron pair (mesh-mesh, box-mesh): the face-clipping manifold's slots
+            if func == cmodel.COL_PLANE_CONVEX and gb["type"] == 5:
+                ncon = 4  # plane-cylinder: MuJoCo's mjc_PlaneCylinder (up to 4 points)
             if ga["priority"] != gb["priority"]:  # the higher priority geom's parameters
                 gp = ga if ga["priority"] > gb["priority"] else gb
                 condim, friction = gp["condim"], gp["friction"][0]
@@ -969,10 +973,63 @@ def compile_mjcf(path: str, timestep: float | None = None) -> Model:
 # ---------------------------------------------------------------------------
 
 
+FACE_MAXV = 16  # vertices kept per hull face polygon (the manifold clips against them)
+
+
+def _polygon_faces(hv, tris, eqs, nbrs):
+    """Hull faces as planar polygons: Qhull's triangles merged across shared
+    edges when their planes agree (unit normals within 1e-6, offsets within
+    1e-7 of the hull's size), each face's vertices in counter-clockwise order
+    about its outward normal.  Returns [(normal, offset, all vertices
+    (ordered), kept vertices)]: a face with more than FACE_MAXV vertices keeps
+    FACE_MAXV of them evenly spaced around it (an inscribed polygon; what the
+    contact manifold clips against), the incidence lists use all of them."""
+    nt = len(tris)
+    parent = list(range(nt))
+
+    def find(a):
+        while parent[a] != a:
+            parent[a] = parent[parent[a]]
+            a = parent[a]
+        return a
+
+    scale = max(float(np.max(np.linalg.norm(hv, axis=1))), 1e-9)
+    for a in range(nt):
+        for b in nbrs[a]:
+            if b < 0 or b < a:
+                continue
+            if (np.abs(eqs[a, :3] - eqs[b, :3]).max() < 1e-6 and abs(eqs[a, 3] - eqs[b, 3]) < 1e-7 * scale):
+                ra, rb = find(a), find(b)
+                if ra != rb:
+                    parent[max(ra, rb)] = min(ra, rb)
+    groups = {}
+    for t in range(nt):
+        groups.setdefault(find(t), []).append(t)
+    faces = []
+    for root in sorted(groups):
+        ts = groups[root]
+        n = eqs[ts, :3].mean(axis=0)
+        n /= np.linalg.norm(n)
+        vs = sorted({int(x) for t in ts for x in tris[t]})
+        P = hv[vs]
+        off = float((P @ n).mean())
+        # order counter-clockwise about n (angles in the face plane)
+        u = np.cross(n, [1.0, 0.0, 0.0] if abs(n[0]) < 0.9 else [0.0, 1.0, 0.0])
+        u /= np.linalg.norm(u)
+        w = np.cross(n, u)
+        c = P.mean(axis=0)
+        ang = np.arctan2((P - c) @ w, (P - c) @ u)
+        order = [vs[k] for k in np.argsort(ang, kind="stable")]
+        kept = order if len(order) <= FACE_MAXV else [order[(k * len(order)) // FACE_MAXV] for k in range(FACE_MAXV)]
+        faces.append((n, off, order, kept))
+    return faces
+
+
 def convex_hull(verts):
-    """Hull vertices (recentred on their mean), the centre, and the vertex
-    graph (neighbour lists) of a point cloud: what hill-climbing support
-    queries walk (MuJoCo keeps the same graph, mesh_graph)."""
+    """Hull vertices (recentred on their mean), the centre, the vertex graph
+    (neighbour lists) of a point cloud -- what hill-climbing support queries
+    walk (MuJoCo keeps the same graph, mesh_graph) -- and the hull's faces
+    (_polygon_faces, in the recentred frame)."""
     from scipy.spatial import ConvexHull
     v = np.unique(np.asarray(verts, dtype=np.float64).reshape(-1, 3), axis=0)
     h = ConvexHull(v)
@@ -981,13 +1038,37 @@ def convex_hull(verts):
     hv = v[idx]
     c = hv.mean(axis=0)
     nbr = [set() for _ in idx]
-    for tri in h.simplices:
-        t = [remap[int(x)] for x in tri]
+    tris = np.array([[remap[int(x)] for x in tri] for tri in h.simplices], dtype=np.int64)
+    for t in tris:
         for a in range(3):
             for b in range(3):
                 if a != b:
                     nbr[t[a]].add(t[b])
-    return hv - c, c, [sorted(n) for n in nbr]
+    eqs = np.array(h.equations, dtype=np.float64)
+    eqs[:, 3] = -(eqs[:, 3] + eqs[:, :3] @ c)  # n . x = offset in the recentred frame
+    faces = _polygon_faces(hv - c, tris, eqs, np.asarray(h.neighbors))
+    return hv - c, c, [sorted(n) for n in nbr], faces
+
+
+def box_faces(size):
+    """The 8 corners (bit k of the index: + side of axis k) and 6 faces
+    (+x, -x, +y, -y, +z, -z) of a box in its frame, as _polygon_faces."""
+    corners = np.array([[size[0] if i & 1 else -size[0], size[1] if i & 2 else -size[1],
+                         size[2] if i & 4 else -size[2]] for i in range(8)], dtype=np.float64)
+    faces = []
+    for ax in range(3):
+        for sg in (1, -1):
+            n = np.zeros(3)
+            n[ax] = sg
+            vs = [i for i in range(8) if ((i >> ax) & 1) == (sg > 0)]
+            P = corners[vs]
+            u = np.zeros(3)
+            u[(ax + 1) % 3] = 1.0
+            w = np.cross(n, u)
+            ang = np.arctan2(P @ w, P @ u)
+            order = [vs[k] for k in np.argsort(ang, kind="stable")]
+            faces.append((n, float(size[ax]), order, order))
+    return corners, faces
 
 
 def _convex_hulls(m, geoms, pairs, meshes):
@@ -997,8 +1078,20 @@ def _convex_hulls(m, geoms, pairs, meshes):
     ng = len(geoms)
     m.geom_hulladr = -np.ones(ng, dtype=np.int64)
     m.geom_hullnum = np.zeros(ng, dtype=np.int64)
+    # polygon faces (the polyhedron contact manifold, mesh-mesh / box-mesh
+    # pairs): per mesh hull and per box that meets a mesh; a box's 8 corners
+    # go after the hull vertices (geom_cornadr), outside every climb graph
+    m.geom_faceadr = -np.ones(ng, dtype=np.int64)
+    m.geom_facenum = np.zeros(ng, dtype=np.int64)
+    m.geom_cornadr = -np.ones(ng, dtype=np.int64)
     used = {p["g1"] for p in pairs} | {p["g2"] for p in pairs}
+    poly = set()
+    for p in pairs:
+        t1, t2 = geoms[p["g1"]]["type"], geoms[p["g2"]]["type"]
+        if {t1, t2} <= {6, 7} and 7 in (t1, t2):
+            poly |= {p["g1"], p["g2"]}
     cache, verts, adjadr, adjnum, adj = {}, [], [], [], []
+    faces = []  # (normal, offset, all global vertices, kept global vertices)
     for gi in sorted(used):
         g = geoms[gi]
         if g["type"] != 7:
@@ -1006,25 +1099,58 @@ def _convex_hulls(m, geoms, pairs, meshes):
         if g["mesh"] not in cache:
             mpath, scale = meshes[g["mesh"]]
             tris = load_stl(mpath) if mpath.lower().endswith(".stl") else load_obj(mpath)
-            hv, c, nbr = convex_hull(tris.reshape(-1, 3) * scale[None, :])
+            hv, c, nbr, fcs = convex_hull(tris.reshape(-1, 3) * scale[None, :])
             base = len(verts)
             for k, n in enumerate(nbr):
                 adjadr.append(len(adj))
                 adjnum.append(len(n))
                 adj.extend(base + x for x in n)
             verts.extend(hv.tolist())
-            cache[g["mesh"]] = (base, len(hv), c, float(np.max(np.linalg.norm(hv, axis=1))))
-        base, num, c, rb = cache[g["mesh"]]
+            fbase = len(faces)
+            faces.extend((n, off, [base + x for x in al], [base + x for x in kp]) for n, off, al, kp in fcs)
+            cache[g["mesh"]] = (base, len(hv), c, float(np.max(np.linalg.norm(hv, axis=1))), fbase, len(fcs))
+        base, num, c, rb, fbase, nf = cache[g["mesh"]]
         m.geom_hulladr[gi] = base
         m.geom_hullnum[gi] = num
         m.geom_pos[gi] = m.geom_pos[gi] + quat2mat(m.geom_quat[gi]) @ c
         m.geom_rbound[gi] = rb
+        if gi in poly:
+            m.geom_faceadr[gi], m.geom_facenum[gi] = fbase, nf
+    nmesh_verts = len(verts)
+    for gi in sorted(poly):
+        if geoms[gi]["type"] != 6:
+            continue
+        corners, fcs = box_faces(np.asarray(m.geom_size[gi], dtype=np.float64))
+        base = len(verts)
+        verts.extend(corners.tolist())
+        adjadr.extend([len(adj)] * 8)
+        adjnum.extend([0] * 8)
+        m.geom_cornadr[gi] = base
+        m.geom_faceadr[gi], m.geom_facenum[gi] = len(faces), len(fcs)
+        faces.extend((n, off, [base + x for x in al], [base + x for x in kp]) for n, off, al, kp in fcs)
     m.nhullv = len(verts)
     m.nhulla = len(adj)
     m.hull_vert = np.array(verts, dtype=np.float64).reshape(-1, 3)
     m.hull_adjadr = np.array(adjadr, dtype=np.int64)
     m.hull_adjnum = np.array(adjnum, dtype=np.int64)
     m.hull_adj = np.array(adj, dtype=np.int64)
+    # faces: plane (n, offset: n . x = offset on the face) and kept polygon;
+    # per vertex the faces it belongs to (every vertex of a face, kept or not)
+    m.nface = len(faces)
+    m.face_plane = np.array([list(f[0]) + [f[1]] for f in faces], dtype=np.float64).reshape(-1, 4)
+    m.face_vadr = np.cumsum([0] + [len(f[3]) for f in faces[:-1]]).astype(np.int64) if faces else np.zeros(0, np.int64)
+    m.face_vnum = np.array([len(f[3]) for f in faces], dtype=np.int64)
+    m.face_vert = np.array([v for f in faces for v in f[3]], dtype=np.int64)
+    m.nfacev = int(m.face_vert.size)
+    inc = [[] for _ in range(len(verts))]
+    for fi, f in enumerate(faces):
+        for v in f[2]:
+            inc[v].append(fi)
+    m.vert_faceadr = np.cumsum([0] + [len(x) for x in inc[:-1]]).astype(np.int64) if inc else np.zeros(0, np.int64)
+    m.vert_facenum = np.array([len(x) for x in inc], dtype=np.int64)
+    m.vert_face = np.array([f for x in inc for f in x], dtype=np.int64)
+    m.nvface = int(m.vert_face.size)
+    del nmesh_verts
 
 
 def _actuators(m, root, defaults, jnt, jnames, autolimits):

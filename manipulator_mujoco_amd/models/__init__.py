@@ -42,7 +42,7 @@ PLANNER_SCENES = ("planner_scene", "ur5e_hande_mjx", "scene_mjx", "dual_arm")
 _SCALARS = ("nbody", "njnt", "nq", "nv", "ngeom", "nsite", "npair", "neq", "ncon", "nslot", "nctrl",
             "hande_body", "tcp_site", "iterations", "ls_iterations", "disableflags", "ntree", "timestep",
             "tolerance", "ls_tolerance", "impratio", "meaninertia", "nu", "nhullv", "nhulla", "integrator",
-            "cone", "nten", "viscosity", "density")
+            "cone", "nten", "viscosity", "density", "nface", "nfacev", "nvface")
 
 
 def save_bundle(m, path):

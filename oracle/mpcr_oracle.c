@@ -1269,10 +1269,15 @@ static int mpr_impl(const mpcr_model_t* m, const odata* d, int g1, int g2, doubl
   }
 }
 
+static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int g2, const double n[3], double depth,
+                         ocontact* out);
 static void col_convex(const mpcr_model_t* m, odata* d, int pair, int g1, int g2, ocontact* out) {
   double depth, n[3], pos[3];
   if (!mpr(m, d, g1, g2, &depth, n, pos, d->hint[pair])) return;
   if (n[0] == 0 && n[1] == 0 && n[2] == 0) n[2] = 1; /* touching: any frame */
+  /* polyhedron pairs: the face-clipping manifold when a face axis carries
+     the contact, else MPR's single point */
+  if (m->pair_ncon[pair] == 4 && depth > 0 && poly_manifold(m, d, pair, g1, g2, n, depth, out)) return;
   set_contact(out, -depth, pos, n);
 }
 
@@ -1379,9 +1384,252 @@ static void col_plane_mesh(const mpcr_model_t* m, odata* d, int pair, int gp, in
 #undef SUP
 }
 
+/* ---- polyhedron pairs (mesh-mesh, box-mesh): face-clipping manifold ------
+   Restates mujoco-mjx 3.3.1 collision_convex.py convex_convex (MJX is the
+   reference's rollout engine, SBP/mjx_planner.py:108,256): the separating
+   axis of least penetration among face normals picks a reference face, the
+   other geom's most anti-parallel face is clipped by the reference face's
+   side planes, the clipped points below the reference plane are the
+   contacts (normal = the reference face's, position half-way through the
+   penetration), at most 4 of them by _manifold_points' picks.  Where MJX
+   scans every face (and edge pair) of both hulls, the axis search here is
+   seeded by MPR's normal n (g1 -> g2): the candidate axes are the faces on
+   the support vertex of g1 along n and of g2 along -n (MPR's direction
+   lies in those vertices' normal cones).  An edge contact -- no candidate
+   face within 5 % of MPR's depth -- keeps MPR's single point.  Parity vs
+   MJX unpinned (DESIGN.md §Dual-arm class). */
+
+/* world outward normal and offset (n . x = off) of face f of geom g */
+static void face_world(const mpcr_model_t* m, const odata* d, int g, int f, double nw[3], double* off) {
+  const double* R = d->geom_xmat[g];
+  mulmv(nw, R, m->face_plane[f]);
+  *off = m->face_plane[f][3] + dot3(nw, d->geom_xpos[g]);
+}
+
+/* hull vertex index of geom g's support point along dir (world): the mesh
+   climb from *hint (updated), or the box corner (an exactly zero component
+   takes the + side) */
+static int support_vertex(const mpcr_model_t* m, const odata* d, int g, const double dir[3], int* hint) {
+  if (m->geom_type[g] == MPCR_GEOM_BOX) {
+    double l[3];
+    mulmtv(l, d->geom_xmat[g], dir);
+    return m->geom_cornadr[g] + (l[0] >= 0 ? 1 : 0) + (l[1] >= 0 ? 2 : 0) + (l[2] >= 0 ? 4 : 0);
+  }
+  double p[3];
+  support(m, d, g, dir, p, hint);
+  return *hint;
+}
+
+static void vert_world(const mpcr_model_t* m, const odata* d, int g, int v, double w[3]) {
+  mulmv(w, d->geom_xmat[g], m->hull_vert[v]);
+  for (int k = 0; k < 3; k++) w[k] += d->geom_xpos[g][k];
+}
+
+/* support value of geom g along dir (world, unit): max over its vertices of dir . x */
+static double support_value(const mpcr_model_t* m, const odata* d, int g, const double dir[3], int* hint) {
+  double p[3];
+  support(m, d, g, dir, p, hint);
+  return dot3(p, dir);
+}
+
+static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int g2, const double n[3], double depth,
+                         ocontact* out) {
+  /* climbs start from the pair's hints (where MPR's queries ended) and do not
+     update them; every query starts afresh (the kernel runs them on parallel
+     lanes) */
+  const int h0 = d->hint[pair][0], h1 = d->hint[pair][1];
+  int h;
+  const double nn[3] = {-n[0], -n[1], -n[2]};
+  h = h0;
+  const int s1 = support_vertex(m, d, g1, n, &h);
+  h = h1;
+  const int s2 = support_vertex(m, d, g2, nn, &h);
+  /* candidate reference faces (g1's on s1, then g2's on s2; at most 64, the
+     kernel's lanes): SAT separation along each outward face normal, the
+     maximum's first candidate within the tie band (order-free, as a wave) */
+  const int c1 = m->vert_facenum[s1] < 64 ? m->vert_facenum[s1] : 64;
+  const int c2 = m->vert_facenum[s2] < 64 - c1 ? m->vert_facenum[s2] : 64 - c1;
+  double sep[64];
+  int fid[64];
+  double mx = -1e300;
+  for (int k = 0; k < c1 + c2; k++) {
+    const int two = k >= c1, g = two ? g2 : g1, go = two ? g1 : g2;
+    const int f = m->vert_face[two ? m->vert_faceadr[s2] + k - c1 : m->vert_faceadr[s1] + k];
+    double nf[3], off, mnf[3];
+    face_world(m, d, g, f, nf, &off);
+    for (int c = 0; c < 3; c++) mnf[c] = -nf[c];
+    h = two ? h0 : h1;
+    sep[k] = -support_value(m, d, go, mnf, &h) - off; /* min over go of nf . x, minus the plane */
+    fid[k] = f;
+    if (sep[k] > mx) mx = sep[k];
+  }
+  int kb = -1;
+  for (int k = 0; k < c1 + c2 && kb < 0; k++)
+    if (near_max(sep[k], mx)) kb = k;
+  if (kb < 0 || -sep[kb] > 1.05 * depth + 1e-5) return 0; /* an edge axis carries the contact */
+  const int best_f = fid[kb], gr = kb >= c1 ? g2 : g1, gi = kb >= c1 ? g1 : g2;
+  double nr[3], offr;
+  face_world(m, d, gr, best_f, nr, &offr);
+  /* incident face: the most anti-parallel face on gi's support vertex along -nr */
+  const double mnr[3] = {-nr[0], -nr[1], -nr[2]};
+  h = gi == g1 ? h0 : h1;
+  const int si = support_vertex(m, d, gi, mnr, &h);
+  const int ci = m->vert_facenum[si] < 64 ? m->vert_facenum[si] : 64;
+  double al[64];
+  mx = -1e300;
+  for (int k = 0; k < ci; k++) {
+    double nf[3], off;
+    face_world(m, d, gi, m->vert_face[m->vert_faceadr[si] + k], nf, &off);
+    al[k] = -dot3(nf, nr);
+    if (al[k] > mx) mx = al[k];
+  }
+  int inc_f = -1;
+  for (int k = 0; k < ci && inc_f < 0; k++)
+    if (near_max(al[k], mx)) inc_f = m->vert_face[m->vert_faceadr[si] + k];
+  if (inc_f < 0) return 0;
+  /* clip the incident polygon by the reference face's side planes */
+  enum { MAXP = 2 * MPCR_FACE_MAXV + 2 };
+  double poly[2][MAXP][3], ref[MPCR_FACE_MAXV][3];
+  int np = m->face_vnum[inc_f], cur = 0;
+  const int nrv = m->face_vnum[best_f];
+  for (int k = 0; k < np; k++) vert_world(m, d, gi, m->face_vert[m->face_vadr[inc_f] + k], poly[0][k]);
+  for (int k = 0; k < nrv; k++) vert_world(m, d, gr, m->face_vert[m->face_vadr[best_f] + k], ref[k]);
+  for (int e = 0; e < nrv && np > 0; e++) {
+    const double* A = ref[e];
+    const double* B = ref[e + 1 == nrv ? 0 : e + 1];
+    double ed[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, sn[3];
+    cross3(sn, ed, nr); /* outward side-plane normal (counter-clockwise polygon about nr) */
+    int no = 0;
+    for (int k = 0; k < np; k++) {
+      const double* P = poly[cur][k];
+      const double* Q = poly[cur][k + 1 == np ? 0 : k + 1];
+      const double dp = sn[0] * (P[0] - A[0]) + sn[1] * (P[1] - A[1]) + sn[2] * (P[2] - A[2]);
+      const double dq = sn[0] * (Q[0] - A[0]) + sn[1] * (Q[1] - A[1]) + sn[2] * (Q[2] - A[2]);
+      if (dp <= 0 && no < MAXP) memcpy(poly[cur ^ 1][no++], P, sizeof(double) * 3);
+      if (((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) && no < MAXP) {
+        const double w = dp / (dp - dq);
+        for (int c = 0; c < 3; c++) poly[cur ^ 1][no][c] = P[c] + w * (Q[c] - P[c]);
+        no++;
+      }
+    }
+    np = no;
+    cur ^= 1;
+  }
+  /* the clipped points below the reference plane */
+  double pts[MAXP][3], dist[MAXP];
+  int nk = 0;
+  const double margin = m->pair_margin[pair] - m->pair_gap[pair];
+  for (int k = 0; k < np; k++) {
+    const double dk = dot3(nr, poly[cur][k]) - offr;
+    if (dk < margin) { memcpy(pts[nk], poly[cur][k], sizeof(double) * 3); dist[nk++] = dk; }
+  }
+  if (nk == 0) return 0;
+  /* at most 4: _manifold_points' picks (a = the first, b = the farthest from
+     a, c = the farthest from line ab, d = the farthest from edge bc or ac;
+     near_max's first index within the tie band) */
+  int idx[4] = {0, 0, 0, 0}, cnt = nk < 4 ? nk : 4;
+  if (nk <= 4) {
+    for (int k = 0; k < nk; k++) idx[k] = k;
+  } else {
+    const double* a = pts[0];
+    double mx, v;
+#define PICK(EXPR, OUT)                                            \
+    do {                                                           \
+      mx = -1;                                                     \
+      for (int k = 0; k < nk; k++) { const double* p = pts[k]; v = (EXPR); if (v > mx) mx = v; } \
+      for (int k = 0; k < nk; k++) { const double* p = pts[k]; if (near_max((EXPR), mx)) { OUT = k; break; } } \
+    } while (0)
+    double best_bp, best_ap;
+    PICK((a[0] - p[0]) * (a[0] - p[0]) + (a[1] - p[1]) * (a[1] - p[1]) + (a[2] - p[2]) * (a[2] - p[2]), idx[1]);
+    const double* b = pts[idx[1]];
+    double amb[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]}, ab[3];
+    cross3(ab, nr, amb);
+    PICK(fabs((a[0] - p[0]) * ab[0] + (a[1] - p[1]) * ab[1] + (a[2] - p[2]) * ab[2]), idx[2]);
+    const double* c = pts[idx[2]];
+    double amc[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]}, bmc[3] = {b[0] - c[0], b[1] - c[1], b[2] - c[2]};
+    double ac[3], bc[3];
+    cross3(ac, nr, amc);
+    cross3(bc, nr, bmc);
+    int ibp = 0, iap = 0;
+    PICK(fabs((b[0] - p[0]) * bc[0] + (b[1] - p[1]) * bc[1] + (b[2] - p[2]) * bc[2]), ibp);
+    best_bp = mx;
+    PICK(fabs((a[0] - p[0]) * ac[0] + (a[1] - p[1]) * ac[1] + (a[2] - p[2]) * ac[2]), iap);
+    best_ap = mx;
+#undef PICK
+    idx[3] = beats(best_ap, best_bp) ? iap : ibp;
+  }
+  const double sg = gr == g1 ? 1.0 : -1.0; /* contact normal g1 -> g2 */
+  const double cn[3] = {sg * nr[0], sg * nr[1], sg * nr[2]};
+  for (int s = 0; s < cnt; s++) {
+    int dup = 0;
+    for (int t = 0; t < s; t++) dup |= idx[t] == idx[s];
+    if (dup) continue;
+    const int k = idx[s];
+    double pos[3];
+    for (int c = 0; c < 3; c++) pos[c] = pts[k][c] - 0.5 * dist[k] * nr[c];
+    set_contact(&out[s], dist[k], pos, cn);
+  }
+  return 1;
+}
+
+/* plane - cylinder (4 slots): MuJoCo's mjc_PlaneCylinder (mujoco 3.3.1
+   engine_collision_primitive.c, restated): slot 0 the deepest rim point of the
+   cap nearer the plane (always reported), then, when it penetrates, the rim
+   point of the other cap on the same side, and two points of the near cap's
+   rim 120 degrees either side of the first (an equilateral triangle with it).
+   Normal = the plane's, positions half-way through the penetration. */
+static void col_plane_cylinder(const mpcr_model_t* m, odata* d, int pair, int gp, int g, ocontact* out) {
+  const double* R1 = d->geom_xmat[gp];
+  const double* R2 = d->geom_xmat[g];
+  const double* sz = m->geom_size[g];
+  const double* x = d->geom_xpos[g];
+  const double n[3] = {R1[2], R1[5], R1[8]};
+  double ax[3] = {R2[2], R2[5], R2[8]}, dif[3], vec[3], pos[3];
+  for (int k = 0; k < 3; k++) dif[k] = x[k] - d->geom_xpos[gp][k];
+  double prjaxis = dot3(n, ax);
+  if (prjaxis > 0) { /* the axis towards the plane */
+    for (int k = 0; k < 3; k++) ax[k] = -ax[k];
+    prjaxis = -prjaxis;
+  }
+  const double dist0 = dot3(dif, n);
+  for (int k = 0; k < 3; k++) vec[k] = ax[k] * prjaxis - n[k]; /* radial direction towards the plane */
+  const double len = norm3(vec);
+  if (len < MINVAL) { vec[0] = R2[0]; vec[1] = R2[3]; vec[2] = R2[6]; }
+  else for (int k = 0; k < 3; k++) vec[k] /= len;
+  for (int k = 0; k < 3; k++) { vec[k] *= sz[0]; ax[k] *= sz[1]; }
+  const double prjvec = dot3(vec, n);
+  prjaxis *= sz[1];
+  const double margin = m->pair_margin[pair] - m->pair_gap[pair];
+  double dist = dist0 + prjaxis + prjvec;
+  for (int k = 0; k < 3; k++) pos[k] = x[k] + vec[k] + ax[k] - 0.5 * dist * n[k];
+  set_contact(&out[0], dist, pos, n);
+  if (!(dist <= margin)) return;
+  dist = dist0 - prjaxis + prjvec;
+  if (dist <= margin) {
+    for (int k = 0; k < 3; k++) pos[k] = x[k] + vec[k] - ax[k] - 0.5 * dist * n[k];
+    set_contact(&out[1], dist, pos, n);
+  }
+  dist = dist0 + prjaxis - 0.5 * prjvec;
+  if (dist <= margin) {
+    double v1[3];
+    cross3(v1, vec, ax);
+    normalize3(v1);
+    for (int k = 0; k < 3; k++) v1[k] *= sz[0] * sqrt(3.0) / 2;
+    for (int sgn = 0; sgn < 2; sgn++) {
+      const double sv = sgn ? -1.0 : 1.0;
+      for (int k = 0; k < 3; k++) pos[k] = x[k] + sv * v1[k] + ax[k] - 0.5 * vec[k] - 0.5 * dist * n[k];
+      set_contact(&out[2 + sgn], dist, pos, n);
+    }
+  }
+}
+
 static void col_plane_convex(const mpcr_model_t* m, odata* d, int pair, int gp, int g, ocontact* out) {
   if (m->geom_type[g] == MPCR_GEOM_MESH) {
     col_plane_mesh(m, d, pair, gp, g, out);
+    return;
+  }
+  if (m->geom_type[g] == MPCR_GEOM_CYLINDER && m->pair_ncon[pair] == 4) {
+    col_plane_cylinder(m, d, pair, gp, g, out);
     return;
   }
   const double* R = d->geom_xmat[gp];

@@ -43,7 +43,11 @@ def test_hull_graphs(dual):
     m = dual
     rng = np.random.default_rng(0)
     adj = [set(m.hull_adj[m.hull_adjadr[v]:m.hull_adjadr[v] + m.hull_adjnum[v]].tolist()) for v in range(m.nhullv)]
+    corners = {int(c) + k for c in m.geom_cornadr if c >= 0 for k in range(8)}  # box corners: faces only
     for v, nb in enumerate(adj):
+        if v in corners:
+            assert not nb
+            continue
         assert len(nb) >= 3 and v not in nb
         for u in nb:
             assert v in adj[u]
@@ -238,3 +242,105 @@ def test_ctrl_zero_servos_pull_arm1_home(dual):
     free.nu = 0
     q, v = run(free)
     assert v[0] > 0.8 * cmd[0]  # (the other joints then sag under gravity: no gravcomp here)
+
+
+def test_polyhedron_faces(dual):
+    """The faces of the polyhedron-pair hulls / boxes (model v7): unit outward
+    normals, every kept vertex on its face plane, counter-clockwise about the
+    normal, the hull inside every face plane, each vertex listed by its faces."""
+    m = dual
+    assert m.nface > 0
+    for g in np.where(m.geom_faceadr >= 0)[0]:
+        f0, nf = m.geom_faceadr[g], m.geom_facenum[g]
+        if m.geom_type[g] == 7:
+            V = m.hull_vert[m.geom_hulladr[g]:m.geom_hulladr[g] + m.geom_hullnum[g]]
+        else:
+            V = m.hull_vert[m.geom_cornadr[g]:m.geom_cornadr[g] + 8]
+        for f in range(f0, f0 + nf):
+            n, off = m.face_plane[f, :3], m.face_plane[f, 3]
+            assert abs(np.linalg.norm(n) - 1) < 1e-9
+            assert (V @ n).max() <= off + 1e-6 * max(1.0, abs(off))  # the hull lies inside
+            P = m.hull_vert[m.face_vert[m.face_vadr[f]:m.face_vadr[f] + m.face_vnum[f]]]
+            assert 3 <= len(P) <= 16
+            assert np.abs(P @ n - off).max() < 1e-5
+            c = P.mean(axis=0)
+            area = sum(np.cross(P[k] - c, P[(k + 1) % len(P)] - c) @ n for k in range(len(P)))
+            assert area > 0  # counter-clockwise
+            for v in m.face_vert[m.face_vadr[f]:m.face_vadr[f] + m.face_vnum[f]]:
+                assert f in m.vert_face[m.vert_faceadr[v]:m.vert_faceadr[v] + m.vert_facenum[v]]
+
+
+def _active(m, qpos=None):
+    r = oracle.step_debug(m, m.qpos_init[:m.nq].copy() if qpos is None else qpos, np.zeros(m.nv), np.zeros(m.nv))
+    names = m.names["geom"]
+    out = {}
+    for k in range(r["ncon"]):
+        p = r["con_pair"][k]
+        key = (names[m.pair_geom1[p]], names[m.pair_geom2[p]])
+        out.setdefault(key, []).append((r["con_dist"][k], r["con_pos"][k], r["con_normal"][k]))
+    return out
+
+
+def test_poly_manifold_cube_flat_on_box(tmp_path):
+    """A mesh cube resting flat 15 mm deep in a box table: the polyhedron
+    manifold (mjx convex_convex restated: reference face, clipped incident
+    face, 4 picks) puts one contact under each bottom corner, all at the same
+    depth, normal along z, half-way through the penetration."""
+    m = _scene(tmp_path, """
+    <body name="k" pos="0.3 0 0.03"><freejoint/><geom name="k" type="mesh" mesh="cube"/></body>
+    <body name="t" pos="0.3 0 -0.015"><geom name="t" type="box" size="0.2 0.2 0.01"/></body>""")
+    c = _active(m)
+    key = ("t", "k") if ("t", "k") in c else ("k", "t")
+    cs = c[key]
+    assert len(cs) == 4
+    for dist, pos, n in cs:
+        assert abs(dist + 0.015) < 1e-9
+        assert abs(abs(n[2]) - 1) < 1e-12
+        assert abs(pos[2] - (-0.02 + 0.0075)) < 1e-9  # half-way between the cube bottom and the table top
+    xy = sorted((round(p[0] - 0.3, 6), round(p[1], 6)) for _, p, _ in cs)
+    assert xy == [(-0.05, -0.05), (-0.05, 0.05), (0.05, -0.05), (0.05, 0.05)]
+
+
+def test_poly_manifold_clips_to_the_smaller_face(tmp_path):
+    """Two mesh cubes, the upper one shifted by half a side: the contact
+    polygon is the overlap of the faces (clipped), 4 corners of the 5 cm x
+    10 cm overlap region; a cube tilted by 45 degrees onto its edge: the
+    lower cube's top face is the reference, the edge's two ends the
+    contacts."""
+    m = _scene(tmp_path, """
+    <body name="a" pos="0 0 0"><freejoint/><geom name="a" type="mesh" mesh="cube"/></body>
+    <body name="b" pos="0.05 0 0.098"><freejoint/><geom name="b" type="mesh" mesh="cube"/></body>
+    <body name="e" pos="1 0 0"><freejoint/><geom name="e" type="mesh" mesh="cube"/></body>
+    <body name="f" pos="1 0 0.1157" euler="0.7853981633974483 0 0"><freejoint/><geom name="f" type="mesh" mesh="cube"/></body>""")
+    c = _active(m)
+    ab = c.get(("a", "b")) or c.get(("b", "a"))
+    assert len(ab) == 4
+    xs = sorted(round(p[0], 6) for _, p, _ in ab)
+    ys = sorted(round(p[1], 6) for _, p, _ in ab)
+    assert xs == [0.0, 0.0, 0.05, 0.05] and ys == [-0.05, -0.05, 0.05, 0.05]
+    for dist, _, n in ab:
+        assert abs(dist + 0.002) < 1e-8 and abs(abs(n[2]) - 1) < 1e-12  # (fp32 STL vertices)
+    ef = c.get(("e", "f")) or c.get(("f", "e"))
+    assert ef is not None and len(ef) == 2
+    depth = 0.05 * np.sqrt(2) - (0.1157 - 0.05)
+    assert sorted(round(p[0], 6) for _, p, _ in ef) == [0.95, 1.05]
+    for dist, _, n in ef:
+        assert abs(dist + depth) < 1e-8 and abs(abs(n[2]) - 1) < 1e-12
+
+
+def test_plane_cylinder_four_points(tmp_path):
+    """Plane-cylinder (MuJoCo's mjc_PlaneCylinder restated): an upright
+    cylinder 3 mm into the floor gets the deepest rim point, the two rim points
+    120 degrees either side of it (all three at the same depth, an equilateral
+    triangle on the bottom cap); its top cap stays clear."""
+    m = _scene(tmp_path, """
+    <body name="y" pos="0 0 0.097"><freejoint/><geom name="y" type="cylinder" size="0.05 0.1"/></body>""")
+    c = _active(m)
+    cs = c.get(("floor", "y")) or c.get(("y", "floor"))
+    assert len(cs) == 3
+    for dist, pos, n in cs:
+        assert abs(dist + 0.003) < 1e-9 and abs(n[2] - 1) < 1e-12
+        assert abs(np.hypot(pos[0], pos[1]) - 0.05) < 1e-9
+    ang = sorted(np.degrees(np.arctan2(p[1], p[0])) % 360 for _, p, _ in cs)
+    gaps = np.diff(ang + [ang[0] + 360])
+    assert np.allclose(gaps, 120, atol=1e-6)

@@ -300,7 +300,7 @@ def test_dual_arm_c4_properties(torch_cuda):
     assert rows_per_step.min() >= 8  # 8 equality rows + the linkage contacts
     # the whole shard against the oracle: conditioning bar and the selection
     o, sens = pu.conditioning(m, _td(Pd, xi.cpu().numpy(), H), seed=7)
-    assert int(o["maxcon"].max()) <= 32 and int(o["maxrows"].max()) <= 8 + 4 * 32  # the wide image's caps
+    assert int(o["maxcon"].max()) <= 40 and int(o["maxrows"].max()) <= 8 + 4 * 40  # the wide image's caps
     # the whole bar, well-conditioned candidates included
     a4 = a.cpu().numpy()
     st_ = pu.check(m, a4[:, 0], o, sens, "C4 shard")
