@@ -55,12 +55,15 @@ CONFIGS = {
 }
 
 
-def flops_per_step(m, nefc_mean):
+def flops_per_step(m, nefc_mean, model_name=None):
     fm = json.load(open(os.path.join(ROOT, "bench", "flops_model.json")))
     nb_moving = int(sum(1 for b in range(1, m.nbody) if m.body_weldid[b] != 0))
-    names = {0: "plane_capsule", 1: "plane_box", 2: "capsule_capsule", 3: "capsule_box", 4: "box_box", 9: "convex",
+    names = {0: "plane_capsule", 1: "plane_box", 2: "capsule_capsule", 3: "capsule_box", 4: "box_box", 9: "convex_cull",
              10: "plane_convex"}
     coll = sum(fm["collision_per_pair"][names[int(f)]] for f in m.pair_func)
+    ex = fm["convex_executed_per_step"].get(model_name) if model_name else None
+    if ex:  # executed MPR solves and polyhedron manifolds only (culled pairs are not credited)
+        coll += ex["mpr_calls"] * fm["collision_per_pair"]["convex"] + ex["hits"] * fm["poly_manifold_per_hit"]
     sp = fm["solve_per_row"]
     nv = m.nv
     solve = fm["solve_base"] + nefc_mean * (sp["row_setup"] + sp["jacobian_per_dof"] * nv
@@ -339,7 +342,7 @@ def main():
 
     if rank == 0:
         value = n_total * args.steps / elapsed
-        fps = flops_per_step(m, nefc_mean)  # mean constraint rows/step measured by the kernel
+        fps = flops_per_step(m, nefc_mean, args.model)  # mean constraint rows/step measured by the kernel
         flops_launch = fps * H * n
         achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
         hbm_launch = n * (66 * 4 + 16 + 2 * 6 * H * 4 + 4)  # xi in; cost4, theta, thetadot, status out

@@ -6,7 +6,8 @@
  * function returns 0 on success or a negative MPCR_E* code; the message of
  * the last failure on the calling thread is available from
  * mpcr_last_error().  Engines are independent (one per host thread / stream);
- * there is no global mutable state besides the thread-local error string.
+ * there is no global mutable state besides the thread-local error string and
+ * the process-wide two-wave batch threshold (mpcr_set_two_wave_max_n).
  *
  * Reference interface each entry point replaces (file:line in
  * /root/reference/sampling_based_planner/):
@@ -126,6 +127,12 @@ int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, con
    VGPRs of the two rollout kernel variants on `device`:
    info[6] = narrow (blocks, lds, vgprs), dual-arm class (blocks, lds, vgprs). */
 int mpcr_rollout_occupancy(int device, int* info);
+/* Narrow-variant batches of at most n candidates run two waves per candidate
+   (the collision phase beside the dynamics; bitwise the one-wave results).
+   n < 0 only queries.  Returns the previous threshold (default: the build's
+   MPCR_WPC2_MAX_N_DEFAULT, or the MPCR_WPC2_MAX_N environment variable).
+   Process-wide: set it before launches, not while one is in flight. */
+int mpcr_set_two_wave_max_n(int n);
 
 /* Same as mpcr_rollout_cost with MPCR_F_DEVICE_PTRS, except that the
    per-call arguments are a device block read when the kernel runs:

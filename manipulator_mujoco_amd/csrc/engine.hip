@@ -950,6 +950,8 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   return MPCR_OK;
 }
 
+extern "C" int mpcr_set_two_wave_max_n(int n) { return rollout_set_wpc2_max_n(n); }
+
 extern "C" int mpcr_rollout_occupancy(int device, int* info) {
   if (!info) return fail(MPCR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(device));

@@ -78,8 +78,13 @@ struct RolloutArgs {
 // multiples of 4 for LD = 20 and 36) -> conflict free, 4x fewer LDS
 // instructions than b32.
 template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false,
-          int JL_ = MAXEFC_, int CPW_ = 1, int MAXACT_ = DX_MAXACT>
+          int JL_ = MAXEFC_, int CPW_ = 1, int MAXACT_ = DX_MAXACT, bool SPLIT_ = false>
 struct __align__(16) SmemT {
+  // SPLIT: the dynamics scratch and the contact / constraint arrays do not
+  // overlay (the two-wave variant runs the dynamics and the collision phase
+  // at the same time)
+  static constexpr bool SPLIT = SPLIT_;
+  static constexpr int DYN_FLOATS = NBW_ * 64 + NVW_ * 16;  // xpos .. fvec below
   static constexpr int NVW = NVW_, NBW = NBW_, NGW = NGW_, LD = NVW_ + 4;
   // candidates per wave: CPW images per workgroup, HL = 64 / CPW lanes each
   static constexpr int CPW = CPW_, HL = WAVE / CPW_;
@@ -94,6 +99,7 @@ struct __align__(16) SmemT {
   static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
   static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
   static constexpr int PMAXW = 2 * MPCR_FACE_MAXV + 2;  // clipped incident face: <= its vertices + one per side plane
+  static constexpr int FRAMEW = WIDE ? 3 : 9;  // contact frame entries kept (the wide image recomputes the tangents)
   // ---- persistent across the step ----
   float qpos[NQW];
   alignas(16) float qvel[NVW];
@@ -132,6 +138,7 @@ struct __align__(16) SmemT {
       float fvec[NVW][8];
     };
     struct {
+      float split_pad_[SPLIT_ ? DYN_FLOATS : 0];  // SPLIT: past the dynamics scratch
       union {
         alignas(16) float J[JL][LDJ];  // constraint rows .. Newton
         struct {                        // collision:
@@ -145,7 +152,7 @@ struct __align__(16) SmemT {
       union {
         struct {  // collision .. constraint rows
           float con_pos[MAXACT][4];
-          float con_frame[MAXACT][12];
+          float con_frame[MAXACT][FRAMEW == 3 ? 4 : 12];  // rows n, t1, t2 (the wide image: n only)
           float con_dist[MAXACT];
           int con_pair[MAXACT];
           int con_row[MAXACT];
@@ -191,6 +198,11 @@ using SmemN = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, 
 #if !defined(MPCR_N_LDS_UNCHECKED)
 static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU (see above)");
 #endif
+// The two-wave narrow image (small batches, rollout_kernel<..., 2>): dynamics
+// scratch and contacts side by side, every J row in LDS (no HBM slab) -- at
+// most 2048 candidates = 8 blocks per CU, so LDS is not the limit
+using SmemN2 = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, MPCR_N_MAXEFC, 1, DX_MAXACT, true>;
+static_assert(sizeof(SmemN2) <= 152448 / 8, "two-wave narrow image: 8 blocks per CU");
 // Dual-arm image: J rows past 40 in the HBM slab, cost history and hull-climb
 // hints in HBM (the class has no robot-masked slots), the convex-pair list
 // inside the J rows, 6-float cdof rows, the mass matrix in an HBM slab:
@@ -201,7 +213,7 @@ static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU
 #define MPCR_W_JL 40
 #endif
 #ifndef MPCR_W_MAXACT
-#define MPCR_W_MAXACT 40  // the polyhedron manifold's 4 contacts per face pair: <= 39 in a 1024 x 100 C4 batch
+#define MPCR_W_MAXACT 48  // the polyhedron manifold's 4 contacts per face pair (40 truncated 0.5 % of a C4 shard)
 #endif
 using SmemW = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT>;
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD + SmemN::NVW, "Hessian + J^T f scratch");
@@ -220,5 +232,6 @@ void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigne
                     hipStream_t st);
 // resident blocks per CU, static LDS bytes, VGPRs: narrow (0..2), wide (3..5)
 hipError_t rollout_occupancy(int* info, size_t dyn_lds);
+int rollout_set_wpc2_max_n(int n);  // two waves per candidate up to n (narrow variant); returns the previous
 
 }  // namespace mpcr

@@ -14,6 +14,8 @@
 //   rollout / output timing  SBP/mjx_planner.py:251-274
 //   cost                     SBP/mjx_planner.py:276-303
 //   mjx.step                 mujoco-mjx 3.3.1 (third party)
+#include <cstdlib>
+
 #include "rollout.h"
 #include "../../include/mpcr_model.h"  // MPCR_LUT_R (the hull start table layout)
 
@@ -89,6 +91,9 @@ namespace mpcr {
 #ifndef MPCR_ABL_FUNC
 #define MPCR_ABL_FUNC 0
 #endif
+#ifndef MPCR_WPC2_MAX_N_DEFAULT
+#define MPCR_WPC2_MAX_N_DEFAULT 0  // batches up to this size run two waves per candidate (narrow variant)
+#endif
 #ifndef MPCR_TD_TABLE
 #define MPCR_TD_TABLE 1
 #endif
@@ -144,9 +149,17 @@ __device__ __forceinline__ int wscan_excl(int v, int& total) {
   total = tot;
   return pre;
 }
-__device__ __forceinline__ void sync() { __syncthreads(); }
-// (a wave-scope fence pair + wave barrier instead -- the workgroup is one
-// wave -- measured the same: 1.963 vs 1.964 ms on C3)
+// Phase barrier of one candidate's wave: orders its lanes' LDS / global
+// accesses (the workgroup-scope fences of __syncthreads, without s_barrier).
+// A one-wave workgroup measured the same with either (1.963 vs 1.964 ms on C3);
+// the two-wave variant (WPC = 2) needs the wave-local form, its waves meet at
+// block_sync() only.
+__device__ __forceinline__ void sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void block_sync() { __syncthreads(); }
 
 // Candidate groups: a wave may carry CPW candidates of HL = 64 / CPW lanes
 // (lanes [32 h, 32 h + 32) for candidate h when CPW = 2).  These are the
@@ -1753,7 +1766,7 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
 #pragma unroll
       for (int c = 0; c < 3; c++) s.con_pos[base][c] = 0.5f * (pa[c] + sc * da[c] + pb[c] + uc * db[c]);
 #pragma unroll
-      for (int e = 0; e < 9; e++) s.con_frame[base][e] = f[e];
+      for (int e = 0; e < S::FRAMEW; e++) s.con_frame[base][e] = f[e];
       s.con_dist[base] = best_edge;
       s.con_pair[base] = p;
     }
@@ -1894,7 +1907,7 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
 #pragma unroll
     for (int k = 0; k < 3; k++) s.con_pos[o][k] = s.poly[cur][lane][k] + nf[k] * 0.5f * depth;
 #pragma unroll
-    for (int e = 0; e < 9; e++) s.con_frame[o][e] = f[e];
+    for (int e = 0; e < S::FRAMEW; e++) s.con_frame[o][e] = f[e];
     s.con_dist[o] = -depth;
     s.con_pair[o] = p;
   }
@@ -1947,7 +1960,7 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
           make_frame(f, nrm[c]);
           s.con_pos[o][0] = pos[c][0]; s.con_pos[o][1] = pos[c][1]; s.con_pos[o][2] = pos[c][2];
 #pragma unroll
-          for (int e = 0; e < 9; e++) s.con_frame[o][e] = f[e];
+          for (int e = 0; e < S::FRAMEW; e++) s.con_frame[o][e] = f[e];
           s.con_dist[o] = dist[c];
           s.con_pair[o] = p;
         }
@@ -2310,10 +2323,19 @@ __device__ __forceinline__ mfx16 mfma_rows32(const S& s, const float* gx, int ne
   return acc;
 }
 
-template <int NVW, int NBW, int NGW, bool WIDE>
-__global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / SmemN::CPW) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
+// WPC = waves per candidate.  WPC = 2 (narrow variant, small batches: one
+// candidate per SIMD or fewer): wave 1 runs the collision
+// phase while wave 0 runs the dynamics (cinert .. M^-1 qfrc_smooth) -- the two
+// are independent given the step's kinematics -- and meets wave 0 at two
+// workgroup barriers per step (geom poses ready; contacts ready).  Same
+// instructions on the same data as WPC = 1, so the results are bitwise equal.
+template <int NVW, int NBW, int NGW, bool WIDE, int WPC = 1>
+__global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / SmemN::CPW) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
-  using S = typename std::conditional<WIDE, SmemW, SmemN>::type;
+  static_assert(WPC == 1 || (WPC == 2 && !WIDE && SmemN::CPW == 1), "two waves per candidate: narrow, CPW 1");
+  using S = typename std::conditional<WIDE, SmemW, typename std::conditional<WPC == 2, SmemN2, SmemN>::type>::type;
+  const int wv = WPC == 2 ? (int)(threadIdx.x >> 6) : 0;
+  const bool run_main = WPC == 1 || wv == 0, run_coll = WPC == 1 || wv == 1;
   static_assert(S::NVW == NVW && S::NBW == NBW && S::NGW == NGW, "variant widths");
   __shared__ S sm[S::CPW];  // one LDS image per candidate of the wave
   S& s = sm[S::CPW == 1 ? 0 : (int)(threadIdx.x >> 5)];
@@ -2334,8 +2356,9 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
   //      (plant mode: the caller's state, no init_pos override)
-  if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
   const bool from_state = (args.plant & 1) != 0;
+  if (run_main) {  // (WPC = 2: wave 0 sets the image up, wave 1 waits at the barrier below)
+  if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
   if constexpr (S::WIDE) {
     // a rollout starts its hull climbs afresh; the plant keeps them across
     // steps (reset by mpcr_plant_set_state), so k plant steps = a k-step rollout
@@ -2361,6 +2384,8 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   }
   if (lane < nc && !from_state) s.qpos[m->ctrl_qposadr[lane]] = s.par[PAR_Q0 + lane];
   sync();
+  }
+  if constexpr (WPC == 2) block_sync();
 
 #if MPCR_TD_TABLE
   // the candidate's joint velocities for the whole horizon, computed up front
@@ -2370,7 +2395,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   const float* tdp;
   if (args.layout == 0) {
     float* tdw = (args.thetadot && live ? args.thetadot : args.tdscratch) + (size_t)b * nc * H;
-    for (int idx = lane; idx < nc * H; idx += S::HL) {
+    for (int idx = lane; run_main && idx < nc * H; idx += S::HL) {
       const int j = idx / H, tt = idx - j * H;
       const float* pd = args.pdot + (size_t)tt * args.nbasis;
       const float* xj = args.input + ((size_t)bi * nc + j) * args.nbasis;
@@ -2382,6 +2407,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
     }
     __threadfence_block();
     sync();
+    if constexpr (WPC == 2) block_sync();
     tdp = tdw;
   } else {
     tdp = args.input + (size_t)bi * nc * H;
@@ -2406,7 +2432,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   unsigned* pace = nullptr;
   int pace_own = 0;
   unsigned pace_v = ~0u;
-  if ((!WIDE || MPCR_W_PACE) && S::CPW == 1 && args.pace) {
+  if ((!WIDE || MPCR_W_PACE) && S::CPW == 1 && WPC == 1 && args.pace) {
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID[3:0]
     const unsigned grp = ((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) *
@@ -2438,6 +2464,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       if (lane < 16) pace_v = __hip_atomic_load(pace + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #endif
+    if (run_main) {  // ---- wave 0 (WPC = 2): joint velocities .. geom poses, eef
     // ---- qvel[:nctrl] = thetadot_t ----------------------------------------------
 #if MPCR_TD_TABLE
     if (lane < nc) {
@@ -2643,9 +2670,13 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       }
     }
 
+    }  // run_main
+    if constexpr (WPC == 2) block_sync();  // geom poses, tree COMs ready for both waves
+
     STAMP(2);
     STOP_AT(2)
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
+    if (run_main) {  // ---- wave 0: the dynamics (cinert .. M^-1 qfrc_smooth)
     // ---- cinert, cdof (+ actuator forces) -------------------------------------
     if constexpr (S::WIDE) {
       if (lane < m->nu) {
@@ -2997,12 +3028,15 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       if (lane < NVW) s.qas[lane] = lane < nv ? x : 0.f;
     }
 
+    }  // run_main (dynamics)
+
     STAMP(6);
     STOP_AT(6)
 #if MPCR_PACE && MPCR_PACE_AT == 0
     PACE_SETPRIO();
 #endif
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
+    if (run_coll) {  // ---- wave 1 (WPC = 2), concurrently with wave 0's dynamics
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
     //      slots; active contacts compacted into the list; box-box pairs
     //      that pass the bounding-sphere cull are solved wave-cooperatively
@@ -3111,6 +3145,11 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
       sync();
       if (lane == 0) s.ncon = S::MAXACT;
       sync();
+    }
+    }  // run_coll
+    if constexpr (WPC == 2) {
+      block_sync();  // the contact list is ready; wave 1 waits for the next step's geom poses
+      if (!run_main) continue;
     }
 
     STAMP(7);
@@ -3269,7 +3308,14 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
             }
           }
         }
+        // the contact frame (the wide image keeps only its normal row: the
+        // tangents are make_frame's of it, bitwise what emit computed)
+        float fw[9];
         const float* f = s.con_frame[c];
+        if constexpr (S::FRAMEW == 3) {
+          make_frame(fw, s.con_frame[c]);
+          f = fw;
+        }
         const float jn = f[0] * jd[0] + f[1] * jd[1] + f[2] * jd[2];
         const int off = s.con_row[c];
         if (m->pair_condim[p] == 1) {
@@ -3829,7 +3875,7 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 
   STAMP(10);
   PROF_FLUSH
-  if (args.plant && live) {  // single-environment plant: qacc of the last step, state back
+  if (args.plant && live && run_main) {  // single-environment plant: qacc of the last step, state back
     if (lane < nv) args.state[ST_QACC + lane] = s.qacc[lane];
     if (args.plant & 2) {
       if (lane < m->nq) args.state[ST_QPOS + lane] = s.qpos[lane];
@@ -3841,6 +3887,14 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
   }
   // ---- final reductions, outputs ----------------------------------------------
   cost_c = hsum<S::CPW>(cost_c);
+  if constexpr (WPC == 2) {  // the collision wave's cost_c and truncation flag
+    block_sync();  // wave 0's last step is done with the image (srch)
+    if (wv == 1 && lane == 0) { s.srch[0] = cost_c; s.pad_ = status; }
+    block_sync();
+    if (wv == 1) return;
+    cost_c = s.srch[0];
+    status |= s.pad_;
+  }
   bool finite = true;
   if (lane < m->nq) finite = isfinite(s.qpos[lane]);
   finite = hballot<S::CPW>(!finite) == 0;
@@ -3881,10 +3935,29 @@ __global__ void __launch_bounds__(WAVE, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / Sme
 // ---------------------------------------------------------------------------
 // launchers (the host side lives in another translation unit)
 
+// batches up to this many candidates run the narrow variant with two waves
+// per candidate (MPCR_WPC2_MAX_N overrides; 0 disables): below one
+// candidate per SIMD pair the second wave of a SIMD is otherwise idle
+static int g_wpc2_max_n = -1;
+static int wpc2_max_n() {
+  if (g_wpc2_max_n < 0) {
+    const char* e = getenv("MPCR_WPC2_MAX_N");
+    g_wpc2_max_n = e ? atoi(e) : MPCR_WPC2_MAX_N_DEFAULT;
+  }
+  return g_wpc2_max_n;
+}
+int rollout_set_wpc2_max_n(int n) {
+  const int prev = wpc2_max_n();
+  if (n >= 0) g_wpc2_max_n = n;
+  return prev;
+}
+
 void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigned grid, size_t dyn_lds,
                     hipStream_t st) {
   if (wide)
     hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), 0, st, a, dm);
+  else if (SmemN::CPW == 1 && (int)grid <= wpc2_max_n())
+    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);
   else
     hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3((grid + SmemN::CPW - 1) / SmemN::CPW), dim3(WAVE),
                        dyn_lds, st, a, dm);

@@ -300,7 +300,7 @@ def test_dual_arm_c4_properties(torch_cuda):
     assert rows_per_step.min() >= 8  # 8 equality rows + the linkage contacts
     # the whole shard against the oracle: conditioning bar and the selection
     o, sens = pu.conditioning(m, _td(Pd, xi.cpu().numpy(), H), seed=7)
-    assert int(o["maxcon"].max()) <= 40 and int(o["maxrows"].max()) <= 8 + 4 * 40  # the wide image's caps
+    assert int(o["maxcon"].max()) <= 48 and int(o["maxrows"].max()) <= 8 + 4 * 48  # the wide image's caps
     # the whole bar, well-conditioned candidates included
     a4 = a.cpu().numpy()
     st_ = pu.check(m, a4[:, 0], o, sens, "C4 shard")
@@ -321,3 +321,35 @@ def test_kernel_occupancy_budget(torch_cuda):
     nb, nlds, nreg, wb, wlds, wreg = list(info)
     assert nlds <= 9520 and nreg <= 128 and nb >= 16, list(info)
     assert wlds <= 152448 // 8 and wreg <= 256 and wb >= 8, list(info)
+
+
+@pytest.mark.parametrize("name,n", [("ur5e_hande_mjx", 1024), ("scene_mjx", 512)])
+def test_two_wave_variant_is_bitwise_one_wave(torch_cuda, name, n):
+    """Small batches may run two waves per candidate (collision beside the
+    dynamics, mpcr_set_two_wave_max_n): the same instructions on the same data,
+    so cost4, theta, thetadot and status equal the one-wave kernel's bit for
+    bit."""
+    torch = torch_cuda
+    from manipulator_mujoco_amd import _lib
+    lib = _lib.load()
+    H = 50
+    m = models.load(name, 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 2, torch.device("cuda:0"))
+    e = Engine(m, H, n, Pd)
+    outs = []
+    prev = lib.mpcr_set_two_wave_max_n(-1)
+    try:
+        for thr in (0, n):
+            lib.mpcr_set_two_wave_max_n(thr)
+            c4 = torch.empty((n, 4), device="cuda:0")
+            th = torch.empty((n, 6 * H), device="cuda:0")
+            td = torch.empty((n, 6 * H), device="cuda:0")
+            st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+            e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, cost4=c4, theta=th, thetadot=td, status=st)
+            torch.cuda.synchronize()
+            outs.append((c4, th, td, st))
+    finally:
+        lib.mpcr_set_two_wave_max_n(prev)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
