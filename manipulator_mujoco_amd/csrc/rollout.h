@@ -23,7 +23,7 @@ enum { PAR_Q0 = 0, PAR_W = 8, PAR_PT = 12, PAR_QT = 16, PAR_N = 20 };
 // debug dump of candidate 0's last step (the same layout as the oracle's
 // oracle_step_debug): active contacts (pos xyz, dist, pair, normal xyz),
 // constraint rows (D, aref, vel), qacc_smooth, the final qacc
-enum { DBG_NCON = 0, DBG_NEFC = 1, DBG_CON = 2, DBG_MAXCON = 32, DBG_ROW = DBG_CON + 8 * DBG_MAXCON, DBG_MAXROW = 136,
+enum { DBG_NCON = 0, DBG_NEFC = 1, DBG_CON = 2, DBG_MAXCON = 48, DBG_ROW = DBG_CON + 8 * DBG_MAXCON, DBG_MAXROW = 200,
        DBG_QAS = DBG_ROW + 3 * DBG_MAXROW, DBG_QACC = DBG_QAS + DX_NV, DBG_INFO = DBG_QACC + DX_NV,
        DBG_GRAD = DBG_INFO + 8, DBG_SRCH = DBG_GRAD + DX_NV, DBG_MPR = DBG_SRCH + DX_NV, DBG_N = DBG_MPR + 112 };
 // DBG_MPR: the host puts a pair index in [0]; the kernel's MPR on that pair writes [1] hit, [2] depth,

@@ -92,7 +92,9 @@ namespace mpcr {
 #define MPCR_ABL_FUNC 0
 #endif
 #ifndef MPCR_WPC2_MAX_N_DEFAULT
-#define MPCR_WPC2_MAX_N_DEFAULT 0  // batches up to this size run two waves per candidate (narrow variant)
+#define MPCR_WPC2_MAX_N_DEFAULT 2048  // batches up to this size run two waves per candidate (narrow variant;
+                                      // C3 512 / 1024 / 2048: 1.38 / 1.43 / 1.52 -> 1.07 / 1.09 / 1.20 ms,
+                                      // 4096: 1.77 -> 3.03 ms, the one-wave kernel stays)
 #endif
 #ifndef MPCR_TD_TABLE
 #define MPCR_TD_TABLE 1
@@ -1111,9 +1113,14 @@ template <class S>
 __device__ __forceinline__ int support_vertex(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
                                               int hint) {
   if (m->geom_type[g] == 6) {
+    // the corner on the side of each axis; an axis within the tie band of
+    // zero (a face normal from fp32 rounding) takes the + side, as MPR's box
+    // support does (tie_sign)
     float l[3];
     mtv(l, s.gxmat[g], dir);
-    return m->geom_cornadr[g] + (l[0] >= 0.f ? 1 : 0) + (l[1] >= 0.f ? 2 : 0) + (l[2] >= 0.f ? 4 : 0);
+    const float ln = sqrtf(l[0] * l[0] + l[1] * l[1] + l[2] * l[2]);
+    return m->geom_cornadr[g] + (tie_sign(l[0], ln) >= 0.f ? 1 : 0) + (tie_sign(l[1], ln) >= 0.f ? 2 : 0) +
+           (tie_sign(l[2], ln) >= 0.f ? 4 : 0);
   }
   float p[3];
   support_geom(m, s, g, dir, p, hint);

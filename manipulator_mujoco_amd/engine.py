@@ -253,7 +253,7 @@ class Plant:
 __all__ = ["Engine", "Model", "Plant", "MPCR_LAYOUT_XI", "MPCR_LAYOUT_THETADOT"]
 
 
-DBG_CON, DBG_MAXCON, DBG_MAXROW, DBG_NV = 2, 32, 136, 32  # rollout.h DBG_* layout
+DBG_CON, DBG_MAXCON, DBG_MAXROW, DBG_NV = 2, 48, 200, 32  # rollout.h DBG_* layout
 
 
 def parse_step_debug(buf, nv):

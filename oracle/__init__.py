@@ -245,12 +245,20 @@ def cone_eval(mu, fri, D, jar, jv, alpha):
     return c.value, f, H.reshape(3, 3), line
 
 
-def step_debug(model, qpos, qvel, qacc_ws):
+def step_debug(model, qpos, qvel, qacc_ws, precision="fp64"):
     """The step's active contacts / rows / qacc_smooth / qacc in the kernel's
-    debug layout (engine.parse_step_debug)."""
+    debug layout (engine.parse_step_debug).  precision="fp32": the fp32 build
+    (probe F of tests/parity_util.py) on the state rounded to fp32."""
     from manipulator_mujoco_amd.engine import parse_step_debug
+    if precision == "fp32":
+        fp = ctypes.POINTER(ctypes.c_float)
+        a = [np.ascontiguousarray(x, dtype=np.float32) for x in (qpos, qvel, qacc_ws)]
+        out = np.zeros(1234, dtype=np.float32)  # rollout.h DBG_N
+        lib_f32().oracle_step_debug(ctypes.byref(struct_f32(model)), *(x.ctypes.data_as(fp) for x in a),
+                                    out.ctypes.data_as(fp))
+        return parse_step_debug(out, model.nv)
     s = model.to_struct()
-    out = np.zeros(802)
+    out = np.zeros(1234)  # rollout.h DBG_N
     a = [np.ascontiguousarray(x, dtype=np.float64) for x in (qpos, qvel, qacc_ws)]
     lib().oracle_step_debug(ctypes.byref(s), *(_p(x) for x in a), _p(out))
     return parse_step_debug(out, model.nv)

@@ -1411,9 +1411,13 @@ static void face_world(const mpcr_model_t* m, const odata* d, int g, int f, doub
    takes the + side) */
 static int support_vertex(const mpcr_model_t* m, const odata* d, int g, const double dir[3], int* hint) {
   if (m->geom_type[g] == MPCR_GEOM_BOX) {
+    /* the corner on the side of each axis; an axis that ties (tie_sign: the
+       kernel's band, or MuJoCo's exact zero under EXACT_SUP) takes the + side */
     double l[3];
     mulmtv(l, d->geom_xmat[g], dir);
-    return m->geom_cornadr[g] + (l[0] >= 0 ? 1 : 0) + (l[1] >= 0 ? 2 : 0) + (l[2] >= 0 ? 4 : 0);
+    const double ln = sqrt(dot3(l, l));
+    return m->geom_cornadr[g] + (tie_sign(l[0], ln) >= 0 ? 1 : 0) + (tie_sign(l[1], ln) >= 0 ? 2 : 0) +
+           (tie_sign(l[2], ln) >= 0 ? 4 : 0);
   }
   double p[3];
   support(m, d, g, dir, p, hint);
@@ -2308,7 +2312,10 @@ static double hash_unit(unsigned seed, int b, int t, int i) {
 
 /* parity debugging: one step like oracle_step, dumping the active contacts,
    the constraint rows, qacc_smooth and qacc in the kernel's DBG_* layout
-   (manipulator_mujoco_amd/csrc/rollout.h; 730 doubles) */
+   (manipulator_mujoco_amd/csrc/rollout.h: 48 contacts, 200 rows; 1234
+   doubles) */
+enum { ODBG_MAXCON = 48, ODBG_ROW = 2 + 8 * ODBG_MAXCON, ODBG_MAXROW = 200, ODBG_QAS = ODBG_ROW + 3 * ODBG_MAXROW,
+       ODBG_QACC = ODBG_QAS + 32, ODBG_INFO = ODBG_QACC + 32, ODBG_N = ODBG_INFO + 8 + 64 + 112 };
 int oracle_step_debug(const mpcr_model_t* m, const double* qpos, const double* qvel, const double* qacc_ws,
                       double* out) {
   odata* d = (odata*)calloc(1, sizeof(odata));
@@ -2318,14 +2325,14 @@ int oracle_step_debug(const mpcr_model_t* m, const double* qpos, const double* q
   memcpy(d->qacc_warmstart, qacc_ws, sizeof(double) * m->nv);
   reset_hints(d);
   forward(m, d);
-  memset(out, 0, sizeof(double) * 802);
-  memcpy(out + 730, d->dbg, sizeof(d->dbg));
-  memcpy(out + 738, d->dbg_gs, sizeof(d->dbg_gs));
+  memset(out, 0, sizeof(double) * ODBG_N);
+  memcpy(out + ODBG_INFO, d->dbg, sizeof(d->dbg));
+  memcpy(out + ODBG_INFO + 8, d->dbg_gs, sizeof(d->dbg_gs));
   int na = 0;
   for (int c = 0; c < d->ncon; c++) {
     const ocontact* k = &d->con[c];
     if (!k->active) continue;
-    if (na < 32) {
+    if (na < ODBG_MAXCON) {
       double* o = out + 2 + 8 * na;
       memcpy(o, k->pos, 3 * sizeof(double));
       o[3] = k->dist; o[4] = k->pair;
@@ -2335,13 +2342,13 @@ int oracle_step_debug(const mpcr_model_t* m, const double* qpos, const double* q
   }
   out[0] = na;
   out[1] = d->nefc;
-  for (int r = 0; r < d->nefc && r < 136; r++) {
-    out[258 + 3 * r] = d->efc_D[r];
-    out[258 + 3 * r + 1] = d->efc_aref[r];
-    out[258 + 3 * r + 2] = d->efc_vel[r];
+  for (int r = 0; r < d->nefc && r < ODBG_MAXROW; r++) {
+    out[ODBG_ROW + 3 * r] = d->efc_D[r];
+    out[ODBG_ROW + 3 * r + 1] = d->efc_aref[r];
+    out[ODBG_ROW + 3 * r + 2] = d->efc_vel[r];
   }
-  memcpy(out + 666, d->qacc_smooth, sizeof(double) * m->nv);
-  memcpy(out + 698, d->qacc, sizeof(double) * m->nv);
+  memcpy(out + ODBG_QAS, d->qacc_smooth, sizeof(double) * m->nv);
+  memcpy(out + ODBG_QACC, d->qacc, sizeof(double) * m->nv);
   free(d);
   return 0;
 }

@@ -41,14 +41,21 @@ def run(idx=2986, H=100):
         qv[np.asarray(m.ctrl_dofadr[:m.nctrl])] = td[:, t]
         plant.set_state(qpos=qpos, qvel=qv, qacc_warmstart=ws)
         kd = plant.step_debug(td[:, t])
-        od = oracle.step_debug(m, qpos, qv, ws)
         o = oracle.step(m, qpos, qv, ws)
-        kp = sorted((int(p), tuple(np.round(x, 4))) for p, x in zip(kd["con_pair"], kd["con_pos"]) if p in mesh_pairs)
-        op = sorted((int(p), tuple(np.round(x, 4))) for p, x in zip(od["con_pair"], od["con_pos"]) if p in mesh_pairs)
         scale = max(1.0, np.abs(o["qacc"]).max())
-        rows.append(dict(t=t, n_mesh=len(op), same=len(kp) == len(op) and all(
-            a[0] == b[0] and np.abs(np.array(a[1]) - np.array(b[1])).max() <= 2e-4 for a, b in zip(kp, op)),
-            qacc_err=float(np.abs(plant.qacc - o["qacc"]).max() / scale)))
+        kp = sorted((int(p), tuple(np.round(x, 4))) for p, x in zip(kd["con_pair"], kd["con_pos"]) if p in mesh_pairs)
+        row = dict(t=t)
+        # the fp64 oracle, and the fp32 build as the second reference (probe F):
+        # a flush mesh-mesh contact (the gripper linkage) can take MPR's other
+        # portal under fp32 rounding, the fp32 oracle the same way as the kernel
+        for tag, prec in (("", "fp64"), ("_f32", "fp32")):
+            od = oracle.step_debug(m, qpos, qv, ws, precision=prec)
+            op = sorted((int(p), tuple(np.round(x, 4))) for p, x in zip(od["con_pair"], od["con_pos"]) if p in mesh_pairs)
+            row["n_mesh" + tag] = len(op)
+            row["same" + tag] = len(kp) == len(op) and all(
+                a[0] == b[0] and np.abs(np.array(a[1]) - np.array(b[1])).max() <= 2e-4 for a, b in zip(kp, op))
+            row["qacc_err" + tag] = float(np.abs(plant.qacc - od["qacc"]).max() / scale)
+        rows.append(row)
         qpos, qvel, ws = o["qpos"], o["qvel"], o["qacc_warmstart"]
     return rows, sorted(big), sorted(mesh_pairs)
 
@@ -56,10 +63,12 @@ def run(idx=2986, H=100):
 if __name__ == "__main__":
     rows, big, pairs = run(int(sys.argv[1]) if len(sys.argv) > 1 else 2986)
     act = [r for r in rows if r["n_mesh"] > 0]
+    best = [min(r["qacc_err"], r["qacc_err_f32"]) for r in rows]
     print(f"big hulls {big}, their plane pairs {pairs}; steps with big-hull plane contacts {len(act)}, "
           f"max contacts {max([r['n_mesh'] for r in act], default=0)}, identical contact sets "
-          f"{sum(r['same'] for r in act)}/{len(act)}; max qacc err/scale {max(r['qacc_err'] for r in rows):.2e}, "
-          f"median {np.median([r['qacc_err'] for r in rows]):.2e}")
-    for r in act:
-        if not r["same"]:
+          f"{sum(r['same'] for r in act)}/{len(act)} (fp32 oracle {sum(r['same_f32'] for r in act)}); "
+          f"max qacc err/scale {max(r['qacc_err'] for r in rows):.2e} vs fp64, {max(best):.2e} vs the nearer, "
+          f"median {np.median(best):.2e}")
+    for r in rows:
+        if r["qacc_err"] > 5e-3 or (r["n_mesh"] and not r["same"]):
             print("  differs:", r)
