@@ -552,6 +552,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.geom_hullnum[i] = m.geom_hullnum[g];
     d.geom_lutadr[i] = m.geom_lutadr[g];
     d.geom_faceadr[i] = m.geom_faceadr[g];
+    d.geom_facenum[i] = m.geom_faceadr[g] >= 0 ? m.geom_facenum[g] : 0;
     d.geom_cornadr[i] = m.geom_cornadr[g];
     for (int k = 0; k < 3; k++) d.geom_size[i][k] = (float)m.geom_size[g][k];
     if (dmap[b] >= 0) {

@@ -129,6 +129,7 @@ struct DevModel {
                             // a climb round addresses them from the vertex index alone (no hull_info load)
   // polygon faces of polyhedron-pair geoms (mesh-mesh / box-mesh manifold) ----
   int geom_faceadr[DX_NG];   // first face, -1: none
+  int geom_facenum[DX_NG];   // its face count
   int geom_cornadr[DX_NG];   // a box's 8 corners in hull_vert (bit k: + side of axis k), -1: none
   const float4* face_plane;  // outward normal xyz | offset (n . x = offset), geom frame
   const int2* face_vinfo;    // (first face_vert entry, count <= MPCR_FACE_MAXV)

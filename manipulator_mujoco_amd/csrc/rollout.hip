@@ -1104,6 +1104,7 @@ __device__ __noinline__ void plane_mesh_manifold_wave(const DevModel* __restrict
 }
 
 constexpr int kPendingManifold = -4;  // narrow_lane: plane-mesh pair awaiting plane_mesh_manifold_wave
+constexpr float kPolyConeCos = 0.94f;  // ~20 degrees: candidate faces' Gauss-map cone about MPR's normal
 constexpr int kPendingPoly = -5;      // narrow_lane: polyhedron pair hit by MPR, awaiting poly_manifold_wave
 
 // hull vertex index of geom g's support point along dir (world): the mesh
@@ -1153,8 +1154,9 @@ __device__ __forceinline__ void vert_rel(const DevModel* __restrict__ m, const S
 // orders), wave-cooperative: every lane calls it with the same pair and MPR's
 // normal n (g1 -> g2) / depth, lane q receives up to 4 contacts (nsl = 4) or
 // keeps MPR's single one (nsl = 1: an edge axis carries the contact).  One
-// lane per candidate reference face (the faces on both support vertices) with
-// its own support query for the SAT separation, one lane per candidate
+// lane per candidate reference face (the faces on both support vertices and
+// those within the Gauss-map cone of MPR's normal) with its own support query
+// for the SAT separation, one lane per candidate
 // incident face, Sutherland-Hodgman against the reference face's side planes
 // with one lane per polygon vertex and scan compaction (as box_box_wave), the
 // _manifold_points picks as wave maxima.  Coordinates relative to g2's
@@ -1176,14 +1178,52 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
   }
   const int s1 = __shfl(sv, 0), s2 = __shfl(sv, 1);
   const int2 i1 = m->vert_finfo[s1], i2 = m->vert_finfo[s2];
-  const int c1 = min(i1.y, WAVE), c2 = min(i2.y, WAVE - c1), nc = c1 + c2;
-  // candidate reference faces: SAT separation along each outward normal
+  const int c1 = min(i1.y, WAVE), c2 = min(i2.y, WAVE - c1), ns = c1 + c2;
+  // candidate reference faces, at most 64 (one per lane), in the oracle's
+  // order: g1's on s1, g2's on s2, then every face whose outward normal lies
+  // within the Gauss-map cone of n (g1) / -n (g2), face index order, those
+  // already listed skipped -- a ballot-compacted scan of both face tables into
+  // an LDS list (the clip buffer's second half, free until the clip)
+  int* const cl = reinterpret_cast<int*>(&s.polyw[1][0][0]);
+  int nc = ns;
+#pragma unroll 1
+  for (int sd = 0; sd < 2; sd++) {
+    const int g = sd ? g2 : g1, fa = m->geom_faceadr[g], fnum = m->geom_facenum[g];
+    const int2 li = sd ? i2 : i1;
+    const int cs = sd ? c2 : c1;
+    const float sg = sd ? -1.f : 1.f;
+#pragma unroll 1
+    for (int b0 = 0; b0 < fnum && nc < WAVE; b0 += WAVE) {
+      bool sel = false;
+      if (b0 + lane < fnum) {
+        const float4 fp = m->face_plane[fa + b0 + lane];
+        const float nl[3] = {fp.x, fp.y, fp.z};
+        float nw[3];
+        mv(nw, s.gxmat[g], nl);
+        sel = sg * (nw[0] * n[0] + nw[1] * n[1] + nw[2] * n[2]) >= kPolyConeCos;
+        if (sel)
+          for (int k = 0; k < cs; k++) sel &= m->vert_face[li.x + k] != fa + b0 + lane;
+      }
+      int tot;
+      const int o = wscan_excl(sel ? 1 : 0, tot);
+      if (sel && nc + o < WAVE) cl[nc - ns + o] = (fa + b0 + lane) | (sd << 24);
+      nc = min(nc + tot, WAVE);
+    }
+  }
+  sync();
+  // SAT separation along each candidate's outward normal
   float sep = -3e38f;
-  int fid = -1;
+  int fid = -1, two = 0;
   if (lane < nc) {
-    const bool two = lane >= c1;
+    if (lane < ns) {
+      two = lane >= c1;
+      fid = m->vert_face[two ? i2.x + lane - c1 : i1.x + lane];
+    } else {
+      const int e = cl[lane - ns];
+      two = e >> 24;
+      fid = e & 0xffffff;
+    }
     const int g = two ? g2 : g1, go = two ? g1 : g2;
-    fid = m->vert_face[two ? i2.x + lane - c1 : i1.x + lane];
     float nw[3], off, pt[3];
     face_rel(m, s, g, fid, c, nw, off);
     const float mn[3] = {-nw[0], -nw[1], -nw[2]};
@@ -1191,8 +1231,12 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
     support_geom(m, s, go, mn, pt, h, c);
     sep = nw[0] * pt[0] + nw[1] * pt[1] + nw[2] * pt[2] - off;
   }
+  // the maximum's tie band: the lowest face index (a flush face pair has the
+  // same separation from either side)
   const float mx = wmax(sep);
-  const unsigned long long bm = __ballot(lane < nc && near_max(sep, mx));
+  const bool nb = lane < nc && near_max(sep, mx);
+  const float fmn = -wmax(nb ? -(float)fid : -3e38f);
+  const unsigned long long bm = __ballot(nb && (float)fid == fmn);
   const int kb = bm ? __builtin_ctzll(bm) : 0;
   const float bsep = __shfl(sep, kb);
   if (!bm || -bsep > 1.05f * depth + 1e-5f) {  // an edge axis: MPR's single contact
@@ -1200,7 +1244,7 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
     return;
   }
   const int fr = __shfl(fid, kb);
-  const bool rtwo = kb >= c1;
+  const bool rtwo = __shfl(two, kb) != 0;
   const int gr = rtwo ? g2 : g1, gi = rtwo ? g1 : g2;
   float nr[3], offr;
   face_rel(m, s, gr, fr, c, nr, offr);
@@ -2467,7 +2511,11 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
 #endif
 #if MPCR_PACE
     if (pace) {  // post this step, read the SIMD mates' (consumed mid-step)
-      if (lane == pace_own) __hip_atomic_store(pace + lane, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // a plain store keeps the line in this XCD's L2 (agent scope would drop
+      // it: every mate's next load then missed L2 -- the launch's largest
+      // HBM stream); the readers share the CU, so their L1-bypassing (sc1)
+      // loads see it in L2
+      if (lane == pace_own) __hip_atomic_store(pace + lane, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (lane < 16) pace_v = __hip_atomic_load(pace + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #endif
@@ -3921,7 +3969,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     }
   }
 #if MPCR_PACE
-  if (pace && lane == pace_own) __hip_atomic_store(pace + lane, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (pace && lane == pace_own) __hip_atomic_store(pace + lane, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
 #ifdef MPCR_WAVETIME
   if (lane == 0 && live && args.prof) {

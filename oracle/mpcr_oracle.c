@@ -1395,9 +1395,12 @@ static void col_plane_mesh(const mpcr_model_t* m, odata* d, int pair, int gp, in
    scans every face (and edge pair) of both hulls, the axis search here is
    seeded by MPR's normal n (g1 -> g2): the candidate axes are the faces on
    the support vertex of g1 along n and of g2 along -n (MPR's direction
-   lies in those vertices' normal cones).  An edge contact -- no candidate
+   lies in those vertices' normal cones) and every face whose normal lies
+   within ~20 degrees of n (resp. -n).  An edge contact -- no candidate
    face within 5 % of MPR's depth -- keeps MPR's single point.  Parity vs
    MJX unpinned (DESIGN.md §Dual-arm class). */
+
+#define POLY_CONE_COS 0.94 /* ~20 degrees: the candidate faces' Gauss-map cone about MPR's normal */
 
 /* world outward normal and offset (n . x = off) of face f of geom g */
 static void face_world(const mpcr_model_t* m, const odata* d, int g, int f, double nw[3], double* off) {
@@ -1436,8 +1439,26 @@ static double support_value(const mpcr_model_t* m, const odata* d, int g, const 
   return dot3(p, dir);
 }
 
+/* diagnostic (oracle_poly_probe): the last manifold decision on one pair --
+   [0] calls, [1] MPR depth, [2] best face separation, [3] its candidate index
+   (-1 none), [4] support-vertex candidates on g1, [5] all candidates, [6] support vertex g1, [7] g2,
+   [8] result (0 edge / no points, 1 face manifold), [9] reference face,
+   [10] incident face, [11] points kept, [12..14] MPR normal */
+static __thread int g_probe_pair = -1;
+static __thread double g_probe[16];
+void oracle_poly_probe(int pair, double* out) {
+  if (out) memcpy(out, g_probe, sizeof(g_probe));
+  g_probe_pair = pair;
+  memset(g_probe, 0, sizeof(g_probe));
+}
+#define PROBE(i, v) do { if (pair == g_probe_pair) g_probe[i] = (v); } while (0)
+
 static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int g2, const double n[3], double depth,
                          ocontact* out) {
+  PROBE(0, g_probe[0] + 1);
+  PROBE(1, depth);
+  PROBE(12, n[0]); PROBE(13, n[1]); PROBE(14, n[2]);
+  PROBE(8, 0); PROBE(9, -1); PROBE(10, -1); PROBE(11, 0);
   /* climbs start from the pair's hints (where MPR's queries ended) and do not
      update them; every query starts afresh (the kernel runs them on parallel
      lanes) */
@@ -1448,30 +1469,49 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   const int s1 = support_vertex(m, d, g1, n, &h);
   h = h1;
   const int s2 = support_vertex(m, d, g2, nn, &h);
-  /* candidate reference faces (g1's on s1, then g2's on s2; at most 64, the
-     kernel's lanes): SAT separation along each outward face normal, the
-     maximum's first candidate within the tie band (order-free, as a wave) */
+  /* candidate reference faces, at most 64 (the kernel's lanes), in this
+     order: g1's on s1, g2's on s2, then the faces whose outward normal lies
+     within the Gauss-map cone of MPR's direction (g1: n . nf >= POLY_CONE_COS,
+     g2 the same about -n; face index order, those already listed skipped) --
+     MJX's SAT scans every face; the cone keeps the axis search independent of
+     which of two near-flush face pairs MPR's portal ended on.  SAT separation
+     along each outward face normal */
   const int c1 = m->vert_facenum[s1] < 64 ? m->vert_facenum[s1] : 64;
   const int c2 = m->vert_facenum[s2] < 64 - c1 ? m->vert_facenum[s2] : 64 - c1;
+  int fid[64], side[64], nc = 0;
+  for (int k = 0; k < c1; k++) { fid[nc] = m->vert_face[m->vert_faceadr[s1] + k]; side[nc++] = 0; }
+  for (int k = 0; k < c2; k++) { fid[nc] = m->vert_face[m->vert_faceadr[s2] + k]; side[nc++] = 1; }
+  for (int sd = 0; sd < 2; sd++) {
+    const int g = sd ? g2 : g1, fa = m->geom_faceadr[g], cs = sd ? c2 : c1;
+    const int ls = sd ? m->vert_faceadr[s2] : m->vert_faceadr[s1];
+    for (int f = fa; f < fa + m->geom_facenum[g] && nc < 64; f++) {
+      double nf[3], off;
+      face_world(m, d, g, f, nf, &off);
+      if ((sd ? -1.0 : 1.0) * dot3(nf, n) < POLY_CONE_COS) continue;
+      int dup = 0;
+      for (int k = 0; k < cs; k++) dup |= m->vert_face[ls + k] == f;
+      if (!dup) { fid[nc] = f; side[nc++] = sd; }
+    }
+  }
   double sep[64];
-  int fid[64];
   double mx = -1e300;
-  for (int k = 0; k < c1 + c2; k++) {
-    const int two = k >= c1, g = two ? g2 : g1, go = two ? g1 : g2;
-    const int f = m->vert_face[two ? m->vert_faceadr[s2] + k - c1 : m->vert_faceadr[s1] + k];
+  for (int k = 0; k < nc; k++) {
+    const int two = side[k], g = two ? g2 : g1, go = two ? g1 : g2;
     double nf[3], off, mnf[3];
-    face_world(m, d, g, f, nf, &off);
+    face_world(m, d, g, fid[k], nf, &off);
     for (int c = 0; c < 3; c++) mnf[c] = -nf[c];
     h = two ? h0 : h1;
     sep[k] = -support_value(m, d, go, mnf, &h) - off; /* min over go of nf . x, minus the plane */
-    fid[k] = f;
     if (sep[k] > mx) mx = sep[k];
   }
+  /* the maximum's tie band: the lowest face index (a flush face pair has the
+     same separation from either side; order-free, as a wave min) */
   int kb = -1;
-  for (int k = 0; k < c1 + c2 && kb < 0; k++)
-    if (near_max(sep[k], mx)) kb = k;
+  for (int k = 0; k < nc; k++)
+    if (near_max(sep[k], mx) && (kb < 0 || fid[k] < fid[kb])) kb = k;
+  PROBE(2, kb >= 0 ? sep[kb] : 0); PROBE(3, kb); PROBE(4, c1); PROBE(5, nc); PROBE(6, s1); PROBE(7, s2);
   if (kb < 0 || -sep[kb] > 1.05 * depth + 1e-5) return 0; /* an edge axis carries the contact */
-  const int best_f = fid[kb], gr = kb >= c1 ? g2 : g1, gi = kb >= c1 ? g1 : g2;
+  const int best_f = fid[kb], gr = side[kb] ? g2 : g1, gi = side[kb] ? g1 : g2;
   double nr[3], offr;
   face_world(m, d, gr, best_f, nr, &offr);
   /* incident face: the most anti-parallel face on gi's support vertex along -nr */
@@ -1527,7 +1567,9 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
     const double dk = dot3(nr, poly[cur][k]) - offr;
     if (dk < margin) { memcpy(pts[nk], poly[cur][k], sizeof(double) * 3); dist[nk++] = dk; }
   }
+  PROBE(9, best_f); PROBE(10, inc_f); PROBE(11, nk);
   if (nk == 0) return 0;
+  PROBE(8, 1);
   /* at most 4: _manifold_points' picks (a = the first, b = the farthest from
      a, c = the farthest from line ab, d = the farthest from edge bc or ac;
      near_max's first index within the tie band) */

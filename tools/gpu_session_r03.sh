@@ -89,4 +89,11 @@ fi
 if [[ $STEPS == *wavetime* ]]; then
   N=4096 run wavetime 120 python tools/wavetime.py scene_mjx $OUT/wavetime_c3_4096.json
 fi
+if [[ $STEPS == *traffic* ]]; then  # HBM traffic attribution (build_variants/t_*.so, tools/build_traffic_variants.py)
+  for v in ${TRAFFIC_VARIANTS:-t_ship t_jl96 t_cprev t_both}; do
+    for c in FETCH_SIZE WRITE_SIZE; do
+      N=4096 R=3 run traffic_${v}_$c 120 rocprofv3 --pmc $c --output-format csv -d $OUT/traffic_${v}_$c -o run -- python3 tools/ab_time.py build_variants/$v.so
+    done
+  done
+fi
 echo "[session] done"
