@@ -26,6 +26,12 @@ constexpr int DX_MAXACT = 20;  // active contacts kept per step
 constexpr int DX_MAXEFC = 96;  // constraint rows kept per step
 constexpr int DX_NSLOT = 192;  // robot-masked contact slots
 constexpr int DX_NTEN = 2;     // spatial (two-site) tendons with length limits
+// polyhedron manifold: the faces of a geom whose outward normal can lie within
+// the Gauss-map cone (kPolyConeCos) of a direction in each cube-map cell of
+// CONE_R x CONE_R per cube face (built on the host from the face planes)
+constexpr int CONE_R = 8;
+constexpr int CONE_CELLS = 6 * CONE_R * CONE_R;
+constexpr double CONE_COS = 0.94;  // the kernel's and the oracle's cone (rollout.hip kPolyConeCos)
 
 // body kinds for the kinematics pass
 enum { BK_STATIC = 0, BK_FREE = 1, BK_HINGE = 2, BK_SLIDE = 3, BK_WELD = 4 };
@@ -136,6 +142,10 @@ struct DevModel {
   const int* face_vert;      // hull_vert indices, counter-clockwise about the normal
   const int2* vert_finfo;    // per hull vertex: (first vert_face entry, count)
   const int* vert_face;      // face indices
+  int geom_coneadr[DX_NG];   // first cone_cell record (CONE_CELLS per geom with faces), -1: none
+  const int2* cone_cell;     // (first cone_face entry, count) per cell
+  const int* cone_face;      // face indices, ascending within a cell: a superset of the faces the
+                             // cone test can accept for any direction in the cell
 
   int ctrl_qposadr[DX_NCTRL], ctrl_dofadr[DX_NCTRL];
 

@@ -24,7 +24,7 @@ namespace mpcr {
 // ---------------------------------------------------------------------------
 // diagnostic phase stamps (separate -DMPCR_PROFILE build; never in the timed one)
 #ifdef MPCR_PROFILE
-#define PROF_DECL unsigned long long prof_acc[24] = {0}; unsigned long long prof_last = __builtin_amdgcn_s_memtime();
+#define PROF_DECL unsigned long long prof_acc[32] = {0}; unsigned long long prof_last = __builtin_amdgcn_s_memtime();
 #define STAMP(i)                                              \
   do {                                                        \
     unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
@@ -33,7 +33,7 @@ namespace mpcr {
   } while (0)
 #define PROF_FLUSH                                                          \
   if (lane == 0 && args.prof)                                               \
-    for (int i_ = 0; i_ < 24; i_++) atomicAdd(&args.prof[i_], prof_acc[i_]);
+    for (int i_ = 0; i_ < 32; i_++) atomicAdd(&args.prof[i_], prof_acc[i_]);
 // wave-level event counter (first active lane adds 1; -DMPCR_PROFILE_COUNTS
 // only: the shared atomics distort the cycle shares)
 #ifdef MPCR_PROFILE_COUNTS
@@ -44,7 +44,17 @@ namespace mpcr {
 #else
 #define PROF_COUNT(m, i)
 #endif
+// sub-phase stamps inside a device function (one atomic per stamp and wave)
+#define PSTAMP_DECL unsigned long long pst_ = __builtin_amdgcn_s_memtime();
+#define PSTAMP(m, i)                                                                       \
+  do {                                                                                     \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                          \
+    if ((m)->prof && (int)__lane_id() == 0) atomicAdd((m)->prof + (i), now_ - pst_);       \
+    pst_ = now_;                                                                           \
+  } while (0)
 #else
+#define PSTAMP_DECL
+#define PSTAMP(m, i)
 #define PROF_DECL
 #define STAMP(i)
 #define PROF_FLUSH
@@ -1165,6 +1175,7 @@ template <class S>
 __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, S& s, const short* hints, int p,
                                                 const float n[3], float depth, int q, int lane, float dist[4],
                                                 float pos[4][3], float nrm[4][3], int& nsl) {
+  PSTAMP_DECL
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   const float c[3] = {s.gxpos[g2][0], s.gxpos[g2][1], s.gxpos[g2][2]};
   const int hw = reinterpret_cast<const int*>(hints)[p - m->cvx_base];
@@ -1177,6 +1188,7 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
     sv = support_vertex(m, s, lane ? g2 : g1, d, lane ? h1 : h0);
   }
   const int s1 = __shfl(sv, 0), s2 = __shfl(sv, 1);
+  PSTAMP(m, 23);
   const int2 i1 = m->vert_finfo[s1], i2 = m->vert_finfo[s2];
   const int c1 = min(i1.y, WAVE), c2 = min(i2.y, WAVE - c1), ns = c1 + c2;
   // candidate reference faces, at most 64 (one per lane), in the oracle's
@@ -1211,6 +1223,7 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
     }
   }
   sync();
+  PSTAMP(m, 24);
   // SAT separation along each candidate's outward normal
   float sep = -3e38f;
   int fid = -1, two = 0;
@@ -1239,6 +1252,7 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
   const unsigned long long bm = __ballot(nb && (float)fid == fmn);
   const int kb = bm ? __builtin_ctzll(bm) : 0;
   const float bsep = __shfl(sep, kb);
+  PSTAMP(m, 25);
   if (!bm || -bsep > 1.05f * depth + 1e-5f) {  // an edge axis: MPR's single contact
     if (lane == q) nsl = 1;
     return;
@@ -1291,6 +1305,7 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
     s.polyw[0][lane][0] = w[0]; s.polyw[0][lane][1] = w[1]; s.polyw[0][lane][2] = w[2];
   }
   sync();
+  PSTAMP(m, 26);
   int np = ninc, cur = 0;
   for (int e = 0; e < nrv && np > 0; e++) {
     const float Ae[3] = {__shfl(A[0], e), __shfl(A[1], e), __shfl(A[2], e)};
@@ -1333,6 +1348,7 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
   const unsigned long long km = __ballot(keep);
   const int nk = __popcll(km);
   sync();  // the clip buffer is free for the next pair
+  PSTAMP(m, 27);
   if (nk == 0) {
     if (lane == q) nsl = 1;
     return;
@@ -1391,6 +1407,7 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
     }
   }
   if (lane == q) nsl = 4;
+  PSTAMP(m, 28);
 }
 
 // per-lane narrow phase for plane/capsule/box-vs-capsule pairs (box-box is
@@ -1970,10 +1987,26 @@ __device__ __forceinline__ void box_box_wave(const DevModel* __restrict__ m, S& 
 // Per-lane contact bookkeeping after a narrow-phase pass: cost_c on the
 // robot-masked slots (SBP/mjx_planner.py:284-296) and ballot-compacted append
 // of the active contacts.  Must be called by all lanes (two barriers).
+// Previous-step masked slot distances (cost_c's history term) of the lane's
+// own pairs, held in registers across the horizon (narrow variant): the lane
+// that owns pair p in 64-pair chunk k owns its <= 4 slots every step, so
+// chunk k < NC keeps them in v[k][0..3] (no per-step HBM slab round trip: the
+// slab's L2 evictions were ~8.6 MB of a C3 launch's 29.7 MB HBM traffic);
+// pairs of later chunks use the slab.  The dual-arm class keeps the slab.
+#ifndef MPCR_N_CPREV_REG
+#define MPCR_N_CPREV_REG 1
+#endif
+template <class S>
+struct SlotHist {
+  static constexpr int NC = (!S::WIDE && MPCR_N_CPREV_REG) ? 128 / S::HL : 0;
+  float v[NC > 0 ? NC : 1][4];
+};
+
 template <class S>
 __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S& s, const RolloutArgs& args, int b,
                                               int t, int H, bool valid, int p, int nsl, const float dist[4],
-                                              const float pos[4][3], const float nrm[4][3], float& cost_c) {
+                                              const float pos[4][3], const float nrm[4][3], float& cost_c,
+                                              SlotHist<S>& sh, int k) {
   int act = 0;
   if (valid) {
     const int sa = m->pair_slotadr[p];
@@ -1984,9 +2017,18 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
         if (c < ns) {
           const float d = dist[c];
           if (d < 0.f) cost_c += 1.f;
-          float* cp = S::CPREV_GLOBAL ? args.slot_prev + (size_t)b * m->nslot : s.cprev;
-          if (t > 0) cost_c += fmaxf(cp[sa + c] * (1.f - 0.005f) - d, 0.f);
-          cp[sa + c] = d;
+          if (SlotHist<S>::NC > 0 && k < SlotHist<S>::NC) {  // this lane's registers (chunk k, slot c)
+            float prev = 0.f;
+#pragma unroll
+            for (int j = 0; j < SlotHist<S>::NC; j++) prev = j == k ? sh.v[j][c] : prev;
+            if (t > 0) cost_c += fmaxf(prev * (1.f - 0.005f) - d, 0.f);
+#pragma unroll
+            for (int j = 0; j < SlotHist<S>::NC; j++) sh.v[j][c] = j == k ? d : sh.v[j][c];
+          } else {
+            float* cp = S::CPREV_GLOBAL ? args.slot_prev + (size_t)b * m->nslot : s.cprev;
+            if (t > 0) cost_c += fmaxf(cp[sa + c] * (1.f - 0.005f) - d, 0.f);
+            cp[sa + c] = d;
+          }
           if (args.trace_slots && b < args.n) args.trace_slots[((size_t)b * H + t) * m->nslot + sa + c] = d;
         }
       }
@@ -2474,6 +2516,11 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
                  ? args.input[((size_t)bi * nc + lane) * args.nbasis + k] : 0.f;
 #endif
   float cost_g = 0.f, cost_r = 0.f, cost_c = 0.f;
+  SlotHist<S> shist;
+#pragma unroll
+  for (int j = 0; j < SlotHist<S>::NC; j++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) shist.v[j][c] = 0.f;
   int status = 0, nefc_sum = 0, nefc_max = 0;
   // this lane's controlled joint addresses, held across the horizon (read
   // every step; the per-step model launder would otherwise reload them)
@@ -3145,7 +3192,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       if (run && func != 4 && !defer && !(MPCR_ABL_FUNC & (1 << func))) nsl = narrow_lane(m, s, hx, p, dist, pos, nrm);
       STAMP(11);
       const unsigned long long bbm = hballot<S::CPW>(run && func == 4 && !(MPCR_ABL_FUNC & 16));
-      emit_contacts(m, s, args, b, t, H, valid && func != 4 && !defer, p, nsl, dist, pos, nrm, cost_c);
+      emit_contacts(m, s, args, b, t, H, valid && func != 4 && !defer, p, nsl, dist, pos, nrm, cost_c, shist, k);
       STAMP(12);
       if (bbm && !(m->disableflags & 16)) {
         unsigned long long mm = bbm;
@@ -3169,6 +3216,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
             int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn, (args.dbg && b == 0 && t == H - 1) ? args.dbg
                                                                                                : nullptr)
                           : 0;
+            STAMP(21);
             for (unsigned long long pm = __ballot(cn_sl == kPendingManifold); pm; pm &= pm - 1) {
               const int q = __builtin_ctzll(pm);  // penetrating plane-mesh pairs, one at a time, all lanes
               const int pq = __shfl(pc, q);
@@ -3178,6 +3226,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
               const float nq[3] = {Rp[2], Rp[5], Rp[8]};
               plane_mesh_manifold_wave(m, s, m->pair_g2[pq], nq, s.gxpos[gp], -dq, q, lane, cd, cp, cn, cn_sl);
             }
+            STAMP(22);
             for (unsigned long long pm = __ballot(cn_sl == kPendingPoly); pm; pm &= pm - 1) {
               const int q = __builtin_ctzll(pm);  // penetrating polyhedron pairs, one at a time, all lanes
               const int pq = __shfl(pc, q);
@@ -3186,7 +3235,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
               poly_manifold_wave(m, s, hx, pq, nq, -dq, q, lane, cd, cp, cn, cn_sl);
             }
             STAMP(17);
-            emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c);
+            emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c, shist, -1);
             STAMP(18);
           }
           sync();

@@ -981,6 +981,9 @@ static int lut_cell(const double l[3]) {
 /* MPR work counters of the calling thread (diagnostic: tools/mpr_stats.py, workers = 1):
    0 calls, 1 support pairs, 2 climb rounds, 3 neighbour evaluations, 4 hits,
    5 discovery iterations, 6 phase-2 iterations, 7 phase-3 iterations,
+   polyhedron manifold: 8 calls, 9 candidate faces, 10 faces scanned for the
+   cone, 11 calls reaching the clip, 12 reference-polygon vertices, 13
+   incident-polygon vertices, 14 climb rounds, 15 support-vertex faces,
    16.. histogram of support pairs per call (capped at 47) */
 static __thread long g_mpr_stats[64]; /* per thread: the checker's pool threads never share it */
 static void support_rel(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint,
@@ -1465,6 +1468,8 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   const int h0 = d->hint[pair][0], h1 = d->hint[pair][1];
   int h;
   const double nn[3] = {-n[0], -n[1], -n[2]};
+  const long climb0 = g_mpr_stats[2];
+  g_mpr_stats[8]++;
   h = h0;
   const int s1 = support_vertex(m, d, g1, n, &h);
   h = h1;
@@ -1493,6 +1498,9 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
       if (!dup) { fid[nc] = f; side[nc++] = sd; }
     }
   }
+  g_mpr_stats[9] += nc;
+  g_mpr_stats[10] += m->geom_facenum[g1] + m->geom_facenum[g2];
+  g_mpr_stats[15] += c1 + c2;
   double sep[64];
   double mx = -1e300;
   for (int k = 0; k < nc; k++) {
@@ -1538,6 +1546,10 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   const int nrv = m->face_vnum[best_f];
   for (int k = 0; k < np; k++) vert_world(m, d, gi, m->face_vert[m->face_vadr[inc_f] + k], poly[0][k]);
   for (int k = 0; k < nrv; k++) vert_world(m, d, gr, m->face_vert[m->face_vadr[best_f] + k], ref[k]);
+  g_mpr_stats[11]++;
+  g_mpr_stats[12] += nrv;
+  g_mpr_stats[13] += np;
+  g_mpr_stats[14] += g_mpr_stats[2] - climb0;
   for (int e = 0; e < nrv && np > 0; e++) {
     const double* A = ref[e];
     const double* B = ref[e + 1 == nrv ? 0 : e + 1];

@@ -29,6 +29,8 @@ st = torch.zeros(n, dtype=torch.int32, device="cuda")
 c4 = torch.empty((n, 4), device="cuda")
 th = torch.empty((n, 6 * H), device="cuda")
 td = torch.empty((n, 6 * H), device="cuda")
+if os.environ.get("THETA", "1") == "0":  # traffic attribution: no theta / thetadot outputs
+    th = td = None
 key = torch.empty(1, dtype=torch.int64, device="cuda")
 args = (xi, MPCR_LAYOUT_XI, q0, (20., 3., 80.), (-0.3, -0.3, 0.5), (0., 1., 0., 0.))
 for _ in range(2):

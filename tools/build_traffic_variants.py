@@ -5,7 +5,8 @@ passes on each).  Diagnostic builds only, never shipped:
   t_jl96   every J row of the narrow image in LDS (no HBM J slab)
   t_cprev  the previous-step slot distances in LDS (no HBM slot history)
   t_both   both (LDS images over the 16-blocks budget: fewer blocks per CU,
-           so only the counters, not the times, mean anything)"""
+           so only the counters, not the times, mean anything)
+  t_nopace pacing off (its slot table's loads and stores)"""
 import os
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -19,6 +20,7 @@ VARIANTS = {
     "t_jl96": ["-DMPCR_N_JL=96", "-DMPCR_N_LDS_UNCHECKED"],
     "t_cprev": ["-DMPCR_N_CPREV_GLOBAL=0", "-DMPCR_N_LDS_UNCHECKED"],
     "t_both": ["-DMPCR_N_JL=96", "-DMPCR_N_CPREV_GLOBAL=0", "-DMPCR_N_LDS_UNCHECKED"],
+    "t_nopace": ["-DMPCR_PACE=0"],
 }
 
 if __name__ == "__main__":

@@ -76,6 +76,9 @@ if [[ $STEPS == *pmc* ]]; then
     run pmc$i 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
   done
 fi
+if [[ $STEPS == *pmcc4* ]]; then  # instruction mix / VALU busy of the dual-arm shard
+  run pmc_c4 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_c4 -o run -- python3 bench.py --config c4 --no-cpu-baseline --no-contact-report --steps 2 --warmup 1
+fi
 if [[ $STEPS == *lat* ]]; then  # memory-latency levels of the rollout kernel (C3 bench command)
   run pmc_lat 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_SMEM SQ_INST_LEVEL_LDS SQ_WAIT_ANY --output-format csv -d $OUT/pmc_lat -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
 fi
@@ -84,16 +87,31 @@ if [[ $STEPS == *c5* ]]; then
   run c5_planner 200 python tools/bench_mpc.py --model planner_scene --ticks 30
 fi
 if [[ $STEPS == *phase* ]]; then  # needs libmpcr_prof.so (python tools/phase_profile.py --build, CPU container)
-  run phase_c4 200 env N=4096 H=100 python tools/phase_profile.py dual_arm $OUT/phase_c4.json
+  N=4096 H=100 run phase_c4 200 python tools/phase_profile.py dual_arm $OUT/phase_c4.json
+  N=4096 H=50 run phase_c3 200 python tools/phase_profile.py scene_mjx $OUT/phase_c3.json
+fi
+if [[ $STEPS == *wavec4* ]]; then
+  N=4096 H=100 run wavetime_c4 200 python tools/wavetime.py dual_arm $OUT/wavetime_c4.json
+fi
+if [[ $STEPS == *wpc* ]]; then  # one vs two waves per candidate (narrow variant) at the small-batch sizes
+  for nm in "1024 ur5e_hande_mjx" "512 scene_mjx" "1024 scene_mjx" "2048 scene_mjx" "4096 scene_mjx"; do
+    set -- $nm
+    for w in 0 8192; do
+      MPCR_WPC2_MAX_N=$w N=$1 MODEL=$2 R=20 run wpc_$2_$1_w$w 200 python tools/ab_time.py manipulator_mujoco_amd/libmpcr.so
+    done
+  done
 fi
 if [[ $STEPS == *wavetime* ]]; then
   N=4096 run wavetime 120 python tools/wavetime.py scene_mjx $OUT/wavetime_c3_4096.json
 fi
 if [[ $STEPS == *traffic* ]]; then  # HBM traffic attribution (build_variants/t_*.so, tools/build_traffic_variants.py)
-  for v in ${TRAFFIC_VARIANTS:-t_ship t_jl96 t_cprev t_both}; do
+  for v in ${TRAFFIC_VARIANTS:-t_ship t_jl96 t_cprev t_both t_nopace}; do
     for c in FETCH_SIZE WRITE_SIZE; do
       N=4096 R=3 run traffic_${v}_$c 120 rocprofv3 --pmc $c --output-format csv -d $OUT/traffic_${v}_$c -o run -- python3 tools/ab_time.py build_variants/$v.so
     done
+  done
+  for c in FETCH_SIZE WRITE_SIZE; do  # the shipped build without the theta / thetadot outputs
+    THETA=0 N=4096 R=3 run traffic_t_ship_notheta_$c 120 rocprofv3 --pmc $c --output-format csv -d $OUT/traffic_t_ship_notheta_$c -o run -- python3 tools/ab_time.py build_variants/t_ship.so
   done
 fi
 echo "[session] done"

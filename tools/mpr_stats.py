@@ -39,3 +39,8 @@ print(f"per step: mpr calls {s[0] / steps:.1f}, hits {s[4] / steps:.2f}, support
 h = s[16:64]
 print("support pairs per call: " + " ".join(f"{k}:{v}" for k, v in enumerate(h) if v))
 print(f"per call: support pairs {s[1] / max(s[0], 1):.2f}, climb rounds per support {s[2] / max(2 * s[1], 1):.2f}")
+if s[8]:
+    print(f"polyhedron manifold per step: calls {s[8] / steps:.2f}, reaching the clip {s[11] / steps:.2f}; per call: "
+          f"candidate faces {s[9] / s[8]:.1f} (support-vertex faces {s[15] / s[8]:.1f}), faces scanned "
+          f"{s[10] / s[8]:.0f}; per clip: reference vertices {s[12] / max(s[11], 1):.1f}, incident vertices "
+          f"{s[13] / max(s[11], 1):.1f}, climb rounds {s[14] / max(s[11], 1):.1f}")

@@ -14,7 +14,8 @@ PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rn
           "coll: box-box", "constraint rows", "newton: line search", "euler", "coll: narrow", "coll: cost+compact",
           "newton: warm start", "newton: grad/H/chol"]
 # slot 7 is the collision loop's tail (box-box moved to 16); 15 packs iteration counts
-EXTRA = {16: "coll: box-box (wave)", 17: "coll: convex narrow (MPR)", 18: "coll: convex emit"}
+EXTRA = {16: "coll: box-box (wave)", 21: "coll: convex narrow (MPR)", 22: "coll: plane-mesh manifold",
+         17: "coll: polyhedron manifold", 18: "coll: convex emit"}
 COUNTS = {19: "hull-climb rounds (wave level)", 20: "mesh support calls (wave level)"}
 
 
@@ -46,11 +47,11 @@ def main():
         xi = np.ascontiguousarray(xi[[int(i) for i in os.environ["SUBSET"].split(",")]])
         n = xi.shape[0]
     e = Engine(m, H, n, Pd)
-    ph = (ctypes.c_ulonglong * 24)()
+    ph = (ctypes.c_ulonglong * 32)()
     f = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
     w, pt, qt = np.array([20, 3, 80.]), np.array([-0.3, -0.3, 0.5]), np.array([0, 1, 0, 0.])
     for _ in range(2):
-        ph = (ctypes.c_ulonglong * 24)()
+        ph = (ctypes.c_ulonglong * 32)()
         _lib.check(lib.mpcr_rollout_profile(e.handle, xi.ctypes.data, MPCR_LAYOUT_XI, n,
                                             q0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), f(w), f(pt), f(qt), ph))
     tot = sum(ph[:15]) + sum(ph[i] for i in EXTRA)
@@ -60,6 +61,11 @@ def main():
     names.update(EXTRA)
     for i, p in names.items():
         print(f"  {p:26s} {ph[i] / n / H:10.0f} cyc  {100 * ph[i] / tot:5.1f}%")
+    sub = {23: "support vertices", 24: "cone face scan", 25: "SAT support queries", 26: "incident face + polygons",
+           27: "clip", 28: "picks"}
+    if any(ph[i] for i in sub):  # inside the polyhedron manifold (wave level, atomics per stamp)
+        for i, p in sub.items():
+            print(f"    poly: {p:24s} {ph[i] / n / H:10.0f} cyc")
     for i, p in COUNTS.items():
         print(f"  {p:34s} {ph[i] / n / H:8.2f} per wave-step")
     print(f"  Newton iterations per step: {(ph[15] & 0xFFFFFFFF) / n / H:.2f}, line-search passes per step: "
