@@ -87,6 +87,8 @@ struct mpcr_engine {
   int* d_face_vert = nullptr;
   int2* d_vert_finfo = nullptr;
   int* d_vert_face = nullptr;
+  int2* d_cone_cell = nullptr;
+  int* d_cone_face = nullptr;
   bool wide = false;  // kernel variant: rollout_kernel<32, 32, 72, true>
 };
 
@@ -823,6 +825,63 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     e->dev.face_vert = e->d_face_vert;
     e->dev.vert_finfo = e->d_vert_finfo;
     e->dev.vert_face = e->d_vert_face;
+    // the polyhedron manifold's cone table: per geom with faces and per
+    // cube-map cell of the local direction (CONE_R x CONE_R per cube face, the
+    // kernel's cone_cell order) every face whose outward normal lies within
+    // acos(CONE_COS) + the cell's angular radius + 0.01 rad of the cell centre
+    // -- a superset of the faces the kernel's cone test accepts for any
+    // direction in the cell (fp32 cell assignment included), ascending, so the
+    // scan of a cell's list compacts the same candidates in the same order as a
+    // scan of all the geom's faces
+    std::vector<int2> ccell;
+    std::vector<int> cface;
+    const double thr0 = std::acos(CONE_COS) + 0.01;
+    for (int i = 0; i < e->dev.ngeom; i++) {
+      e->dev.geom_coneadr[i] = -1;
+      const int fa = e->dev.geom_faceadr[i], fnum = e->dev.geom_facenum[i];
+      if (fa < 0 || fnum <= 0) continue;
+      e->dev.geom_coneadr[i] = (int)ccell.size();
+      for (int c = 0; c < CONE_CELLS; c++) {
+        const int fc = c / (CONE_R * CONE_R), iu = (c / CONE_R) % CONE_R, iv = c % CONE_R;
+        const int ax = fc / 2;
+        const double sa = (fc & 1) ? -1.0 : 1.0;
+        auto dir = [&](double u, double v, double out[3]) {
+          out[ax] = sa; out[(ax + 1) % 3] = u; out[(ax + 2) % 3] = v;
+          const double nn = std::sqrt(out[0] * out[0] + out[1] * out[1] + out[2] * out[2]);
+          for (int k = 0; k < 3; k++) out[k] /= nn;
+        };
+        const double u0 = -1.0 + 2.0 * iu / CONE_R, u1 = -1.0 + 2.0 * (iu + 1) / CONE_R;
+        const double v0 = -1.0 + 2.0 * iv / CONE_R, v1 = -1.0 + 2.0 * (iv + 1) / CONE_R;
+        double ctr[3], cr[3];
+        dir(0.5 * (u0 + u1), 0.5 * (v0 + v1), ctr);
+        double rad = 0.0;
+        for (double u : {u0, u1})
+          for (double v : {v0, v1}) {
+            dir(u, v, cr);
+            const double cd = ctr[0] * cr[0] + ctr[1] * cr[1] + ctr[2] * cr[2];
+            rad = std::max(rad, std::acos(std::min(1.0, cd)));
+          }
+        const double cth = std::cos(thr0 + rad);
+        const int start = (int)cface.size();
+        for (int f = fa; f < fa + fnum; f++) {
+          const double* fp = h.face_plane[f];
+          const double fn = std::sqrt(fp[0] * fp[0] + fp[1] * fp[1] + fp[2] * fp[2]);
+          if (fn > 0 && (fp[0] * ctr[0] + fp[1] * ctr[1] + fp[2] * ctr[2]) / fn >= cth) cface.push_back(f);
+        }
+        ccell.push_back(make_int2(start, (int)cface.size() - start));
+      }
+    }
+    if (cface.empty()) cface.push_back(0);
+    if (ccell.empty()) ccell.push_back(make_int2(0, 0));
+    if (hipMalloc(&e->d_cone_cell, sizeof(int2) * ccell.size()) != hipSuccess ||
+        hipMalloc(&e->d_cone_face, sizeof(int) * cface.size()) != hipSuccess ||
+        hipMemcpy(e->d_cone_cell, ccell.data(), sizeof(int2) * ccell.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_cone_face, cface.data(), sizeof(int) * cface.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      mpcr_engine_free(e);
+      return fail(MPCR_ENOMEM, "cone table upload failed");
+    }
+    e->dev.cone_cell = e->d_cone_cell;
+    e->dev.cone_face = e->d_cone_face;
   }
   const int nc = e->host.nctrl;
   const size_t in_cols = (size_t)nc * (horizon > nbasis ? horizon : nbasis);
@@ -886,6 +945,8 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_face_vert);
   (void)hipFree(e->d_vert_finfo);
   (void)hipFree(e->d_vert_face);
+  (void)hipFree(e->d_cone_cell);
+  (void)hipFree(e->d_cone_face);
   (void)hipFree(e->d_hull_vert);
   (void)hipFree(e->d_hull_info);
   (void)hipFree(e->d_hull_adjv);

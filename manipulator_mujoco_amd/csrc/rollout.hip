@@ -711,6 +711,7 @@ __device__ __forceinline__ int climb_round(const DevModel* __restrict__ m, int v
 // cube-map cell of a local direction (the model's hull_lut order, oracle
 // lut_cell): major axis (lowest on ties), its sign, the other two components
 // (cyclic order) over |l_axis| in MPCR_LUT_R bins
+template <int R = MPCR_LUT_R>
 __device__ __forceinline__ int lut_cell(const float l[3]) {
   const float a0 = fabsf(l[0]), a1 = fabsf(l[1]), a2 = fabsf(l[2]);
   const int ax = (a0 >= a1 && a0 >= a2) ? 0 : (a1 >= a2 ? 1 : 2);
@@ -719,7 +720,6 @@ __device__ __forceinline__ int lut_cell(const float l[3]) {
   const float lv = ax == 0 ? l[2] : (ax == 1 ? l[0] : l[1]);
   const float la = fabsf(lax);
   if (!(la > 0.f)) return 0;
-  constexpr int R = MPCR_LUT_R;
   const int iu = min(max((int)floorf((lu / la + 1.f) * 0.5f * R), 0), R - 1);
   const int iv = min(max((int)floorf((lv / la + 1.f) * 0.5f * R), 0), R - 1);
   return (2 * ax + (lax < 0.f ? 1 : 0)) * R * R + iu * R + iv;
@@ -1115,6 +1115,7 @@ __device__ __noinline__ void plane_mesh_manifold_wave(const DevModel* __restrict
 
 constexpr int kPendingManifold = -4;  // narrow_lane: plane-mesh pair awaiting plane_mesh_manifold_wave
 constexpr float kPolyConeCos = 0.94f;  // ~20 degrees: candidate faces' Gauss-map cone about MPR's normal
+static_assert(kPolyConeCos == (float)CONE_COS, "the host's cone table is built for this cone");
 constexpr int kPendingPoly = -5;      // narrow_lane: polyhedron pair hit by MPR, awaiting poly_manifold_wave
 
 // hull vertex index of geom g's support point along dir (world): the mesh
@@ -1196,29 +1197,43 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
   // within the Gauss-map cone of n (g1) / -n (g2), face index order, those
   // already listed skipped -- a ballot-compacted scan of both face tables into
   // an LDS list (the clip buffer's second half, free until the clip)
+  // The faces scanned are the host's cone table entries for the cube-map cell
+  // of the local direction (DevModel::cone_cell: a superset of the faces the
+  // test below accepts, ascending), not all of the geom's faces (up to 5219
+  // on the dual arm's hulls): the same candidates in the same order.  The
+  // support-vertex faces of each side sit one per lane (lane k: entry k) and
+  // the duplicate test reads them with readlane.
   int* const cl = reinterpret_cast<int*>(&s.polyw[1][0][0]);
   int nc = ns;
+  const int vf1 = lane < c1 ? m->vert_face[i1.x + lane] : -1, vf2 = lane < c2 ? m->vert_face[i2.x + lane] : -1;
 #pragma unroll 1
   for (int sd = 0; sd < 2; sd++) {
-    const int g = sd ? g2 : g1, fa = m->geom_faceadr[g], fnum = m->geom_facenum[g];
-    const int2 li = sd ? i2 : i1;
-    const int cs = sd ? c2 : c1;
+    const int g = sd ? g2 : g1;
+    const int cs = sd ? c2 : c1, vfs = sd ? vf2 : vf1;
     const float sg = sd ? -1.f : 1.f;
+    float l[3];
+    {
+      const float dn[3] = {sg * n[0], sg * n[1], sg * n[2]};
+      mtv(l, s.gxmat[g], dn);
+    }
+    const int2 cc = m->cone_cell[m->geom_coneadr[g] + lut_cell<CONE_R>(l)];
 #pragma unroll 1
-    for (int b0 = 0; b0 < fnum && nc < WAVE; b0 += WAVE) {
+    for (int b0 = 0; b0 < cc.y && nc < WAVE; b0 += WAVE) {
       bool sel = false;
-      if (b0 + lane < fnum) {
-        const float4 fp = m->face_plane[fa + b0 + lane];
+      int f = -1;
+      if (b0 + lane < cc.y) {
+        f = m->cone_face[cc.x + b0 + lane];
+        const float4 fp = m->face_plane[f];
         const float nl[3] = {fp.x, fp.y, fp.z};
         float nw[3];
         mv(nw, s.gxmat[g], nl);
         sel = sg * (nw[0] * n[0] + nw[1] * n[1] + nw[2] * n[2]) >= kPolyConeCos;
-        if (sel)
-          for (int k = 0; k < cs; k++) sel &= m->vert_face[li.x + k] != fa + b0 + lane;
       }
+#pragma unroll 1
+      for (int k = 0; k < cs; k++) sel &= __builtin_amdgcn_readlane(vfs, k) != f;
       int tot;
       const int o = wscan_excl(sel ? 1 : 0, tot);
-      if (sel && nc + o < WAVE) cl[nc - ns + o] = (fa + b0 + lane) | (sd << 24);
+      if (sel && nc + o < WAVE) cl[nc - ns + o] = f | (sd << 24);
       nc = min(nc + tot, WAVE);
     }
   }
@@ -1262,6 +1277,12 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
   const int gr = rtwo ? g2 : g1, gi = rtwo ? g1 : g2;
   float nr[3], offr;
   face_rel(m, s, gr, fr, c, nr, offr);
+  // the reference polygon's vertices (lane k: vertex k), loaded here so their
+  // latency hides behind the incident face's support climb
+  const int2 fri = m->face_vinfo[fr];
+  const int nrv = fri.y;
+  float A[3] = {0.f, 0.f, 0.f}, sn[3];
+  if (lane < nrv) vert_rel(m, s, gr, m->face_vert[fri.x + lane], c, A);
   // incident face: the most anti-parallel face on gi's support vertex along -nr
   int si = 0;
   if (lane == 0) {
@@ -1290,10 +1311,8 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, 
   const int fi = __shfl(finc, __builtin_ctzll(bma));
   // reference polygon (lane k: vertex k and its edge's outward side-plane
   // normal), incident polygon into the clip buffer
-  const int2 fri = m->face_vinfo[fr], fii = m->face_vinfo[fi];
-  const int nrv = fri.y, ninc = fii.y;
-  float A[3] = {0.f, 0.f, 0.f}, sn[3];
-  if (lane < nrv) vert_rel(m, s, gr, m->face_vert[fri.x + lane], c, A);
+  const int2 fii = m->face_vinfo[fi];
+  const int ninc = fii.y;
   {
     const int ln = lane + 1 >= nrv ? 0 : lane + 1;
     const float ed[3] = {__shfl(A[0], ln) - A[0], __shfl(A[1], ln) - A[1], __shfl(A[2], ln) - A[2]};
