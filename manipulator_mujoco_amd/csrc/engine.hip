@@ -778,10 +778,10 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       mpcr_engine_free(e);
       return fail(MPCR_ENOMEM, "hull upload failed");
     }
-    e->dev.hull_vert = e->d_hull_vert;
-    e->dev.hull_info = e->d_hull_info;
-    e->dev.hull_adjv = e->d_hull_adjv;
-    e->dev.hull_head = e->d_hull_head;
+    e->dev.hull_vert = as_gmem(e->d_hull_vert);
+    e->dev.hull_info = as_gmem(e->d_hull_info);
+    e->dev.hull_adjv = as_gmem(e->d_hull_adjv);
+    e->dev.hull_head = as_gmem(e->d_hull_head);
     std::vector<float4> hl(MPCR_MAX_HULLLUT);
     int nlut = 0;
     for (int g = 0; g < h.ngeom; g++)
@@ -795,7 +795,7 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       mpcr_engine_free(e);
       return fail(MPCR_ENOMEM, "hull table upload failed");
     }
-    e->dev.hull_lut = e->d_hull_lut;
+    e->dev.hull_lut = as_gmem(e->d_hull_lut);
   }
   if (e->host.nface > 0) {  // polygon faces + vertex incidence, pointed to by the device model
     const mpcr_model_t& h = e->host;
@@ -820,11 +820,11 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       mpcr_engine_free(e);
       return fail(MPCR_ENOMEM, "face upload failed");
     }
-    e->dev.face_plane = e->d_face_plane;
-    e->dev.face_vinfo = e->d_face_vinfo;
-    e->dev.face_vert = e->d_face_vert;
-    e->dev.vert_finfo = e->d_vert_finfo;
-    e->dev.vert_face = e->d_vert_face;
+    e->dev.face_plane = as_gmem(e->d_face_plane);
+    e->dev.face_vinfo = as_gmem(e->d_face_vinfo);
+    e->dev.face_vert = as_gmem(e->d_face_vert);
+    e->dev.vert_finfo = as_gmem(e->d_vert_finfo);
+    e->dev.vert_face = as_gmem(e->d_vert_face);
     // the polyhedron manifold's cone table: per geom with faces and per
     // cube-map cell of the local direction (CONE_R x CONE_R per cube face, the
     // kernel's cone_cell order) every face whose outward normal lies within
@@ -880,8 +880,8 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       mpcr_engine_free(e);
       return fail(MPCR_ENOMEM, "cone table upload failed");
     }
-    e->dev.cone_cell = e->d_cone_cell;
-    e->dev.cone_face = e->d_cone_face;
+    e->dev.cone_cell = as_gmem(e->d_cone_cell);
+    e->dev.cone_face = as_gmem(e->d_cone_face);
   }
   const int nc = e->host.nctrl;
   const size_t in_cols = (size_t)nc * (horizon > nbasis ? horizon : nbasis);

@@ -33,6 +33,21 @@ constexpr int CONE_R = 8;
 constexpr int CONE_CELLS = 6 * CONE_R * CONE_R;
 constexpr double CONE_COS = 0.94;  // the kernel's and the oracle's cone (rollout.hip kPolyConeCos)
 
+// The model's table pointers are global memory: typed so in the device pass
+// (same 8-byte layout as the host's plain pointers), so the kernel's loads
+// through them are global_load, not flat_load (a flat load counts against the
+// LDS wait counter too, and waits for an LDS read then also wait for it)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MPCR_GMEM __attribute__((address_space(1)))
+#else
+#define MPCR_GMEM
+#endif
+// host side: a device allocation as the model's table pointer type
+template <class T>
+inline const MPCR_GMEM T* as_gmem(T* p) {
+  return (const MPCR_GMEM T*)p;
+}
+
 // body kinds for the kinematics pass
 enum { BK_STATIC = 0, BK_FREE = 1, BK_HINGE = 2, BK_SLIDE = 3, BK_WELD = 4 };
 
@@ -126,25 +141,25 @@ struct DevModel {
   int geom_hulladr[DX_NG];
   int geom_hullnum[DX_NG];
   int geom_lutadr[DX_NG];  // first hull_lut cell, -1: no table
-  const float4* hull_vert;  // xyz | degree (int bits in w)
-  const int2* hull_info;    // (adjacency start, count) per vertex
-  const float4* hull_adjv;  // neighbour xyz | (index | degree << 16) (bits in w): one load per neighbour
-  const float4* hull_lut;   // support start table records (as hull_adjv), MPCR_LUT_R cube-map cells per hull
+  const MPCR_GMEM float4* hull_vert;  // xyz | degree (int bits in w)
+  const MPCR_GMEM int2* hull_info;    // (adjacency start, count) per vertex
+  const MPCR_GMEM float4* hull_adjv;  // neighbour xyz | (index | degree << 16) (bits in w): one load per neighbour
+  const MPCR_GMEM float4* hull_lut;   // support start table records (as hull_adjv), MPCR_LUT_R cube-map cells per hull
   unsigned long long* prof;  // wave-level event counters (MPCR_PROFILE builds; else null)
-  const float4* hull_head;  // per vertex its first 8 neighbour records as hull_adjv, padded with NaN records:
+  const MPCR_GMEM float4* hull_head;  // per vertex its first 8 neighbour records as hull_adjv, padded with NaN records:
                             // a climb round addresses them from the vertex index alone (no hull_info load)
   // polygon faces of polyhedron-pair geoms (mesh-mesh / box-mesh manifold) ----
   int geom_faceadr[DX_NG];   // first face, -1: none
   int geom_facenum[DX_NG];   // its face count
   int geom_cornadr[DX_NG];   // a box's 8 corners in hull_vert (bit k: + side of axis k), -1: none
-  const float4* face_plane;  // outward normal xyz | offset (n . x = offset), geom frame
-  const int2* face_vinfo;    // (first face_vert entry, count <= MPCR_FACE_MAXV)
-  const int* face_vert;      // hull_vert indices, counter-clockwise about the normal
-  const int2* vert_finfo;    // per hull vertex: (first vert_face entry, count)
-  const int* vert_face;      // face indices
+  const MPCR_GMEM float4* face_plane;  // outward normal xyz | offset (n . x = offset), geom frame
+  const MPCR_GMEM int2* face_vinfo;    // (first face_vert entry, count <= MPCR_FACE_MAXV)
+  const MPCR_GMEM int* face_vert;      // hull_vert indices, counter-clockwise about the normal
+  const MPCR_GMEM int2* vert_finfo;    // per hull vertex: (first vert_face entry, count)
+  const MPCR_GMEM int* vert_face;      // face indices
   int geom_coneadr[DX_NG];   // first cone_cell record (CONE_CELLS per geom with faces), -1: none
-  const int2* cone_cell;     // (first cone_face entry, count) per cell
-  const int* cone_face;      // face indices, ascending within a cell: a superset of the faces the
+  const MPCR_GMEM int2* cone_cell;     // (first cone_face entry, count) per cell
+  const MPCR_GMEM int* cone_face;      // face indices, ascending within a cell: a superset of the faces the
                              // cone test can accept for any direction in the cell
 
   int ctrl_qposadr[DX_NCTRL], ctrl_dofadr[DX_NCTRL];

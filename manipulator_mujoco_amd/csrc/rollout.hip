@@ -122,6 +122,30 @@ namespace mpcr {
 // ---------------------------------------------------------------------------
 // wave helpers
 
+// Address spaces at the entry of a non-inlined device function: its pointer
+// arguments are generic, so without these the model reads, the LDS image and
+// the caller's contact arrays all go through flat instructions (which also
+// count against the LDS wait counter)
+// (device pass only: the host pass parses device bodies with other builtin signatures)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ASSUME_GLOBAL(p) __builtin_assume(!__builtin_amdgcn_is_shared((const void*)(p)) && \
+                                          !__builtin_amdgcn_is_private((const void*)(p)))
+#define ASSUME_LDS(p) __builtin_assume(__builtin_amdgcn_is_shared((const void*)(p)))
+#define ASSUME_PRIVATE(p) __builtin_assume(__builtin_amdgcn_is_private((const void*)(p)))
+#else
+#define ASSUME_GLOBAL(p)
+#define ASSUME_LDS(p)
+#define ASSUME_PRIVATE(p)
+#endif
+// the model pointer as a wave-uniform (SGPR) global pointer: a non-inlined
+// function receives it in VGPRs, and its field reads then become per-lane
+// vector loads instead of scalar ones
+__device__ __forceinline__ const MPCR_GMEM DevModel* uniform_model(const DevModel* p) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return reinterpret_cast<const MPCR_GMEM DevModel*>(((unsigned long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ float rdlane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -1016,9 +1040,12 @@ __device__ __forceinline__ float wmax(float v) {
 // of four serial per-lane scans (a 2691-vertex hull touching the table made a
 // handful of dual-arm candidates 3x slower than the rest).
 template <class S>
-__device__ __noinline__ void plane_mesh_manifold_wave(const DevModel* __restrict__ m, const S& s, int g,
-                                                      const float n[3], const float* xp, float depth, int q, int lane,
+__device__ __noinline__ void plane_mesh_manifold_wave(const DevModel* __restrict__ m_, const S& s, int g,
+                                                      const float n_[3], const float* xp_, float depth, int q, int lane,
                                                       float dist[4], float pos[4][3], float nrm[4][3], int& nsl) {
+  const MPCR_GMEM DevModel* __restrict__ m = uniform_model(m_);
+  ASSUME_LDS(&s); ASSUME_PRIVATE(dist); ASSUME_PRIVATE(pos); ASSUME_PRIVATE(nrm); ASSUME_PRIVATE(&nsl);
+  const float n[3] = {n_[0], n_[1], n_[2]}, xp[3] = {xp_[0], xp_[1], xp_[2]};  // in registers (no alias reloads)
   const float* R = s.gxmat[g];
   const float* xg = s.gxpos[g];
   float nl[3], pl[3];
@@ -1027,7 +1054,7 @@ __device__ __noinline__ void plane_mesh_manifold_wave(const DevModel* __restrict
   mtv(pl, R, dx);
   const float thr = fmaxf(0.f, depth - 1e-3f);
   const int v0 = m->geom_hulladr[g], v1 = v0 + m->geom_hullnum[g];
-  const float4* __restrict__ hv = m->hull_vert;
+  const MPCR_GMEM float4* __restrict__ hv = m->hull_vert;
   auto sup = [&](const float4& v) { return (pl[0] - v.x) * nl[0] + (pl[1] - v.y) * nl[1] + (pl[2] - v.z) * nl[2]; };
   int ia = -1, il = -1;
   for (int base = v0; base < v1; base += WAVE) {
@@ -1173,9 +1200,13 @@ __device__ __forceinline__ void vert_rel(const DevModel* __restrict__ m, const S
 // _manifold_points picks as wave maxima.  Coordinates relative to g2's
 // centre, as MPR's.
 template <class S>
-__device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m, S& s, const short* hints, int p,
-                                                const float n[3], float depth, int q, int lane, float dist[4],
+__device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hints, int p,
+                                                const float n_[3], float depth, int q, int lane, float dist[4],
                                                 float pos[4][3], float nrm[4][3], int& nsl) {
+  const MPCR_GMEM DevModel* __restrict__ m = uniform_model(m_);
+  ASSUME_GLOBAL(hints); ASSUME_LDS(&s); ASSUME_PRIVATE(dist); ASSUME_PRIVATE(pos); ASSUME_PRIVATE(nrm);
+  ASSUME_PRIVATE(&nsl);
+  const float n[3] = {n_[0], n_[1], n_[2]};  // in registers (no alias reloads)
   PSTAMP_DECL
   const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
   const float c[3] = {s.gxpos[g2][0], s.gxpos[g2][1], s.gxpos[g2][2]};
