@@ -3685,6 +3685,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           const float gauss = hsum<S::CPW>(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
           const float cost = 0.5f * gauss + 0.5f * hsum<S::CPW>(cc);
           sync();
+          STAMP(29);
           constexpr bool MFMA_HESS = NVW == 16 && S::CPW == 1 && MPCR_MFMA_HESS;
           constexpr bool MFMA_HESS_W = NVW == 32 && S::CPW == 1 && MPCR_MFMA_HESS_W;
           constexpr int RPW = S::HL / NVW;
@@ -3744,6 +3745,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
             for (int o = NVW; o < S::HL; o <<= 1) qc += __shfl_xor(qc, o);
             grad = lane < nv ? ma - s.qfs[lane] - qc : 0.f;
           }
+          STAMP(30);
           const float gn = sqrtf(hsum<S::CPW>(grad * grad));
           // MuJoCo's stop test, plus its fp32 floor: an improvement within ~8 ulp
           // of the cost is rounding noise (without it fp32 iterates on noise
@@ -3817,6 +3819,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
             for (int k = 0; k < QPL; k++) reinterpret_cast<float4*>(Hs + gi * S::LD)[gq + RPW * k] = hq[k];
             sync();
           }
+          STAMP(31);
           float mg;
           if (S::CPW == 1 && !coupled && blk_usable<NVW>(m)) {
             // no row couples two trees: H is block diagonal like M
@@ -3930,6 +3933,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           if (improved && lane < NVW) s.qacc[lane] = s.qacc[lane] + alpha * s.srch[lane];
           prev_cost = cost;
           sync();
+          STAMP(9);
         }
       } else {
         if (lane < NVW) s.qacc[lane] = qacc_l;

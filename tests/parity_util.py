@@ -119,7 +119,8 @@ def check(m, g_cost, o, sens, label="", strict_well=True):
     stats["well_miss_allowed"] = float((bw + _sigma3(bw, nw)) * max(nw, 1))
     ig, io = int(np.argmin(g)), int(np.argmin(oc))
     ug, uo = max(TOL, sens[ig], pb[ig], pf[ig]), max(TOL, sens[io], pb[io], pf[io])
-    stats.update(sel_gpu=ig, sel_oracle=io, sel_rel=float(rel[ig]), sel_gap=float((oc[ig] - oc[io]) / abs(oc[io])))
+    stats.update(sel_gpu=ig, sel_oracle=io, sel_rel=float(rel[ig]), sel_gap=float((oc[ig] - oc[io]) / abs(oc[io])),
+                 sel_cond=float(ug), sel_probe_f=float(pf[ig]))
     _log(label, stats)
     assert not strict_well or stats["well_miss"] <= stats["well_miss_allowed"], (
         label, "well-conditioned misses beyond probe B's",

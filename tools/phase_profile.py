@@ -12,9 +12,9 @@ from manipulator_mujoco_amd import _lib, basis, build, models  # noqa: E402
 
 PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rne", "M/bias", "M solve",
           "coll: box-box", "constraint rows", "newton: line search", "euler", "coll: narrow", "coll: cost+compact",
-          "newton: warm start", "newton: grad/H/chol"]
+          "newton: warm start", "newton: factor/solve"]
 # slot 7 is the collision loop's tail (box-box moved to 16); 15 packs iteration counts
-EXTRA = {16: "coll: box-box (wave)", 21: "coll: convex narrow (MPR)", 22: "coll: plane-mesh manifold",
+EXTRA = {29: "newton: jar/cost", 30: "newton: J^T f + grad", 31: "newton: Hessian", 16: "coll: box-box (wave)", 21: "coll: convex narrow (MPR)", 22: "coll: plane-mesh manifold",
          17: "coll: polyhedron manifold", 18: "coll: convex emit"}
 COUNTS = {19: "hull-climb rounds (wave level)", 20: "mesh support calls (wave level)"}
 
