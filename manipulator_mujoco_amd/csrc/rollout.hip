@@ -106,6 +106,10 @@ namespace mpcr {
                                       // C3 512 / 1024 / 2048: 1.38 / 1.43 / 1.52 -> 1.07 / 1.09 / 1.20 ms,
                                       // 4096: 1.77 -> 3.03 ms, the one-wave kernel stays)
 #endif
+// wide Newton's J^T f / J^T D J on two MFMA accumulators with batched row loads
+#ifndef MPCR_W_MFMA_SPLIT
+#define MPCR_W_MFMA_SPLIT 0  // measured: C4 50.97 vs 50.90 ms (noise), results move by an ulp: not kept
+#endif
 #ifndef MPCR_TD_TABLE
 #define MPCR_TD_TABLE 1
 #endif
@@ -1399,8 +1403,26 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m_,
   const int nk = __popcll(km);
   sync();  // the clip buffer is free for the next pair
   PSTAMP(m, 27);
+  const float sg = rtwo ? -1.f : 1.f;  // contact normal g1 -> g2
   if (nk == 0) {
-    if (lane == q) nsl = 1;
+    // no clipped point below the reference plane (a small reference face
+    // over a deep penetration): the SAT axis still carries the contact, one
+    // point at gi's support vertex along -nr (the oracle's rule; MPR's own
+    // normal for a penetration this deep is path-dependent)
+    float w[3];
+    vert_rel(m, s, gi, si, c, w);
+    const float dk = nr[0] * w[0] + nr[1] * w[1] + nr[2] * w[2] - offr;
+    if (lane == q) {
+      if (dk < m->pair_margin[p]) {
+        dist[0] = dk;
+        dist[1] = dist[2] = dist[3] = 1e30f;
+#pragma unroll
+        for (int e = 0; e < 3; e++) { pos[0][e] = w[e] - 0.5f * dk * nr[e] + c[e]; nrm[0][e] = sg * nr[e]; }
+        nsl = 4;
+      } else {
+        nsl = 1;
+      }
+    }
     return;
   }
   int idx[4] = {-1, -1, -1, -1};
@@ -1441,7 +1463,6 @@ __device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m_,
     const int iap = pick(fabsf((a[0] - P[0]) * ac[0] + (a[1] - P[1]) * ac[1] + (a[2] - P[2]) * ac[2]), bap);
     idx[0] = ia; idx[1] = ib; idx[2] = ic; idx[3] = beats(bap, bbp) ? iap : ibp;
   }
-  const float sg = rtwo ? -1.f : 1.f;  // contact normal g1 -> g2
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     bool dup = idx[j] < 0;
@@ -2439,7 +2460,35 @@ __device__ __forceinline__ mfx4 mm16(AF&& af, BF&& bf, mfx4 acc, int lane) {
 template <class S, class BF>
 __device__ __forceinline__ mfx16 mfma_rows32(const S& s, const float* gx, int nefc, int gi, int gq, BF&& bf,
                                              mfx16 acc) {
-  static_assert(S::JL % 2 == 0, "a row pair never straddles the LDS / slab boundary");
+  static_assert(S::JL % 8 == 0, "a row group never straddles the LDS / slab boundary");
+#if MPCR_W_MFMA_SPLIT
+  // two accumulators (row groups alternate), four row pairs' operands loaded
+  // before their MFMAs: the dependent 32x32x2 chain and the LDS / slab loads
+  // feeding it overlap (the sum is reassociated once at the end)
+  mfx16 acc2;
+#pragma unroll
+  for (int v = 0; v < 16; v++) acc2[v] = 0.f;
+  for (int r0 = 0; r0 < nefc; r0 += 8) {
+    float a[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int r = r0 + 2 * u + gq;
+      a[u] = r < nefc ? (r < S::JL ? s.J[r][gi] : gx[(r - S::JL) * S::LDJ + gi]) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int r = r0 + 2 * u + gq;
+      bv[u] = r < nefc ? bf(r, a[u]) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u += 2) {
+      if (r0 + 2 * u < nefc) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], bv[u], acc, 0, 0, 0);
+      if (r0 + 2 * u + 2 < nefc) acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u + 1], bv[u + 1], acc2, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < 16; v++) acc[v] += acc2[v];
+#else
   const int n1 = nefc < S::JL ? nefc : S::JL;
   for (int r0 = 0; r0 < n1; r0 += 2) {
     const int r = r0 + gq;
@@ -2463,6 +2512,7 @@ __device__ __forceinline__ mfx16 mfma_rows32(const S& s, const float* gx, int ne
       }
     }
   }
+#endif
   return acc;
 }
 

@@ -980,8 +980,7 @@ static int lut_cell(const double l[3]) {
 
 /* MPR work counters of the calling thread (diagnostic: tools/mpr_stats.py, workers = 1):
    0 calls, 1 support pairs, 2 climb rounds, 3 neighbour evaluations, 4 hits,
-   5 discovery iterations, 6 phase-2 iterations, 7 phase-3 iterations,
-   polyhedron manifold: 8 calls, 9 candidate faces, 10 faces scanned for the
+   polyhedron manifold: 5 clips that keep no point (the support-vertex contact), 8 calls, 9 candidate faces, 10 faces scanned for the
    cone, 11 calls reaching the clip, 12 reference-polygon vertices, 13
    incident-polygon vertices, 14 climb rounds, 15 support-vertex faces,
    16.. histogram of support pairs per call (capped at 47) */
@@ -1580,7 +1579,24 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
     if (dk < margin) { memcpy(pts[nk], poly[cur][k], sizeof(double) * 3); dist[nk++] = dk; }
   }
   PROBE(9, best_f); PROBE(10, inc_f); PROBE(11, nk);
-  if (nk == 0) return 0;
+  const double sg = gr == g1 ? 1.0 : -1.0; /* contact normal g1 -> g2 */
+  const double cn[3] = {sg * nr[0], sg * nr[1], sg * nr[2]};
+  if (nk == 0) {
+    /* no clipped point below the reference plane (a small reference face over
+       a deep penetration): the SAT axis still carries the contact -- one point
+       at gi's support vertex along -nr, at its distance from the reference
+       plane (MPR's own normal for a penetration this deep is the portal face
+       it ends on, a path that fp32 and fp64 take differently) */
+    g_mpr_stats[5]++;
+    double P[3], pos[3];
+    vert_world(m, d, gi, si, P);
+    const double dk = dot3(nr, P) - offr;
+    if (!(dk < margin)) return 0;
+    for (int c = 0; c < 3; c++) pos[c] = P[c] - 0.5 * dk * nr[c];
+    set_contact(&out[0], dk, pos, cn);
+    PROBE(8, 2);
+    return 1;
+  }
   PROBE(8, 1);
   /* at most 4: _manifold_points' picks (a = the first, b = the farthest from
      a, c = the farthest from line ab, d = the farthest from edge bc or ac;
@@ -1616,8 +1632,6 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
 #undef PICK
     idx[3] = beats(best_ap, best_bp) ? iap : ibp;
   }
-  const double sg = gr == g1 ? 1.0 : -1.0; /* contact normal g1 -> g2 */
-  const double cn[3] = {sg * nr[0], sg * nr[1], sg * nr[2]};
   for (int s = 0; s < cnt; s++) {
     int dup = 0;
     for (int t = 0; t < s; t++) dup |= idx[t] == idx[s];

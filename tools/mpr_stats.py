@@ -43,4 +43,5 @@ if s[8]:
     print(f"polyhedron manifold per step: calls {s[8] / steps:.2f}, reaching the clip {s[11] / steps:.2f}; per call: "
           f"candidate faces {s[9] / s[8]:.1f} (support-vertex faces {s[15] / s[8]:.1f}), faces scanned "
           f"{s[10] / s[8]:.0f}; per clip: reference vertices {s[12] / max(s[11], 1):.1f}, incident vertices "
-          f"{s[13] / max(s[11], 1):.1f}, climb rounds {s[14] / max(s[11], 1):.1f}")
+          f"{s[13] / max(s[11], 1):.1f}, climb rounds {s[14] / max(s[11], 1):.1f}; clips keeping no point "
+          f"{s[5] / steps:.3f} per step")
