@@ -96,7 +96,7 @@ struct mpcr_engine {
 // joint equalities only) covers the single-arm scenes; anything else runs the
 // wide one (dual-arm class).
 static bool needs_wide(const mpcr_model_t& m, const DevModel& d) {
-  if (m.nv > 16 || d.nbody > 16 || d.ngeom > 24 || m.nq > 24 || m.nu > 0 || d.has_spring ||
+  if (m.nv > 16 || d.nbody > 16 || d.ngeom > 24 || m.nq > MPCR_N_NQ || m.nu > 0 || d.has_spring ||
       m.integrator != MPCR_INT_EULER || m.cone != MPCR_CONE_PYRAMIDAL || m.nten > 0 || m.viscosity != 0)
     return true;
   for (int e = 0; e < m.neq; e++)

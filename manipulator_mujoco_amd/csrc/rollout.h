@@ -77,6 +77,11 @@ struct RolloutArgs {
 // reading 16 different rows hit distinct bank quads (LD*r mod 64 distinct
 // multiples of 4 for LD = 20 and 36) -> conflict free, 4x fewer LDS
 // instructions than b32.
+// qpos entries of the narrow image (the engine sends larger models to the wide
+// variant; the single-arm scenes have nq <= 15)
+#ifndef MPCR_N_NQ
+#define MPCR_N_NQ 20
+#endif
 template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false,
           int JL_ = MAXEFC_, int CPW_ = 1, int MAXACT_ = DX_MAXACT, bool SPLIT_ = false>
 struct __align__(16) SmemT {
@@ -95,7 +100,7 @@ struct __align__(16) SmemT {
   static constexpr bool CPREV_GLOBAL = CPREV_GLOBAL_;     // previous slot distances in HBM (L2) instead of LDS
   static constexpr int LOG_NVW = NVW_ == 32 ? 5 : 4;
   static constexpr bool WIDE = NVW_ == 32;  // dual-arm class: equalities, actuators, convex hulls
-  static constexpr int NQW = WIDE ? DX_NQ : 24, NEQP = WIDE ? DX_NEQ : 1, NACT = WIDE ? DX_NU : 1;
+  static constexpr int NQW = WIDE ? DX_NQ : MPCR_N_NQ, NEQP = WIDE ? DX_NEQ : 1, NACT = WIDE ? DX_NU : 1;
   static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
   static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
   static constexpr int PMAXW = 2 * MPCR_FACE_MAXV + 2;  // clipped incident face: <= its vertices + one per side plane
@@ -169,7 +174,7 @@ struct __align__(16) SmemT {
   };
 };
 // The two variants: single-arm scenes (nv <= 16) and the dual-arm class.
-// Single-arm image: 96 constraint rows of which the first 36 keep their J row
+// Single-arm image: 96 constraint rows of which the first 40 keep their J row
 // in LDS (stride 16) and the rest in a per-candidate HBM slab (RolloutArgs::jx;
 // the per-step row count is ~23 on average, p50 of a candidate's busiest step
 // 39, so the slab serves a minority of the rows), the contacts overlaid with
@@ -183,7 +188,7 @@ struct __align__(16) SmemT {
 #define MPCR_N_MAXEFC DX_MAXEFC
 #endif
 #ifndef MPCR_N_JL
-#define MPCR_N_JL 36
+#define MPCR_N_JL 40  // 36 -> 40 with the 20-entry qpos image: the budget exactly (C3 1.616 -> 1.610 ms)
 #endif
 #ifndef MPCR_N_LDJ
 #define MPCR_N_LDJ 16
