@@ -580,6 +580,9 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
   for (int p = d.cvx_base; p < m.npair; p++)
     if (m.pair_func[p] < MPCR_COL_CONVEX) return fail(MPCR_EMODEL, "convex pairs must be sorted last");
   if (m.npair - d.cvx_base > 512) return fail(MPCR_EMODEL, "%d general-convex pairs > 512", m.npair - d.cvx_base);
+  d.coll_rows = m.npair <= WAVE;  // DevModel::coll_rows: a light collision phase
+  for (int p = 0; p < m.npair; p++)
+    if (m.pair_func[p] == MPCR_COL_BOX_BOX) d.coll_rows = 0;
   if (m.nhullv > 32767) return fail(MPCR_EMODEL, "hull vertex table exceeds 16-bit hints");
   for (int p = 0; p < m.npair; p++) {
     int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];

@@ -2646,6 +2646,48 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
   unsigned wt_newton = 0, wt_ls = 0, wt_cvx = 0;  // Newton iterations, line-search passes, convex flush chunks
 #endif
 
+  // motion subspaces cdof (lanes over dofs): in the dynamics phase, or --
+  // two waves per candidate -- before the first barrier, since the collision
+  // wave's constraint rows need them
+  auto cdof_phase = [&]() {
+    if (lane < nv) {
+      const int bd = m->dof_body[lane], kind = m->dof_kind[lane];
+      const int tr = m->body_tree[bd];
+      float* c = s.cdof[lane];
+      float R[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = s.xmat[bd][k];
+      if (kind == 2) {  // free translation
+        c[0] = c[1] = c[2] = 0.f;
+        const int k = m->dof_sub[lane];
+        c[3] = k == 0 ? 1.f : 0.f;
+        c[4] = k == 1 ? 1.f : 0.f;
+        c[5] = k == 2 ? 1.f : 0.f;
+      } else {
+        float ax[3], anchor[3];
+        if (kind == 3) {
+          const int k = m->dof_sub[lane];
+          ax[0] = s.xmat[bd][k]; ax[1] = s.xmat[bd][3 + k]; ax[2] = s.xmat[bd][6 + k];  // by index, no selects
+          anchor[0] = s.xpos[bd][0]; anchor[1] = s.xpos[bd][1]; anchor[2] = s.xpos[bd][2];
+        } else {
+          const int j = m->dof_jnt[lane];
+          float w[3];
+          mv(ax, R, m->jnt_axis[j]);
+          mv(w, R, m->jnt_pos[j]);
+          anchor[0] = s.xpos[bd][0] + w[0]; anchor[1] = s.xpos[bd][1] + w[1]; anchor[2] = s.xpos[bd][2] + w[2];
+        }
+        if (kind == 1) {
+          c[0] = c[1] = c[2] = 0.f;
+          c[3] = ax[0]; c[4] = ax[1]; c[5] = ax[2];
+        } else {
+          float off[3] = {s.com[tr][0] - anchor[0], s.com[tr][1] - anchor[1], s.com[tr][2] - anchor[2]}, cr[3];
+          cross(cr, ax, off);
+          c[0] = ax[0]; c[1] = ax[1]; c[2] = ax[2];
+          c[3] = cr[0]; c[4] = cr[1]; c[5] = cr[2];
+        }
+      }
+    }
+  };
   for (int t = 0; t < H; t++) {
     // Launder the model pointer every step: otherwise the compiler hoists
     // every loop-invariant model load out of the horizon loop and keeps them
@@ -2872,8 +2914,12 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       }
     }
 
+    if constexpr (WPC == 2) {
+      if (m->coll_rows) cdof_phase();
+      sync();
+    }
     }  // run_main
-    if constexpr (WPC == 2) block_sync();  // geom poses, tree COMs ready for both waves
+    if constexpr (WPC == 2) block_sync();  // geom poses, tree COMs, cdof ready for both waves
 
     STAMP(2);
     STOP_AT(2)
@@ -2927,43 +2973,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       c[6] = mass * d[0]; c[7] = mass * d[1]; c[8] = mass * d[2];
       c[9] = mass;
     }
-    if (lane < nv) {
-      const int bd = m->dof_body[lane], kind = m->dof_kind[lane];
-      const int tr = m->body_tree[bd];
-      float* c = s.cdof[lane];
-      float R[9];
-#pragma unroll
-      for (int k = 0; k < 9; k++) R[k] = s.xmat[bd][k];
-      if (kind == 2) {  // free translation
-        c[0] = c[1] = c[2] = 0.f;
-        const int k = m->dof_sub[lane];
-        c[3] = k == 0 ? 1.f : 0.f;
-        c[4] = k == 1 ? 1.f : 0.f;
-        c[5] = k == 2 ? 1.f : 0.f;
-      } else {
-        float ax[3], anchor[3];
-        if (kind == 3) {
-          const int k = m->dof_sub[lane];
-          ax[0] = s.xmat[bd][k]; ax[1] = s.xmat[bd][3 + k]; ax[2] = s.xmat[bd][6 + k];  // by index, no selects
-          anchor[0] = s.xpos[bd][0]; anchor[1] = s.xpos[bd][1]; anchor[2] = s.xpos[bd][2];
-        } else {
-          const int j = m->dof_jnt[lane];
-          float w[3];
-          mv(ax, R, m->jnt_axis[j]);
-          mv(w, R, m->jnt_pos[j]);
-          anchor[0] = s.xpos[bd][0] + w[0]; anchor[1] = s.xpos[bd][1] + w[1]; anchor[2] = s.xpos[bd][2] + w[2];
-        }
-        if (kind == 1) {
-          c[0] = c[1] = c[2] = 0.f;
-          c[3] = ax[0]; c[4] = ax[1]; c[5] = ax[2];
-        } else {
-          float off[3] = {s.com[tr][0] - anchor[0], s.com[tr][1] - anchor[1], s.com[tr][2] - anchor[2]}, cr[3];
-          cross(cr, ax, off);
-          c[0] = ax[0]; c[1] = ax[1]; c[2] = ax[2];
-          c[3] = cr[0]; c[4] = cr[1]; c[5] = cr[2];
-        }
-      }
-    }
+    if (WPC == 1 || !m->coll_rows) cdof_phase();
     sync();
 
     STAMP(3);
@@ -3351,9 +3361,17 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       sync();
     }
     }  // run_coll
+    // WPC = 2 and DevModel::coll_rows: the collision wave builds the
+    // constraint rows too, still beside wave 0's dynamics (they need the
+    // contacts, qpos, qvel, cdof and the tree COMs, all ready before the first
+    // barrier) and hands them over at the second; otherwise wave 0 builds them
+    // after the contact list is handed over
+    const bool rows_c = WPC == 2 && m->coll_rows;
     if constexpr (WPC == 2) {
-      block_sync();  // the contact list is ready; wave 1 waits for the next step's geom poses
-      if (!run_main) continue;
+      if (!rows_c) {
+        block_sync();  // the contact list is ready; wave 1 waits for the next step's geom poses
+        if (!run_main) continue;
+      }
     }
 
     STAMP(7);
@@ -3361,7 +3379,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- constraint rows: equality, limits, contacts ------------------------
     bool coupled = true;  // a constraint row spans two kinematic trees (Newton's H not block diagonal)
-    {
+    if (WPC == 1 || (rows_c ? run_coll : run_main)) {
       const int ncon = s.ncon;
       const int neq = (m->disableflags & 64) ? 0 : (S::WIDE ? m->neqrow : m->neq);
       int nlim_l = 0, lsides = 0;
@@ -3631,10 +3649,18 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           o[3] = s.con_dist[lane]; o[4] = (float)s.con_pair[lane];
           o[5] = s.con_frame[lane][0]; o[6] = s.con_frame[lane][1]; o[7] = s.con_frame[lane][2];
         }
-        if (lane < NVW) args.dbg[DBG_QAS + lane] = s.qas[lane];
       }
       sync();
+    }  // constraint rows
+    if constexpr (WPC == 2) {
+      if (rows_c) {
+        if (run_coll && lane == 0) s.pad_ = coupled ? 1 : 0;
+        block_sync();  // contacts and constraint rows ready; wave 1 waits for the next step's geom poses
+        if (!run_main) continue;
+        coupled = s.pad_ != 0;
+      }
     }
+    if (args.dbg && b == 0 && t == H - 1 && lane < NVW) args.dbg[DBG_QAS + lane] = s.qas[lane];
     nefc_sum += s.nefc;
     nefc_max = max(nefc_max, s.nefc);
 
