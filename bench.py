@@ -191,7 +191,7 @@ def main():
                     help="candidates (per GPU for weak, total for strong)")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--model", default=None)
-    ap.add_argument("--cpu-sample", type=int, default=2048)
+    ap.add_argument("--cpu-sample", type=int, default=0, help="candidates timed on the host (0 = the whole batch)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every usable host core (affinity mask capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -243,12 +243,18 @@ def main():
         # host-core baseline before the process initialises the GPU
         usable, ncpu, model, aff, quota = _host_cpu()
         threads = args.cpu_threads or usable
-        sample = xi_host[: args.cpu_sample].numpy()
-        one = sample[: max(32, args.cpu_sample // 16)]
+        sample = xi_host[: args.cpu_sample or n].numpy()
+        one = sample[: max(32, sample.shape[0] // 16)]
         v32, reps = cpu_baseline(m, sample, H, Pd, threads, precision="fp32")
         v32_1, _ = cpu_baseline(m, one, H, Pd, 1, precision="fp32")
         v64, reps64 = cpu_baseline(m, sample, H, Pd, threads, precision="fp64")
         v64_1, _ = cpu_baseline(m, one, H, Pd, 1, precision="fp64")
+        # the affinity mask may show more CPUs than the cgroup quota grants (the
+        # GPU box: 256 vs 16): one run with a thread per affinity CPU shows
+        # the quota binding (not the reported value)
+        v32_aff = None
+        if aff > threads and not args.cpu_threads:
+            v32_aff, _ = cpu_baseline(m, sample, H, Pd, aff, reps=3, precision="fp32")
         cpu_rec = {"value": round(v32, 1), "unit": "rollouts/s", "cores": threads, "kind": "port",
                    "sample": f"{sample.shape[0]} of the same {args.config.upper()} candidates x {H} steps; fp32 "
                              f"scalar C restatement of the reference rollout + cost (oracle/oracle_f32.c = "
@@ -257,6 +263,7 @@ def main():
                              f"(pool and model set up before the clock); 1 thread: {v32_1:.1f} rollouts/s; fp64 "
                              f"build: {v64:.1f} ({threads} threads), {v64_1:.1f} (1 thread)",
                    "precision": "fp32", "one_core": round(v32_1, 1), "reps": reps,
+                   "affinity_threads": None if v32_aff is None else {"threads": aff, "value": round(v32_aff, 1)},
                    "fp64": {"value": round(v64, 1), "one_core": round(v64_1, 1), "reps": reps64},
                    "host": {"usable_cores": usable, "affinity_cores": aff, "cgroup_cpu_quota": quota, "nproc": ncpu,
                             "cpu_model": model}}

@@ -217,7 +217,9 @@ class Runner:
         td = np.ascontiguousarray(td, dtype=self.dt)
         n, H = td.shape[0], td.shape[1] // self.model.nctrl
         cost4 = np.zeros((n, 4), dtype=self.dt)
-        cuts = np.linspace(0, n, min(self.workers, n) + 1).astype(int)
+        # 8 chunks per thread: candidates differ in work (contacts, rows), so
+        # one static chunk per thread would leave threads idle at the end
+        cuts = np.linspace(0, n, min(8 * self.workers, n) + 1).astype(int)
         q0, w, pt, qt = self.args
         p = self.p
 
