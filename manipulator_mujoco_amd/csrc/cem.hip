@@ -27,6 +27,11 @@ constexpr int PJ_NB = 11;    // order-10 Bernstein basis (the planner's)
 constexpr int PJ_BLK = 12;   // per-joint block, padded (48-byte aligned rows)
 constexpr int PJ_MAXD = 8;   // joints (waves per workgroup)
 constexpr int TOPK_MAX = 4096;
+constexpr int PJ_RG = 4;     // projection rows per load group (interleaved dot chains)
+#ifndef MPCR_PJ_NS
+#define MPCR_PJ_NS 2
+#endif
+constexpr int PJ_NS = MPCR_PJ_NS;  // waves per (candidate block, joint): row parts
 
 struct ProjArgs {
   const float* xi_in;     // n x nv (read when mean == nullptr)
@@ -70,17 +75,30 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, fl
   z1 = r * s;
 }
 
-// One workgroup = 64 candidates x nd waves; wave j owns joint j's 11
-// coefficients of each of its 64 candidates (lane = candidate).
-__global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a) {
+// One workgroup = 64 candidates x nd joints x PJ_NS row parts: wave
+// (part, j) owns joint j's 11 coefficients of each of its 64 candidates
+// (lane = candidate) and, in the ADMM iterations, the part-th share of the
+// 3H constraint rows; the parts' partial sums meet through LDS.  The row
+// loop is a chain of dependent VALU instructions (one wave per SIMD ran at
+// ~10 cycles an instruction): splitting the rows halves each wave's chain and
+// doubles the waves that hide each other's latency.
+__global__ void __launch_bounds__(64 * PJ_MAXD * PJ_NS) sample_project_kernel(ProjArgs a) {
   extern __shared__ float pj_smem[];
   const int nd = a.nd, NV = nd * PJ_NB, RS = nd * PJ_BLK + 4;  // LDS row stride: conflict-free b128
   const int lane = threadIdx.x & 63;
-  const int j = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform joint
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = wv % nd, part = wv / nd;  // wave-uniform joint and row part
   const int cand = blockIdx.x * 64 + lane;
   const bool live = cand < a.n;
   float* row = pj_smem + lane * RS;  // this candidate's padded vector (rhs / z)
   const int jb = j * PJ_BLK;
+  // the constraint rows X (identical for every joint, candidate and ADMM
+  // iteration) copied to LDS once: each row is a broadcast ds_read
+  float* const Xs = pj_smem + 64 * RS;
+  // the parts' partial A^T res / A^T (b - s) sums: [part][j][c][lane]
+  float* const Ps = Xs + 3 * a.H * PJ_BLK;
+  for (int i = threadIdx.x; i < 3 * a.H * PJ_BLK; i += blockDim.x) Xs[i] = a.X[i];
+  __syncthreads();
 
   float xi[PJ_NB];
   if (a.mean) {
@@ -94,8 +112,10 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
       box_muller(c[2], c[3], z[4 * q + 2], z[4 * q + 3]);
     }
     z[PJ_NB] = 0.f;
+    if (part == 0) {
 #pragma unroll
-    for (int c = 0; c < PJ_BLK; c++) row[jb + c] = z[c];
+      for (int c = 0; c < PJ_BLK; c++) row[jb + c] = z[c];
+    }
     __syncthreads();
     // xi[r] = mean[r] + sum_{c <= r} L[r][c] z[c]; L is stored transposed
     // (LT[c][r]) so the 11 coefficients of one c are contiguous and uniform.
@@ -136,10 +156,13 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
     for (int r = 0; r < PJ_NB; r++) lam[r] = sl[r] = 0.f;
     const int LD = nd * PJ_BLK;
     for (int it = 0; it < a.maxiter; it++) {
-      // -lincost = lam + rho xi + rho sum_k A_k^T (b - s_k)
+      // -lincost = lam + rho xi + rho sum_k A_k^T (b - s_k)  (every part holds
+      // the same values; part 0 writes them)
+      if (part == 0) {
 #pragma unroll
-      for (int r = 0; r < PJ_NB; r++) row[jb + r] = lam[r] + a.rho * xi[r] + a.rho * sl[r];
-      row[jb + PJ_NB] = 0.f;
+        for (int r = 0; r < PJ_NB; r++) row[jb + r] = lam[r] + a.rho * xi[r] + a.rho * sl[r];
+        row[jb + PJ_NB] = 0.f;
+      }
       __syncthreads();
       // primal = Qinv[rows, :nv] @ rhs + qb  (QT rows are wave-uniform)
 #pragma unroll
@@ -162,9 +185,13 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
       for (int r = 0; r < PJ_NB; r++) dl[r] = sl[r] = 0.f;
       for (int k = 0; k < 3; k++) {
         const float b = a.bound[k];
-        const float* Xk = a.X + (size_t)k * a.H * PJ_BLK;
-        for (int t = 0; t < a.H; t++) {
-          const float* x = Xk + t * PJ_BLK;
+        const float* Xk = Xs + (size_t)k * a.H * PJ_BLK;
+        // rows in groups of PJ_RG: the group's wave-uniform rows load with one
+        // scalar-memory wait (scalar loads return out of order, so each wait is
+        // for all of them) and the group's dot chains interleave; one row at a
+        // time waited on its s_load and an 11-deep FMA chain (~350 cycles a
+        // row for the one wave a SIMD holds)
+        auto row_update = [&](const float* x) {
           float v = 0.f;
 #pragma unroll
           for (int c = 0; c < PJ_NB; c++) v = fmaf(x[c], p[c], v);
@@ -175,7 +202,36 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
             dl[c] = fmaf(x[c], e_res, dl[c]);
             sl[c] = fmaf(x[c], e_sl, sl[c]);
           }
+        };
+        // this part's rows: [t0, t1) of each family
+        const int t0 = (a.H * part) / PJ_NS, t1 = (a.H * (part + 1)) / PJ_NS;
+        int t = t0;
+        for (; t + PJ_RG <= t1; t += PJ_RG) {
+          float xg[PJ_RG][PJ_NB];
+#pragma unroll
+          for (int u = 0; u < PJ_RG; u++)
+#pragma unroll
+            for (int c = 0; c < PJ_NB; c++) xg[u][c] = Xk[(t + u) * PJ_BLK + c];
+#pragma unroll
+          for (int u = 0; u < PJ_RG; u++) row_update(xg[u]);
         }
+        for (; t < t1; t++) row_update(Xk + t * PJ_BLK);
+      }
+      if constexpr (PJ_NS > 1) {
+        // every part publishes its partial sums, then each adds all parts in
+        // part order (the same operands in the same order: identical totals)
+        float* const mine = Ps + ((size_t)(part * nd + j) * 2 * PJ_NB) * 64 + lane;
+#pragma unroll
+        for (int c = 0; c < PJ_NB; c++) { mine[c * 64] = dl[c]; mine[(PJ_NB + c) * 64] = sl[c]; }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < PJ_NB; c++) dl[c] = sl[c] = 0.f;
+        for (int q = 0; q < PJ_NS; q++) {
+          const float* const src = Ps + ((size_t)(q * nd + j) * 2 * PJ_NB) * 64 + lane;
+#pragma unroll
+          for (int c = 0; c < PJ_NB; c++) { dl[c] += src[c * 64]; sl[c] += src[(PJ_NB + c) * 64]; }
+        }
+        __syncthreads();  // the partials are read before the next iteration rewrites them
       }
 #pragma unroll
       for (int r = 0; r < PJ_NB; r++) lam[r] -= a.rho * dl[r];
@@ -183,7 +239,7 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
   }
   // all global stores at the end: nothing before may clobber the tables, so
   // their wave-uniform loads stay scalar (s_load) loads
-  if (live) {
+  if (live && part == 0) {
     if (a.mean && a.xi_samples) {
 #pragma unroll
       for (int r = 0; r < PJ_NB; r++) a.xi_samples[(size_t)cand * NV + j * PJ_NB + r] = xi[r];
