@@ -28,10 +28,11 @@ constexpr int PJ_BLK = 12;   // per-joint block, padded (48-byte aligned rows)
 constexpr int PJ_MAXD = 8;   // joints (waves per workgroup)
 constexpr int TOPK_MAX = 4096;
 constexpr int PJ_RG = 4;     // projection rows per load group (interleaved dot chains)
-#ifndef MPCR_PJ_NS
-#define MPCR_PJ_NS 2
-#endif
-constexpr int PJ_NS = MPCR_PJ_NS;  // waves per (candidate block, joint): row parts
+// candidates per workgroup (and per wave) of the projection kernel, chosen
+// per launch: 16 below 8192 candidates, 32 from there (10-iteration
+// projection, H = 50: 4096 -> 0.130 / 0.172 ms, 8192 -> 0.249 / 0.181 ms for
+// 16 / 32; 8 gave 0.199 / 0.384 ms)
+constexpr int PJ_CPW_SMALL = 16, PJ_CPW_LARGE = 32, PJ_CPW_SWITCH = 8192;
 
 struct ProjArgs {
   const float* xi_in;     // n x nv (read when mean == nullptr)
@@ -75,28 +76,30 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, fl
   z1 = r * s;
 }
 
-// One workgroup = 64 candidates x nd joints x PJ_NS row parts: wave
-// (part, j) owns joint j's 11 coefficients of each of its 64 candidates
-// (lane = candidate) and, in the ADMM iterations, the part-th share of the
-// 3H constraint rows; the parts' partial sums meet through LDS.  The row
-// loop is a chain of dependent VALU instructions (one wave per SIMD ran at
-// ~10 cycles an instruction): splitting the rows halves each wave's chain and
-// doubles the waves that hide each other's latency.
-__global__ void __launch_bounds__(64 * PJ_MAXD * PJ_NS) sample_project_kernel(ProjArgs a) {
+// One workgroup = PJ_CPW candidates x nd waves; wave j owns joint j's 11
+// coefficients of each of its candidates, and lane = candidate + PJ_CPW x
+// part: the PJ_NP lanes of a candidate split the 3H constraint rows of each
+// ADMM iteration and add their partial sums with two lane swaps.  Few
+// candidates per workgroup spread a batch over every CU (64 candidates per
+// workgroup left 3 of 4 CUs idle at 4096), and the split shortens each
+// lane's chain of dependent row updates (the loop ran at ~10 cycles an
+// instruction with one wave per SIMD).  The KKT solve is per candidate and
+// repeated by its parts.
+template <int PJ_CPW>
+__global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a) {
+  constexpr int PJ_NP = 64 / PJ_CPW;  // row parts: the lanes of one candidate
   extern __shared__ float pj_smem[];
   const int nd = a.nd, NV = nd * PJ_NB, RS = nd * PJ_BLK + 4;  // LDS row stride: conflict-free b128
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int j = wv % nd, part = wv / nd;  // wave-uniform joint and row part
-  const int cand = blockIdx.x * 64 + lane;
+  const int j = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform joint
+  const int cl = lane & (PJ_CPW - 1), part = lane / PJ_CPW;  // candidate in the workgroup, row part
+  const int cand = blockIdx.x * PJ_CPW + cl;
   const bool live = cand < a.n;
-  float* row = pj_smem + lane * RS;  // this candidate's padded vector (rhs / z)
+  float* row = pj_smem + cl * RS;  // this candidate's padded vector (rhs / z)
   const int jb = j * PJ_BLK;
   // the constraint rows X (identical for every joint, candidate and ADMM
-  // iteration) copied to LDS once: each row is a broadcast ds_read
-  float* const Xs = pj_smem + 64 * RS;
-  // the parts' partial A^T res / A^T (b - s) sums: [part][j][c][lane]
-  float* const Ps = Xs + 3 * a.H * PJ_BLK;
+  // iteration) in LDS
+  float* const Xs = pj_smem + PJ_CPW * RS;
   for (int i = threadIdx.x; i < 3 * a.H * PJ_BLK; i += blockDim.x) Xs[i] = a.X[i];
   __syncthreads();
 
@@ -155,6 +158,8 @@ __global__ void __launch_bounds__(64 * PJ_MAXD * PJ_NS) sample_project_kernel(Pr
 #pragma unroll
     for (int r = 0; r < PJ_NB; r++) lam[r] = sl[r] = 0.f;
     const int LD = nd * PJ_BLK;
+    // this part's rows [t0, t1) of each constraint family
+    const int t0 = (a.H * part) / PJ_NP, t1 = (a.H * (part + 1)) / PJ_NP;
     for (int it = 0; it < a.maxiter; it++) {
       // -lincost = lam + rho xi + rho sum_k A_k^T (b - s_k)  (every part holds
       // the same values; part 0 writes them)
@@ -179,19 +184,16 @@ __global__ void __launch_bounds__(64 * PJ_MAXD * PJ_NS) sample_project_kernel(Pr
         }
       }
       __syncthreads();  // everyone has read row[] before it is rewritten
-      // slacks, residuals, multipliers for Pdot (v), Pddot (a), P (p)
+      // slacks, residuals, multipliers for Pdot (v), Pddot (a), P (p): this
+      // part's rows, then the parts' sums
       float dl[PJ_NB];
 #pragma unroll
       for (int r = 0; r < PJ_NB; r++) dl[r] = sl[r] = 0.f;
       for (int k = 0; k < 3; k++) {
         const float b = a.bound[k];
         const float* Xk = Xs + (size_t)k * a.H * PJ_BLK;
-        // rows in groups of PJ_RG: the group's wave-uniform rows load with one
-        // scalar-memory wait (scalar loads return out of order, so each wait is
-        // for all of them) and the group's dot chains interleave; one row at a
-        // time waited on its s_load and an 11-deep FMA chain (~350 cycles a
-        // row for the one wave a SIMD holds)
-        auto row_update = [&](const float* x) {
+        auto row_update = [&](const float4 x0, const float4 x1, const float4 x2) {
+          const float x[PJ_BLK] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x, x2.y, x2.z, x2.w};
           float v = 0.f;
 #pragma unroll
           for (int c = 0; c < PJ_NB; c++) v = fmaf(x[c], p[c], v);
@@ -203,35 +205,30 @@ __global__ void __launch_bounds__(64 * PJ_MAXD * PJ_NS) sample_project_kernel(Pr
             sl[c] = fmaf(x[c], e_sl, sl[c]);
           }
         };
-        // this part's rows: [t0, t1) of each family
-        const int t0 = (a.H * part) / PJ_NS, t1 = (a.H * (part + 1)) / PJ_NS;
         int t = t0;
-        for (; t + PJ_RG <= t1; t += PJ_RG) {
-          float xg[PJ_RG][PJ_NB];
+        for (; t + PJ_RG <= t1; t += PJ_RG) {  // a group's LDS loads issue together
+          float4 xg[PJ_RG][3];
 #pragma unroll
           for (int u = 0; u < PJ_RG; u++)
 #pragma unroll
-            for (int c = 0; c < PJ_NB; c++) xg[u][c] = Xk[(t + u) * PJ_BLK + c];
+            for (int q = 0; q < 3; q++) xg[u][q] = reinterpret_cast<const float4*>(Xk + (t + u) * PJ_BLK)[q];
 #pragma unroll
-          for (int u = 0; u < PJ_RG; u++) row_update(xg[u]);
+          for (int u = 0; u < PJ_RG; u++) row_update(xg[u][0], xg[u][1], xg[u][2]);
         }
-        for (; t < t1; t++) row_update(Xk + t * PJ_BLK);
+        for (; t < t1; t++) {
+          const float4* xr = reinterpret_cast<const float4*>(Xk + t * PJ_BLK);
+          row_update(xr[0], xr[1], xr[2]);
+        }
       }
-      if constexpr (PJ_NS > 1) {
-        // every part publishes its partial sums, then each adds all parts in
-        // part order (the same operands in the same order: identical totals)
-        float* const mine = Ps + ((size_t)(part * nd + j) * 2 * PJ_NB) * 64 + lane;
+      // the parts' sums: lanes cl + PJ_CPW q (q = 0..3) swap and add; fp32
+      // addition commutes, so all four hold bitwise the same totals
 #pragma unroll
-        for (int c = 0; c < PJ_NB; c++) { mine[c * 64] = dl[c]; mine[(PJ_NB + c) * 64] = sl[c]; }
-        __syncthreads();
+      for (int c = 0; c < PJ_NB; c++) {
 #pragma unroll
-        for (int c = 0; c < PJ_NB; c++) dl[c] = sl[c] = 0.f;
-        for (int q = 0; q < PJ_NS; q++) {
-          const float* const src = Ps + ((size_t)(q * nd + j) * 2 * PJ_NB) * 64 + lane;
-#pragma unroll
-          for (int c = 0; c < PJ_NB; c++) { dl[c] += src[c * 64]; sl[c] += src[(PJ_NB + c) * 64]; }
+        for (int o = PJ_CPW; o < 64; o <<= 1) {
+          dl[c] += __shfl_xor(dl[c], o);
+          sl[c] += __shfl_xor(sl[c], o);
         }
-        __syncthreads();  // the partials are read before the next iteration rewrites them
       }
 #pragma unroll
       for (int r = 0; r < PJ_NB; r++) lam[r] -= a.rho * dl[r];

@@ -1571,11 +1571,13 @@ extern "C" int mpcr_cem_sample_project(mpcr_cem* c, int n, const float* mean, ui
   a.beq_stride = beq_stride;
   for (int k = 0; k < 3; k++) a.bound[k] = bounds ? bounds[k] : 0.f;
   a.rho = rho;
-  // the candidates' padded rows, the constraint rows X (3 x H x 12) and the
-  // row parts' partial sums in LDS
-  const size_t lds = sizeof(float) * (64 * (c->nd * PJ_BLK + 4) + 3 * (size_t)c->H * PJ_BLK +
-                                      (PJ_NS > 1 ? (size_t)PJ_NS * c->nd * 2 * PJ_NB * 64 : 0));
-  hipLaunchKernelGGL(sample_project_kernel, dim3((n + 63) / 64), dim3(64 * c->nd * PJ_NS), lds, st, a);
+  // the candidates' padded rows and the constraint rows X (3 x H x 12) in LDS
+  const int cpw = n >= PJ_CPW_SWITCH ? PJ_CPW_LARGE : PJ_CPW_SMALL;
+  const size_t lds = sizeof(float) * (cpw * (c->nd * PJ_BLK + 4) + 3 * (size_t)c->H * PJ_BLK);
+  if (cpw == PJ_CPW_LARGE)
+    hipLaunchKernelGGL(sample_project_kernel<PJ_CPW_LARGE>, dim3((n + cpw - 1) / cpw), dim3(64 * c->nd), lds, st, a);
+  else
+    hipLaunchKernelGGL(sample_project_kernel<PJ_CPW_SMALL>, dim3((n + cpw - 1) / cpw), dim3(64 * c->nd), lds, st, a);
   HIPCHK(hipGetLastError());
   if (flags & MPCR_F_SYNC) HIPCHK(hipStreamSynchronize(st));
   return MPCR_OK;
