@@ -253,6 +253,7 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
 __global__ void __launch_bounds__(256) cholesky_kernel(const float* __restrict__ cov, int nd, float reg,
                                                         float* __restrict__ LT) {
   __shared__ float A[PJ_MAXD * PJ_NB][PJ_MAXD * PJ_NB + 1];
+  __shared__ float Ld[PJ_MAXD * PJ_NB];  // the factor's diagonal (A's diagonal is never overwritten)
   const int nv = nd * PJ_NB, LD = nd * PJ_BLK;
   for (int i = threadIdx.x; i < nv * nv; i += blockDim.x) {
     const int r = i / nv, c = i % nv;
@@ -260,21 +261,26 @@ __global__ void __launch_bounds__(256) cholesky_kernel(const float* __restrict__
   }
   for (int i = threadIdx.x; i < LD * LD; i += blockDim.x) LT[i] = 0.f;
   __syncthreads();
+  // right-looking, 16 x 16 threads over the trailing block (no integer
+  // division per element: that alone was ~40 instructions an element), two
+  // barriers per column
+  const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
   for (int k = 0; k < nv; k++) {
     const float d = sqrtf(A[k][k]);
+    const float id = 1.f / d;
+    for (int i = k + 1 + threadIdx.x; i < nv; i += blockDim.x) A[i][k] *= id;
+    if (threadIdx.x == 0) Ld[k] = d;
     __syncthreads();
-    for (int i = k + threadIdx.x; i < nv; i += blockDim.x) A[i][k] = i == k ? d : A[i][k] / d;
-    __syncthreads();
-    const int m = nv - k - 1;
-    for (int e = threadIdx.x; e < m * m; e += blockDim.x) {
-      const int i = k + 1 + e / m, c = k + 1 + e % m;
-      if (c <= i) A[i][c] -= A[i][k] * A[c][k];
+    for (int i = k + 1 + tr; i < nv; i += 16) {
+      const float aik = A[i][k];
+      for (int c = k + 1 + tc; c <= i; c += 16) A[i][c] -= aik * A[c][k];
     }
     __syncthreads();
   }
   for (int i = threadIdx.x; i < nv * nv; i += blockDim.x) {
     const int r = i / nv, c = i % nv;
-    if (c <= r) LT[(size_t)((c / PJ_NB) * PJ_BLK + c % PJ_NB) * LD + (r / PJ_NB) * PJ_BLK + r % PJ_NB] = A[r][c];
+    if (c <= r)
+      LT[(size_t)((c / PJ_NB) * PJ_BLK + c % PJ_NB) * LD + (r / PJ_NB) * PJ_BLK + r % PJ_NB] = r == c ? Ld[r] : A[r][c];
   }
 }
 
