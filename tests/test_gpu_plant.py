@@ -270,3 +270,52 @@ def test_dual_arm_large_hull_plane_manifold_matches_oracle(torch_cuda):
     bad = [r for r in rows if min(r["qacc_err"], r["qacc_err_f32"]) >= 5e-3]
     assert not bad, bad[:3]
     assert np.median([r["qacc_err"] for r in rows]) < 5e-3
+
+
+def test_dual_arm_finger_hulls_match_oracle_at_traced_steps(torch_cuda):
+    """C4's selected candidate (558 of the seed-4 shard):
+    the Hand-E finger hulls interpenetrate ~2 cm, where the polyhedron
+    manifold's clip can keep no point and the SAT axis then carries one
+    contact at the incident support vertex.  The plant, set to the fp64
+    oracle's state at each traced step, finds that pair's contacts with the
+    oracle's normal and depth, and the step's qacc within 5e-3 of its scale
+    (the GPU left the oracle there by 0.14 of 235-822 before the rule)."""
+    import torch
+
+    from manipulator_mujoco_amd.projection import ProjectionFilter
+    m, H = models.load("dual_arm", 0.05), 100
+    B, G = m.names["body"], m.geom_bodyid
+    pair = next(p for p in range(m.npair)
+                if {B[G[m.pair_geom1[p]]], B[G[m.pair_geom2[p]]]} == {"hande_left_finger", "hande_right_finger"})
+    _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
+    f = ProjectionFilter(P, Pd, Pdd, 6, torch.device("cpu"))
+    rng = np.random.default_rng(20250629 + 4)
+    xi = torch.tensor(rng.normal(0, np.sqrt(10.003), (4096, 66)).astype(np.float32))[[558]]
+    q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
+    xi = f(xi, f.boundary(q0, np.zeros(6), np.zeros(6), 1), 10).numpy()
+    td = np.einsum("tk,njk->njt", Pd, xi.reshape(1, 6, 11).astype(np.float64)).reshape(6, H)
+    qa, da = np.asarray(m.ctrl_qposadr[:6]), np.asarray(m.ctrl_dofadr[:6])
+    qpos = np.array(m.qpos_init[:m.nq], dtype=np.float64)
+    qpos[qa] = q0
+    qvel, ws = np.array(m.qvel_init[:m.nv], dtype=np.float64), np.zeros(m.nv)
+    plant = Plant(m)
+    checked = 0
+    for t in range(66):
+        qv = qvel.copy()
+        qv[da] = td[:, t]
+        if t in (30, 54, 65):
+            od = oracle.step_debug(m, qpos, qv, ws)
+            plant.set_state(qpos=qpos, qvel=qv, qacc_warmstart=ws)
+            gd = plant.step_debug(td[:, t])
+            ko = [k for k in range(od["ncon"]) if od["con_pair"][k] == pair]
+            kg = [k for k in range(gd["ncon"]) if gd["con_pair"][k] == pair]
+            assert bool(ko) == bool(kg), (t, ko, kg)
+            if ko:
+                checked += 1
+                assert np.abs(gd["con_normal"][kg[0]] - od["con_normal"][ko[0]]).max() < 1e-3, t
+                assert abs(min(gd["con_dist"][k] for k in kg) - min(od["con_dist"][k] for k in ko)) < 1e-5, t
+            scale = max(1.0, np.abs(od["qacc"]).max())
+            assert np.abs(gd["qacc"] - od["qacc"]).max() < 5e-3 * scale, t
+        st = oracle.step(m, qpos, qv, ws)
+        qpos, qvel, ws = st["qpos"], st["qvel"], st["qacc_warmstart"]
+    assert checked >= 2
