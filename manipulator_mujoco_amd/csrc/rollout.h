@@ -208,14 +208,14 @@ static_assert(sizeof(SmemN) <= 9520, "narrow LDS image must fit 16 blocks per CU
 // most 2048 candidates = 8 blocks per CU, so LDS is not the limit
 using SmemN2 = SmemT<16, 16, 24, MPCR_N_MAXEFC, MPCR_N_LDJ, MPCR_N_CPREV_GLOBAL, MPCR_N_MAXEFC, 1, DX_MAXACT, true>;
 static_assert(sizeof(SmemN2) <= 152448 / 8, "two-wave narrow image: 8 blocks per CU");
-// Dual-arm image: J rows past 40 in the HBM slab, cost history and hull-climb
+// Dual-arm image: J rows past 44 in the HBM slab, cost history and hull-climb
 // hints in HBM (the class has no robot-masked slots), the convex-pair list
 // inside the J rows, 6-float cdof rows, the mass matrix in an HBM slab:
 // 17.2 KB -> 8 blocks per CU (21.7 KB / 7 before the M slab; 32.3 KB / 4
 // before the J slab); the kernel is compiled for 2 waves/SIMD (<= 256 VGPRs),
 // so 8 blocks per CU is also its register limit.
 #ifndef MPCR_W_JL
-#define MPCR_W_JL 40
+#define MPCR_W_JL 44  // 40 -> 44 since the manifold doubled the rows (53.5 per step): C4 50.4 -> 49.7 ms
 #endif
 #ifndef MPCR_W_MAXACT
 #define MPCR_W_MAXACT 48  // the polyhedron manifold's 4 contacts per face pair (40 truncated 0.5 % of a C4 shard)

@@ -2460,7 +2460,7 @@ __device__ __forceinline__ mfx4 mm16(AF&& af, BF&& bf, mfx4 acc, int lane) {
 template <class S, class BF>
 __device__ __forceinline__ mfx16 mfma_rows32(const S& s, const float* gx, int nefc, int gi, int gq, BF&& bf,
                                              mfx16 acc) {
-  static_assert(S::JL % 8 == 0, "a row group never straddles the LDS / slab boundary");
+  static_assert(S::JL % (MPCR_W_MFMA_SPLIT ? 8 : 2) == 0, "a row group never straddles the LDS / slab boundary");
 #if MPCR_W_MFMA_SPLIT
   // two accumulators (row groups alternate), four row pairs' operands loaded
   // before their MFMAs: the dependent 32x32x2 chain and the LDS / slab loads
