@@ -2357,10 +2357,10 @@ __device__ __forceinline__ void ls_add(LsPt& p, float c0, float c1, float c2) {
 #endif
 #if MPCR_PHASE_LAUNDER
 #define LAUNDER_PHASE() LAUNDER_MODEL()
-#elif MPCR_LANE_LAUNDER >= 2
-#define LAUNDER_PHASE()                \
-  do {                                 \
-    if constexpr (!WIDE) LAUNDER_LANE(); \
+#elif MPCR_LANE_LAUNDER >= 2 || MPCR_W_LANE_LAUNDER >= 2
+#define LAUNDER_PHASE()                                                          \
+  do {                                                                           \
+    if constexpr (WIDE ? MPCR_W_LANE_LAUNDER >= 2 : MPCR_LANE_LAUNDER >= 2) LAUNDER_LANE(); \
   } while (0)
 #else
 #define LAUNDER_PHASE() \
