@@ -1035,6 +1035,10 @@ __device__ __forceinline__ float wmax(float v) {
   return v;
 }
 
+// inline the manifold callees (experiment): 1 polyhedron, 2 both
+#ifndef MPCR_POLY_INLINE
+#define MPCR_POLY_INLINE 2  // both inlined: 241 -> 235 VGPRs, no scratch (the contact arrays stay in registers), C4 48.6 -> 46.7 ms
+#endif
 // Plane-mesh manifold (MJX plane_convex / _manifold_points, the oracle's
 // col_plane_mesh), wave-cooperative: every lane calls it with the same pair
 // (mesh g, plane normal n through xp, penetration depth) and lane q receives
@@ -1044,7 +1048,12 @@ __device__ __forceinline__ float wmax(float v) {
 // of four serial per-lane scans (a 2691-vertex hull touching the table made a
 // handful of dual-arm candidates 3x slower than the rest).
 template <class S>
-__device__ __noinline__ void plane_mesh_manifold_wave(const DevModel* __restrict__ m_, const S& s, int g,
+#if MPCR_POLY_INLINE >= 2
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+void plane_mesh_manifold_wave(const DevModel* __restrict__ m_, const S& s, int g,
                                                       const float n_[3], const float* xp_, float depth, int q, int lane,
                                                       float dist[4], float pos[4][3], float nrm[4][3], int& nsl) {
   const MPCR_GMEM DevModel* __restrict__ m = uniform_model(m_);
@@ -1204,7 +1213,12 @@ __device__ __forceinline__ void vert_rel(const DevModel* __restrict__ m, const S
 // _manifold_points picks as wave maxima.  Coordinates relative to g2's
 // centre, as MPR's.
 template <class S>
-__device__ __noinline__ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hints, int p,
+#if MPCR_POLY_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hints, int p,
                                                 const float n_[3], float depth, int q, int lane, float dist[4],
                                                 float pos[4][3], float nrm[4][3], int& nsl) {
   const MPCR_GMEM DevModel* __restrict__ m = uniform_model(m_);
