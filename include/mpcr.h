@@ -117,7 +117,8 @@ void mpcr_engine_free(mpcr_engine* e);
                         bit1: non-finite state) | (max constraint rows in
                         one step, capped at 63, << 2) | (constraint rows
                         summed over the horizon << 8)            (nullable)
-   stream               hipStream_t or NULL (default stream)                  */
+   stream               hipStream_t or NULL (default stream)
+   n = 0 is a no-op returning MPCR_OK (input and cost4 may then be NULL). */
 int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
                       const float* w, const float* ptgt, const float* qtgt, float* cost4, float* theta,
                       float* thetadot, uint64_t* best_key, int index_base, int* status, int flags,

@@ -1028,10 +1028,11 @@ extern "C" int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout,
                                  const float* w, const float* ptgt, const float* qtgt, float* cost4, float* theta,
                                  float* thetadot, uint64_t* best_key, int index_base, int* status, int flags,
                                  void* stream) {
-  if (!e || !input || !q0 || !w || !ptgt || !qtgt || !cost4) return fail(MPCR_EINVAL, "null argument");
+  if (!e || !q0 || !w || !ptgt || !qtgt) return fail(MPCR_EINVAL, "null argument");
   if (n < 0 || n > e->max_n) return fail(MPCR_EINVAL, "n=%d outside [0, max_n=%d]", n, e->max_n);
   if (layout != MPCR_LAYOUT_XI && layout != MPCR_LAYOUT_THETADOT) return fail(MPCR_EINVAL, "bad layout %d", layout);
-  if (n == 0) return MPCR_OK;
+  if (n == 0) return MPCR_OK;  // an empty batch: input / cost4 may be null (a zero-size tensor's data pointer)
+  if (!input || !cost4) return fail(MPCR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;
   auto* key = reinterpret_cast<unsigned long long*>(best_key);
@@ -1069,10 +1070,11 @@ extern "C" int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout,
 extern "C" int mpcr_rollout_cost_dp(mpcr_engine* e, const float* input, int layout, int n, const float* params,
                                     float* cost4, float* theta, float* thetadot, uint64_t* best_key, int index_base,
                                     int* status, int flags, void* stream) {
-  if (!e || !input || !params || !cost4) return fail(MPCR_EINVAL, "null argument");
+  if (!e) return fail(MPCR_EINVAL, "null argument");
   if (n < 0 || n > e->max_n) return fail(MPCR_EINVAL, "n=%d outside [0, max_n=%d]", n, e->max_n);
   if (layout != MPCR_LAYOUT_XI && layout != MPCR_LAYOUT_THETADOT) return fail(MPCR_EINVAL, "bad layout %d", layout);
-  if (n == 0) return MPCR_OK;
+  if (n == 0) return MPCR_OK;  // an empty batch: the buffers may be null
+  if (!input || !params || !cost4) return fail(MPCR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;
   Launch l;

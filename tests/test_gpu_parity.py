@@ -237,6 +237,44 @@ def test_full_size_properties(torch_cuda):
     assert i_hi == half + int(torch.argmin(a[half:, 0]))
 
 
+@pytest.mark.parametrize("name,H,n", [("scene_mjx", 20, 4099), ("dual_arm", 10, 515)])
+def test_ragged_batches_are_batch_independent(torch_cuda, name, H, n):
+    """Ragged batch sizes (1, an odd handful, one past a wave of 64, a partial
+    last launch round; small ones take the two-wave variant) give each
+    candidate exactly the outputs it has inside the full batch, the best key
+    names the prefix's own argmin, and an empty batch is a no-op."""
+    torch = torch_cuda
+    from manipulator_mujoco_amd import _lib
+    m = models.load(name, 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 7, torch.device("cuda:0"))
+    e = Engine(m, H, n, Pd)
+
+    def run(k):
+        c4 = torch.full((k, 4), float("nan"), device="cuda:0")
+        th = torch.empty((k, 6 * H), device="cuda:0")
+        st = torch.zeros(k, dtype=torch.int32, device="cuda:0")
+        key = torch.empty(1, dtype=torch.int64, device="cuda:0")
+        e.rollout_cost(xi[:k].contiguous(), MPCR_LAYOUT_XI, Q0, W, PT, QT, cost4=c4, theta=th, best_key=key,
+                       status=st)
+        torch.cuda.synchronize()
+        return c4, th, st, key
+
+    full = run(n)
+    assert torch.isfinite(full[0]).all()
+    for k in (1, 3, 65, n - 2):
+        c4, th, st, key = run(k)
+        assert torch.equal(c4, full[0][:k]), k
+        assert torch.equal(th, full[1][:k]), k
+        assert torch.equal(st, full[2][:k]), k
+        idx, val = _lib.decode_key(int(key.item()) & 0xFFFFFFFFFFFFFFFF)
+        assert idx == int(torch.argmin(c4[:, 0])) and val == float(c4[idx, 0]), k
+    empty = torch.empty((0, 66), device="cuda:0")
+    c0 = e.rollout_cost(empty, MPCR_LAYOUT_XI, Q0, W, PT, QT)
+    torch.cuda.synchronize()
+    assert c0.shape == (0, 4)
+
+
 def test_compute_cem_dropin(torch_cuda):
     from manipulator_mujoco_amd.planner import cem_planner
     p = cem_planner(num_dof=6, num_batch=256, num_steps=16, timestep=0.05, maxiter_cem=3, num_elite=0.05,
