@@ -99,16 +99,16 @@ def pmc_traffic(path):
 
 
 def pmc_valu(path, n, H, flops_step):
-    """VALU instructions per candidate-step (one wave = one candidate) and the
-    lane-flop efficiency flops / (64 x VALU instructions) from a committed SQ
-    counter CSV of the same workload."""
+    """VALU instructions per candidate-step (over all of a candidate's waves:
+    the two-wave variant runs two) and the lane-flop efficiency flops / (64 x
+    VALU instructions) from a committed SQ counter CSV of the same workload."""
     c = _pmc_rows(path)
     if "SQ_INSTS_VALU" not in c:
         return None
     insts = float(np.mean(c["SQ_INSTS_VALU"]))
     waves = float(np.mean(c.get("SQ_WAVES", [n])))
-    per = insts / (waves * H)
-    rec = {"valu_insts_per_candidate_step": round(per, 1),
+    per = insts / (n * H)
+    rec = {"valu_insts_per_candidate_step": round(per, 1), "waves_per_candidate": round(waves / n, 2),
            "lane_flop_efficiency": round(flops_step / (64.0 * per), 4), "source": os.path.relpath(path, ROOT)}
     if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
         # SQ_ACTIVE_INST_VALU counts quad-cycles; GRBM_GUI_ACTIVE is summed over
@@ -353,10 +353,17 @@ def main():
         flops_launch = fps * H * n
         achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
         hbm_launch = n * (66 * 4 + 16 + 2 * 6 * H * 4 + 4)  # xi in; cost4, theta, thetadot, status out
-        default_prof = args.config == "c3" and args.n == 4096 and args.scaling == "weak"
-        pmc = args.pmc or (os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_rollout.csv") if default_prof else None)
-        pmc_sq = args.pmc_sq or (os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_sq.csv") if default_prof
-                                 else None)
+        # the committed counter passes of this exact workload (the config's own
+        # batch, weak mode): C3 r03_pmc_rollout.csv / r03_pmc_sq.csv, the other
+        # configs the same names suffixed _c2 / _c4
+        default_prof = args.n == cfg["n"] and args.scaling == "weak"
+        sfx = "" if args.config == "c3" else "_" + args.config
+
+        def committed(kind):
+            path = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_{kind}{sfx}.csv")
+            return path if default_prof and os.path.exists(path) else None
+        pmc = args.pmc or committed("rollout")
+        pmc_sq = args.pmc_sq or committed("sq")
         traffic = pmc_traffic(pmc) if pmc else None
         valu = pmc_valu(pmc_sq, n, H, fps) if pmc_sq else None
         rec = {

@@ -79,6 +79,14 @@ fi
 if [[ $STEPS == *pmcc4* ]]; then  # instruction mix / VALU busy of the dual-arm shard
   run pmc_c4 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_c4 -o run -- python3 bench.py --config c4 --no-cpu-baseline --no-contact-report --steps 2 --warmup 1
 fi
+if [[ $STEPS == *pmccfg* ]]; then  # HBM traffic passes of the C2 / C4 bench lines (+ C2's SQ pass)
+  for cf in c2 c4; do
+    for grp in FETCH_SIZE WRITE_SIZE; do
+      run pmc_${cf}_$grp 200 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_${cf}_$grp -o run -- python3 bench.py --config $cf --no-cpu-baseline --no-contact-report --steps 2 --warmup 1
+    done
+  done
+  run pmc_c2_sq 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_c2_sq -o run -- python3 bench.py --config c2 --no-cpu-baseline --no-contact-report --steps 2 --warmup 1
+fi
 if [[ $STEPS == *l2hit* ]]; then  # L2 hit rate of the dual-arm shard and the C3 launch
   run l2_c4 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/l2_c4 -o run -- python3 bench.py --config c4 --no-cpu-baseline --no-contact-report --steps 2 --warmup 1
   run l2_c3 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/l2_c3 -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
