@@ -275,6 +275,34 @@ def test_ragged_batches_are_batch_independent(torch_cuda, name, H, n):
     assert c0.shape == (0, 4)
 
 
+@pytest.mark.parametrize("name,H", [("scene_mjx", 50), ("dual_arm", 20)])
+def test_c4_global_batch_on_one_gpu(torch_cuda, name, H):
+    """The largest batch of BASELINE (C4's global 32768 candidates) on one
+    GPU: eight launch rounds, the per-candidate HBM slabs at their largest.
+    Each 4096-candidate shard equals its own launch bitwise (the shards the
+    8-GPU run hands to its ranks) and the best key names the global argmin."""
+    torch = torch_cuda
+    from manipulator_mujoco_amd import _lib
+    n, shard = 32768, 4096
+    m = models.load(name, 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 8, torch.device("cuda:0"))
+    e = Engine(m, H, n, Pd)
+    st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    key = torch.empty(1, dtype=torch.int64, device="cuda:0")
+    a = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, best_key=key, status=st).clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all()
+    assert int((st & 1).sum()) == 0  # no constraint-row truncation
+    for r in (0, 3, 7):
+        lo = r * shard
+        c = e.rollout_cost(xi[lo:lo + shard].contiguous(), MPCR_LAYOUT_XI, Q0, W, PT, QT, index_base=lo).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(c, a[lo:lo + shard]), r
+    idx, val = _lib.decode_key(int(key.item()) & 0xFFFFFFFFFFFFFFFF)
+    assert idx == int(torch.argmin(a[:, 0])) and val == float(a[idx, 0])
+
+
 def test_compute_cem_dropin(torch_cuda):
     from manipulator_mujoco_amd.planner import cem_planner
     p = cem_planner(num_dof=6, num_batch=256, num_steps=16, timestep=0.05, maxiter_cem=3, num_elite=0.05,
