@@ -129,7 +129,9 @@ int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, con
    info[6] = narrow (blocks, lds, vgprs), dual-arm class (blocks, lds, vgprs). */
 int mpcr_rollout_occupancy(int device, int* info);
 /* Narrow-variant batches of at most n candidates run two waves per candidate
-   (the collision phase beside the dynamics; bitwise the one-wave results).
+   (the collision phase beside the dynamics; bitwise the one-wave results);
+   dual-arm batches of at most min(n, 1024) too (MPCR_WPC2W_MAX_N overrides
+   the 1024: four two-wave blocks per CU).  0 disables both.
    n < 0 only queries.  Returns the previous threshold (default: the build's
    MPCR_WPC2_MAX_N_DEFAULT, or the MPCR_WPC2_MAX_N environment variable).
    Process-wide: set it before launches, not while one is in flight. */

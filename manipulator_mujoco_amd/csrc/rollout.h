@@ -221,6 +221,10 @@ static_assert(sizeof(SmemN2) <= 152448 / 8, "two-wave narrow image: 8 blocks per
 #define MPCR_W_MAXACT 48  // the polyhedron manifold's 4 contacts per face pair (40 truncated 0.5 % of a C4 shard)
 #endif
 using SmemW = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT>;
+// The two-wave dual-arm image (MPCR_W_WPC2 builds, small batches): the
+// dynamics scratch beside the contact / constraint arrays
+using SmemW2 = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT, true>;
+static_assert(sizeof(SmemW2) <= 152448 / 4, "two-wave dual-arm image: 4 blocks per CU");
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD + SmemN::NVW, "Hessian + J^T f scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 static_assert(SmemW::JL * SmemW::LDJ * 4 >= SmemW::CVXN * 4 + 2 * SmemW::PMAXW * 16 + 16,

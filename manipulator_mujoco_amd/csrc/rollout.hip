@@ -2542,8 +2542,9 @@ __device__ __forceinline__ mfx16 mfma_rows32(const S& s, const float* gx, int ne
 template <int NVW, int NBW, int NGW, bool WIDE, int WPC = 1>
 __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / SmemN::CPW) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
-  static_assert(WPC == 1 || (WPC == 2 && !WIDE && SmemN::CPW == 1), "two waves per candidate: narrow, CPW 1");
-  using S = typename std::conditional<WIDE, SmemW, typename std::conditional<WPC == 2, SmemN2, SmemN>::type>::type;
+  static_assert(WPC == 1 || (WPC == 2 && SmemN::CPW == 1), "two waves per candidate: CPW 1");
+  using S = typename std::conditional<WIDE, typename std::conditional<WPC == 2, SmemW2, SmemW>::type,
+                                      typename std::conditional<WPC == 2, SmemN2, SmemN>::type>::type;
   const int wv = WPC == 2 ? (int)(threadIdx.x >> 6) : 0;
   const bool run_main = WPC == 1 || wv == 0, run_coll = WPC == 1 || wv == 1;
   static_assert(S::NVW == NVW && S::NBW == NBW && S::NGW == NGW, "variant widths");
@@ -4203,8 +4204,34 @@ int rollout_set_wpc2_max_n(int n) {
   return prev;
 }
 
+// Dual-arm batches up to min(this, the narrow threshold above) run two waves
+// per candidate too (rollout_kernel<32, 32, 72, true, 2>: collision, the MPR
+// flush and the manifolds beside the dynamics).  Its 29 KB image and 235
+// VGPRs leave 4 blocks per CU, so the default is 4 x 256 CUs: every candidate
+// resident in one round (measured on MI355X, H = 100: 1024 candidates 22.6 ->
+// 21.2 ms; 2048 would take two rounds, 24.5 -> 46.3 ms).  Bitwise the one-wave
+// results.  MPCR_WPC2W_MAX_N overrides.
+#ifndef MPCR_W_WPC2
+#define MPCR_W_WPC2 1
+#endif
+#if MPCR_W_WPC2
+static int wpc2w_max_n() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MPCR_WPC2W_MAX_N");
+    v = e ? atoi(e) : 1024;
+  }
+  return min(v, wpc2_max_n());
+}
+#endif
+
 void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigned grid, size_t dyn_lds,
                     hipStream_t st) {
+#if MPCR_W_WPC2
+  if (wide && (int)grid <= wpc2w_max_n())
+    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);
+  else
+#endif
   if (wide)
     hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), 0, st, a, dm);
   else if (SmemN::CPW == 1 && (int)grid <= wpc2_max_n())

@@ -389,7 +389,7 @@ def test_kernel_occupancy_budget(torch_cuda):
     assert wlds <= 152448 // 8 and wreg <= 256 and wb >= 8, list(info)
 
 
-@pytest.mark.parametrize("name,n", [("ur5e_hande_mjx", 1024), ("scene_mjx", 512)])
+@pytest.mark.parametrize("name,n", [("ur5e_hande_mjx", 1024), ("scene_mjx", 512), ("dual_arm", 1024)])
 def test_two_wave_variant_is_bitwise_one_wave(torch_cuda, name, n):
     """Small batches may run two waves per candidate (collision beside the
     dynamics, mpcr_set_two_wave_max_n): the same instructions on the same data,

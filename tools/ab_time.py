@@ -59,3 +59,5 @@ rows = f" rows/step {float((sv >> 8).mean()) / H:.1f} max-rows p50/p90/p99 " + "
     str(int(np.percentile((sv >> 2) & 63, q))) for q in (50, 90, 99))
 print(f"{os.path.basename(sys.argv[1])}{occ}{rows} {name} median {np.median(ts):.3f} ms min {np.min(ts):.3f} "
       f"-> {n / np.median(ts) * 1e3:.0f} rollouts/s  cost0 {float(c4[:, 0].sum()):.6e}")
+if os.environ.get("SAVE"):  # outputs of the last launch, for bitwise comparisons between variants
+    np.savez(os.environ["SAVE"], c4=c4.cpu().numpy(), th=None if th is None else th.cpu().numpy(), st=sv)
