@@ -41,7 +41,7 @@ PT = (-0.3, -0.3, 0.5)
 QT = (0.0, 1.0, 0.0, 0.0)
 PEAK_F32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (FMA) peak
 PEAK_HBM_GBS = 8000.0
-PROFILE_TAG = "r03"
+PROFILE_TAG = "r04"
 
 # BASELINE.json configs; c3 is the metric's workload (default)
 CONFIGS = {
@@ -174,6 +174,80 @@ def cpu_baseline(m, xi, H, Pd, threads, reps=5, precision="fp32"):
     return n / float(np.median(ts)), [round(n / t, 1) for t in ts]
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc, argv, grace_s=30.0):
+    """`python bench.py --gpus N` outside torch.distributed.run: start N fresh
+    child processes of this script, one per GPU (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT in their environment), and return
+    the worst child's exit code.  Called before anything imports torch, so the
+    parent never touches the GPU; the children inherit stdout, and rank 0's
+    JSON line is the run's output.  When a rank fails, the others get
+    `grace_s` seconds to end on their own (a collective's error reaches them)
+    and are then killed by PID."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    deadline = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        if deadline is None and any(rc not in (None, 0) for rc in rcs):
+            deadline = time.monotonic() + grace_s
+        if deadline is not None and time.monotonic() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.05)
+    # a signal death (negative returncode) maps to the shell's 128 + signal
+    codes = [rc if rc >= 0 else 128 - rc for rc in (p.returncode for p in procs)]
+    return max(codes)
+
+
+def launch_selftest():
+    """--launch-selftest: the spawn path's plumbing without a GPU (CPU test,
+    tests/test_bench_launch.py): each rank joins a gloo group and all-reduces;
+    rank 0 prints one JSON line; MPCR_SELFTEST_FAIL_RANK=r makes rank r exit 3."""
+    import torch
+    import torch.distributed as dist
+    rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    if os.environ.get("MPCR_SELFTEST_FAIL_RANK") == str(rank):
+        sys.exit(3)
+    dist.init_process_group("gloo")
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}
+    if rank == 0:
+        print(json.dumps({"world": world, "sum_ranks_plus_1": int(t.item()), "env": env}))
+    dist.destroy_process_group()
+
+
+def committed_counters(kind, sfx):
+    """A committed rocprof counter CSV (profiles/<tag>_pmc_<kind><sfx>.csv) and
+    its provenance, attached only when the profile manifest
+    (profiles/<tag>_pmc_manifest.json) records the same libmpcr.so source hash
+    as this checkout -- a profile of an earlier build is not this run's."""
+    from manipulator_mujoco_amd import build as b
+    path = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_{kind}{sfx}.csv")
+    man = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_manifest.json")
+    if not (os.path.exists(path) and os.path.exists(man)):
+        return None, None
+    rec = json.load(open(man)).get(os.path.basename(path))
+    if not rec or rec.get("source_hash") != b.source_hash():
+        return None, "stale (profile of another build, not attached)"
+    return path, "committed 1-GPU profile of this build (" + os.path.relpath(path, ROOT) + ")"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,7 +275,14 @@ def main():
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="N > 1: nccl (= RCCL over xGMI, one GPU per rank) or gloo (host-staged; ranks may share "
                          "a GPU, device = local rank mod the visible GPUs: rehearses the multi-rank path on one GPU)")
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # not under torch.distributed.run: one fresh process per GPU, spawned
+        # before this process imports torch (it never initialises the GPU)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_selftest:
+        return launch_selftest()
     cfg = CONFIGS[args.config]
     args.model = args.model or cfg["model"]
     args.n = args.n or cfg["n"]
@@ -218,8 +299,6 @@ def main():
     from manipulator_mujoco_amd.projection import ProjectionFilter
 
     rank, world, local = md.env_rank()
-    if world == 1 and args.gpus > 1:
-        raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
 
     H = args.horizon
     if args.scaling == "strong":
@@ -348,24 +427,28 @@ def main():
                    "first_active_step_median": float(np.median(first[first >= 0])) if (first >= 0).any() else None}
 
     if rank == 0:
+        coll = {"nccl": "RCCL (xGMI)", "gloo": "gloo (host-staged)"}.get(backend, str(backend))
         value = n_total * args.steps / elapsed
         fps = flops_per_step(m, nefc_mean, args.model)  # mean constraint rows/step measured by the kernel
         flops_launch = fps * H * n
         achieved_tf = flops_launch / (kern_ms * 1e-3) / 1e12
         hbm_launch = n * (66 * 4 + 16 + 2 * 6 * H * 4 + 4)  # xi in; cost4, theta, thetadot, status out
-        # the committed counter passes of this exact workload (the config's own
-        # batch, weak mode): C3 r03_pmc_rollout.csv / r03_pmc_sq.csv, the other
-        # configs the same names suffixed _c2 / _c4
-        default_prof = args.n == cfg["n"] and args.scaling == "weak"
+        # counters: the CSVs passed explicitly (--pmc / --pmc-sq, a profile of
+        # this command), else the committed 1-GPU passes of this exact workload
+        # (the config's own batch, weak mode, one rank) when they were taken
+        # from this build: C3 <tag>_pmc_rollout.csv / _sq.csv, the other
+        # configs the same names suffixed _c2 / _c4.  A multi-rank line gets
+        # none: no rank of it was profiled.
+        default_prof = args.n == cfg["n"] and args.scaling == "weak" and world == 1
         sfx = "" if args.config == "c3" else "_" + args.config
-
-        def committed(kind):
-            path = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_{kind}{sfx}.csv")
-            return path if default_prof and os.path.exists(path) else None
-        pmc = args.pmc or committed("rollout")
-        pmc_sq = args.pmc_sq or committed("sq")
+        pmc, pmc_src = (args.pmc, "--pmc " + args.pmc) if args.pmc else (
+            committed_counters("rollout", sfx) if default_prof else (None, None))
+        pmc_sq, sq_src = (args.pmc_sq, "--pmc-sq " + args.pmc_sq) if args.pmc_sq else (
+            committed_counters("sq", sfx) if default_prof else (None, None))
         traffic = pmc_traffic(pmc) if pmc else None
         valu = pmc_valu(pmc_sq, n, H, fps) if pmc_sq else None
+        if valu is not None:
+            valu["source"] = sq_src
         rec = {
             "metric": METRIC, "value": round(value, 1), "unit": "rollouts/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
@@ -378,12 +461,16 @@ def main():
                        "parallelism": f"dp{world} (candidate shards; {args.exchange} exchange)",
                        "world_size_seen": world, "backend": backend or "single process",
                        "gpus_visible": ndev,
-                       "exchange": "8-byte RCCL MIN all-reduce of the best key" + (
-                           "; local top-E + RCCL all-gather of (xi, cost) rows + global top-E"
+                       "launcher": ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
+                                    else "bench.py self-launch" if world > 1 else "single process"),
+                       "exchange": ("none (one rank: the fused atomic-min key is the global best)" if world == 1
+                                    else f"8-byte {coll} MIN all-reduce of the best key") + (
+                           f"; local top-E + {coll} all-gather of (xi, cost) rows + global top-E"
                            if args.exchange == "elite" else "")},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_VALU_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_VALU_TFLOPS, 5),
                          "traffic": None if traffic is None else round(traffic),
+                         "traffic_source": pmc_src if traffic is not None else pmc_src or "not profiled in this run",
                          "kernel": "rollout_kernel", "kernel_ms": round(kern_ms, 4),
                          "kernel_ms_mean": round(float(np.mean(kms)), 4),
                          "flops_per_step": fps, "hbm_algorithmic_bytes": hbm_launch,

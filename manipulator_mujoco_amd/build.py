@@ -42,6 +42,20 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-pass-failed",
          "-Xarch_device", "-fapprox-func", "-mllvm", "-simplifycfg-sink-common=false"]
 
 
+def source_hash() -> str:
+    """sha256 over libmpcr.so's sources and compile flags: identifies the build
+    a committed counter profile was taken from (bench.py attaches committed
+    rocprof counters only to a run of the same build)."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in DEPS:
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    h.update(repr((FLAGS, [f for _, f in UNITS])).encode())
+    return h.hexdigest()[:16]
+
+
 def hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if c and os.path.exists(c):

@@ -49,3 +49,24 @@ def test_bench_two_ranks_equal_one_gpu():
     assert two["elites"]["exchanges_timed"] == 2
     assert two["elites"]["cost_sum"] == one["elites"]["cost_sum"]
     assert two["elites"]["first"] == one["elites"]["first"]
+
+
+def test_bench_self_launch_two_ranks_equal_one_gpu():
+    """`python bench.py --gpus 2` without torchrun: the
+    parent spawns the two ranks itself; same best and elites as one GPU, and
+    the multi-rank line carries no borrowed one-GPU counters."""
+    one = _run([sys.executable, "bench.py"] + COMMON)
+    env_clean = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo"] + COMMON, cwd=ROOT,
+                       env=env_clean, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    two = json.loads(lines[0])
+    assert two["config"]["launcher"] == "bench.py self-launch"
+    assert two["config"]["world_size_seen"] == 2 and two["config"]["backend"] == "gloo"
+    assert "gloo" in two["config"]["exchange"] and "RCCL" not in two["config"]["exchange"]
+    assert two["roofline"]["traffic"] is None and "valu" not in two["roofline"]
+    assert two["best"] == one["best"]
+    assert two["elites"]["cost_sum"] == one["elites"]["cost_sum"]
+    assert two["elites"]["first"] == one["elites"]["first"]
