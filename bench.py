@@ -152,18 +152,23 @@ def _host_cpu():
     return usable, os.cpu_count() or 1, model, aff, quota
 
 
+EXACT_MPR = 4  # oracle/mpcr_oracle.c: ccd_tolerance exact; Newton / line-search floors as in the kernel
+
+
 def cpu_baseline(m, xi, H, Pd, threads, reps=5, precision="fp32"):
     """The scalar C oracle (oracle/mpcr_oracle.c, a restatement of the
     reference's rollout + cost, SBP/mjx_planner.py:123-124; precision "fp32"
     = oracle_f32.c, every double as float, the reference's own precision) on
     host threads: pool started and model converted before the clock; median
-    of `reps` timed repetitions of the rollout compute only.  Returns
-    rollouts/s."""
+    of `reps` timed repetitions of the rollout compute only.  The fp32 build
+    runs the kernel's stop rules (EXACT_MPR only: the fp32 Newton /
+    line-search floors), the fp64 build MuJoCo's.  Returns rollouts/s."""
     import oracle
     oracle.build()
     n = xi.shape[0]
     td = np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
-    run = oracle.Runner(m, threads, Q0, W, PT, QT, precision=precision)
+    run = oracle.Runner(m, threads, Q0, W, PT, QT, precision=precision,
+                        exact_mask=EXACT_MPR if precision == "fp32" else None)
     run.rollout(td[: max(1, min(n, threads))])  # warm-up (page in, first-touch)
     ts = []
     for _ in range(reps):
@@ -342,6 +347,8 @@ def main():
                              f"(pool and model set up before the clock); 1 thread: {v32_1:.1f} rollouts/s; fp64 "
                              f"build: {v64:.1f} ({threads} threads), {v64_1:.1f} (1 thread)",
                    "precision": "fp32", "one_core": round(v32_1, 1), "reps": reps,
+                   "stop_rules": "fp32: the kernel's (ccd_tolerance 1e-6, fp32 Newton / line-search floors); "
+                                 "fp64: MuJoCo's (ccd_tolerance 1e-6, scale*dcost < tol, no bracket floor)",
                    "affinity_threads": None if v32_aff is None else {"threads": aff, "value": round(v32_aff, 1)},
                    "fp64": {"value": round(v64, 1), "one_core": round(v64_1, 1), "reps": reps64},
                    "host": {"usable_cores": usable, "affinity_cores": aff, "cgroup_cpu_quota": quota, "nproc": ncpu,
@@ -414,7 +421,7 @@ def main():
     elapsed, kern_ms = float(t[0]), float(t[1])
     idx, best = md.decode_key(int(key.item()))
     trunc = int((status & 1).sum().item())
-    nefc_mean = float((status >> 8).double().mean().item()) / H
+    nefc_mean = float((status >> 10).double().mean().item()) / H
 
     contact = None
     if rank == 0 and not args.no_contact_report and m.nslot:
@@ -463,10 +470,11 @@ def main():
                        "gpus_visible": ndev,
                        "launcher": ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
                                     else "bench.py self-launch" if world > 1 else "single process"),
-                       "exchange": ("none (one rank: the fused atomic-min key is the global best)" if world == 1
-                                    else f"8-byte {coll} MIN all-reduce of the best key") + (
-                           f"; local top-E + {coll} all-gather of (xi, cost) rows + global top-E"
-                           if args.exchange == "elite" else "")},
+                       "exchange": ("none (one rank: the fused atomic-min key is the global best"
+                                    + ("; the local top-E is the global top-E)" if args.exchange == "elite" else ")")
+                                    if world == 1 else f"8-byte {coll} MIN all-reduce of the best key" + (
+                                        f"; local top-E + {coll} all-gather of (xi, cost) rows + global top-E"
+                                        if args.exchange == "elite" else ""))},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_VALU_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_VALU_TFLOPS, 5),
                          "traffic": None if traffic is None else round(traffic),

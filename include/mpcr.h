@@ -115,8 +115,8 @@ void mpcr_engine_free(mpcr_engine* e);
                         (ordered(cost) << 32 | (index_base + i)), NaN first (nullable)
    status [n]           per-candidate flags (bit0: constraint rows truncated,
                         bit1: non-finite state) | (max constraint rows in
-                        one step, capped at 63, << 2) | (constraint rows
-                        summed over the horizon << 8)            (nullable)
+                        one step, 8 bits capped at 255, << 2) | (constraint
+                        rows summed over the horizon << 10)      (nullable)
    stream               hipStream_t or NULL (default stream)
    n = 0 is a no-op returning MPCR_OK (input and cost4 may then be NULL). */
 int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
@@ -134,7 +134,8 @@ int mpcr_rollout_occupancy(int device, int* info);
    the 1024: four two-wave blocks per CU).  0 disables both.
    n < 0 only queries.  Returns the previous threshold (default: the build's
    MPCR_WPC2_MAX_N_DEFAULT, or the MPCR_WPC2_MAX_N environment variable).
-   Process-wide: set it before launches, not while one is in flight. */
+   Process-wide (an atomic read by every engine's next launch; the
+   environment is read once, when the library loads). */
 int mpcr_set_two_wave_max_n(int n);
 
 /* Same as mpcr_rollout_cost with MPCR_F_DEVICE_PTRS, except that the

@@ -1476,6 +1476,16 @@ extern "C" int mpcr_cem_create(int device, int num_dof, int horizon, int nbasis,
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return fail(MPCR_ENODEV, "device %d is %s; libmpcr is built for gfx950 only", device, prop.gcnArchName);
   const int nd = num_dof, H = horizon, nb = PJ_NB, nv = nd * nb, ne = 5 * nd, NK = nv + ne, LD = nd * PJ_BLK;
+  {
+    // sample_project_kernel stages the constraint rows X (3 x H x 12) and the
+    // candidates' rows in LDS (mpcr_cem_sample_project): refuse a horizon
+    // whose image exceeds the device's per-workgroup LDS
+    const int cpw = PJ_CPW_LARGE > PJ_CPW_SMALL ? PJ_CPW_LARGE : PJ_CPW_SMALL;
+    const size_t lds = sizeof(float) * (cpw * (nd * PJ_BLK + 4) + 3 * (size_t)H * PJ_BLK);
+    if (lds > prop.sharedMemPerBlock)
+      return fail(MPCR_EINVAL, "horizon=%d: the projection kernel's LDS image (%zu B) exceeds the device's %zu B per "
+                  "workgroup", H, lds, (size_t)prop.sharedMemPerBlock);
+  }
   std::vector<float> Pf((size_t)H * nb), Pdf((size_t)H * nb), Pddf((size_t)H * nb);
   for (int i = 0; i < H * nb; i++) { Pf[i] = (float)P[i]; Pdf[i] = (float)Pdot[i]; Pddf[i] = (float)Pddot[i]; }
   std::vector<double> Kinv;

@@ -15,6 +15,7 @@
 //   cost                     SBP/mjx_planner.py:276-303
 //   mjx.step                 mujoco-mjx 3.3.1 (third party)
 #include <cstdlib>
+#include <atomic>
 
 #include "rollout.h"
 #include "../../include/mpcr_model.h"  // MPCR_LUT_R (the hull start table layout)
@@ -4157,7 +4158,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     args.cost4[4 * (size_t)b + 1] = cost_g;
     args.cost4[4 * (size_t)b + 2] = cost_r;
     args.cost4[4 * (size_t)b + 3] = cost_c;
-    if (args.status) args.status[b] = status | (min(nefc_max, 63) << 2) | (nefc_sum << 8);
+    if (args.status) args.status[b] = status | (min(nefc_max, 255) << 2) | (nefc_sum << 10);
     if (args.best_key) {
       const uint32_t u = __float_as_uint(cost);
       uint32_t key = isnan(cost) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
@@ -4190,18 +4191,16 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
 // batches up to this many candidates run the narrow variant with two waves
 // per candidate (MPCR_WPC2_MAX_N overrides; 0 disables): below one
 // candidate per SIMD pair the second wave of a SIMD is otherwise idle
-static int g_wpc2_max_n = -1;
-static int wpc2_max_n() {
-  if (g_wpc2_max_n < 0) {
-    const char* e = getenv("MPCR_WPC2_MAX_N");
-    g_wpc2_max_n = e ? atoi(e) : MPCR_WPC2_MAX_N_DEFAULT;
-  }
-  return g_wpc2_max_n;
+// (process-wide, atomic: read by every engine's launches, initialised once
+// from the environment when the library loads)
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
+static std::atomic<int> g_wpc2_max_n{env_int("MPCR_WPC2_MAX_N", MPCR_WPC2_MAX_N_DEFAULT)};
+static int wpc2_max_n() { return g_wpc2_max_n.load(std::memory_order_relaxed); }
 int rollout_set_wpc2_max_n(int n) {
-  const int prev = wpc2_max_n();
-  if (n >= 0) g_wpc2_max_n = n;
-  return prev;
+  return n >= 0 ? g_wpc2_max_n.exchange(n) : wpc2_max_n();
 }
 
 // Dual-arm batches up to min(this, the narrow threshold above) run two waves
@@ -4215,14 +4214,8 @@ int rollout_set_wpc2_max_n(int n) {
 #define MPCR_W_WPC2 1
 #endif
 #if MPCR_W_WPC2
-static int wpc2w_max_n() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MPCR_WPC2W_MAX_N");
-    v = e ? atoi(e) : 1024;
-  }
-  return min(v, wpc2_max_n());
-}
+static const int g_wpc2w_max_n = env_int("MPCR_WPC2W_MAX_N", 1024);
+static int wpc2w_max_n() { return min(g_wpc2w_max_n, wpc2_max_n()); }
 #endif
 
 void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigned grid, size_t dyn_lds,

@@ -199,9 +199,16 @@ class Runner:
     """Cost-only rollouts on a fixed thread pool over one prepared model
     struct -- what bench.py's cpu_baseline times: the pool is started and the
     model converted before the clock, each call is only the C rollouts
-    (ctypes drops the GIL, so the threads run the C code concurrently)."""
+    (ctypes drops the GIL, so the threads run the C code concurrently).
 
-    def __init__(self, model, workers, q0, w, ptgt, qtgt, precision="fp64"):
+    exact_mask: the EXACT_* rules of mpcr_oracle.c for these rollouts (None =
+    the library default, MuJoCo's stop tests).  bench.py's fp32 baseline uses
+    EXACT_MPR only, i.e. the kernel's own rules (ccd_tolerance 1e-6 and the
+    fp32 Newton / line-search floors): fp32 without the floors iterates on
+    rounding noise, which would inflate the GPU/CPU ratio.  Set on
+    the library while the Runner lives (process-global: one Runner at a time)."""
+
+    def __init__(self, model, workers, q0, w, ptgt, qtgt, precision="fp64", exact_mask=None):
         from concurrent.futures import ThreadPoolExecutor
         self.model, self.workers = model, max(1, int(workers))
         self.dt = np.float32 if precision == "fp32" else np.float64
@@ -210,6 +217,10 @@ class Runner:
         ct = ctypes.c_float if precision == "fp32" else ctypes.c_double
         self.p = lambda a: None if a is None else a.ctypes.data_as(ctypes.POINTER(ct))  # noqa: E731
         self.args = [np.ascontiguousarray(x, dtype=self.dt) for x in (q0, w, ptgt, qtgt)]
+        self.prev_exact = None
+        if exact_mask is not None:
+            self.prev_exact = self.L.oracle_get_exact()
+            self.L.oracle_set_exact(int(exact_mask))
         self.ex = ThreadPoolExecutor(self.workers)
         list(self.ex.map(lambda i: i, range(self.workers)))  # start every thread now
 
@@ -235,6 +246,9 @@ class Runner:
 
     def close(self):
         self.ex.shutdown()
+        if self.prev_exact is not None:
+            self.L.oracle_set_exact(self.prev_exact)
+            self.prev_exact = None
 
 
 def cone_eval(mu, fri, D, jar, jv, alpha):

@@ -1404,11 +1404,16 @@ static void col_plane_mesh(const mpcr_model_t* m, odata* d, int pair, int gp, in
 
 #define POLY_CONE_COS 0.94 /* ~20 degrees: the candidate faces' Gauss-map cone about MPR's normal */
 
-/* world outward normal and offset (n . x = off) of face f of geom g */
-static void face_world(const mpcr_model_t* m, const odata* d, int g, int f, double nw[3], double* off) {
+/* world outward normal and offset (n . (x - c) = off) of face f of geom g,
+   relative to the point c (the manifold works relative to g2's centre, as
+   MPR and the kernel do: world coordinates would carry ~1e-7 m of fp32
+   rounding into every separation, relative ones ~ulp(5 cm)) */
+static void face_world(const mpcr_model_t* m, const odata* d, int g, int f, double nw[3], double* off,
+                       const double* c) {
   const double* R = d->geom_xmat[g];
   mulmv(nw, R, m->face_plane[f]);
-  *off = m->face_plane[f][3] + dot3(nw, d->geom_xpos[g]);
+  const double dx[3] = {d->geom_xpos[g][0] - c[0], d->geom_xpos[g][1] - c[1], d->geom_xpos[g][2] - c[2]};
+  *off = m->face_plane[f][3] + dot3(nw, dx);
 }
 
 /* hull vertex index of geom g's support point along dir (world): the mesh
@@ -1429,15 +1434,18 @@ static int support_vertex(const mpcr_model_t* m, const odata* d, int g, const do
   return *hint;
 }
 
-static void vert_world(const mpcr_model_t* m, const odata* d, int g, int v, double w[3]) {
+/* hull vertex v of geom g relative to c */
+static void vert_world(const mpcr_model_t* m, const odata* d, int g, int v, double w[3], const double* c) {
   mulmv(w, d->geom_xmat[g], m->hull_vert[v]);
-  for (int k = 0; k < 3; k++) w[k] += d->geom_xpos[g][k];
+  for (int k = 0; k < 3; k++) w[k] += d->geom_xpos[g][k] - c[k];
 }
 
-/* support value of geom g along dir (world, unit): max over its vertices of dir . x */
-static double support_value(const mpcr_model_t* m, const odata* d, int g, const double dir[3], int* hint) {
+/* support value of geom g along dir (unit), relative to c: max over its
+   vertices of dir . (x - c) */
+static double support_value(const mpcr_model_t* m, const odata* d, int g, const double dir[3], int* hint,
+                            const double* c) {
   double p[3];
-  support(m, d, g, dir, p, hint);
+  support_rel(m, d, g, dir, p, hint, c);
   return dot3(p, dir);
 }
 
@@ -1467,6 +1475,7 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   const int h0 = d->hint[pair][0], h1 = d->hint[pair][1];
   int h;
   const double nn[3] = {-n[0], -n[1], -n[2]};
+  const double* cg = d->geom_xpos[g2]; /* the frame's origin: g2's centre */
   const long climb0 = g_mpr_stats[2];
   g_mpr_stats[8]++;
   h = h0;
@@ -1490,7 +1499,7 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
     const int ls = sd ? m->vert_faceadr[s2] : m->vert_faceadr[s1];
     for (int f = fa; f < fa + m->geom_facenum[g] && nc < 64; f++) {
       double nf[3], off;
-      face_world(m, d, g, f, nf, &off);
+      face_world(m, d, g, f, nf, &off, cg);
       if ((sd ? -1.0 : 1.0) * dot3(nf, n) < POLY_CONE_COS) continue;
       int dup = 0;
       for (int k = 0; k < cs; k++) dup |= m->vert_face[ls + k] == f;
@@ -1505,10 +1514,10 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   for (int k = 0; k < nc; k++) {
     const int two = side[k], g = two ? g2 : g1, go = two ? g1 : g2;
     double nf[3], off, mnf[3];
-    face_world(m, d, g, fid[k], nf, &off);
+    face_world(m, d, g, fid[k], nf, &off, cg);
     for (int c = 0; c < 3; c++) mnf[c] = -nf[c];
     h = two ? h0 : h1;
-    sep[k] = -support_value(m, d, go, mnf, &h) - off; /* min over go of nf . x, minus the plane */
+    sep[k] = -support_value(m, d, go, mnf, &h, cg) - off; /* min over go of nf . x, minus the plane */
     if (sep[k] > mx) mx = sep[k];
   }
   /* the maximum's tie band: the lowest face index (a flush face pair has the
@@ -1520,7 +1529,7 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   if (kb < 0 || -sep[kb] > 1.05 * depth + 1e-5) return 0; /* an edge axis carries the contact */
   const int best_f = fid[kb], gr = side[kb] ? g2 : g1, gi = side[kb] ? g1 : g2;
   double nr[3], offr;
-  face_world(m, d, gr, best_f, nr, &offr);
+  face_world(m, d, gr, best_f, nr, &offr, cg);
   /* incident face: the most anti-parallel face on gi's support vertex along -nr */
   const double mnr[3] = {-nr[0], -nr[1], -nr[2]};
   h = gi == g1 ? h0 : h1;
@@ -1530,7 +1539,7 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   mx = -1e300;
   for (int k = 0; k < ci; k++) {
     double nf[3], off;
-    face_world(m, d, gi, m->vert_face[m->vert_faceadr[si] + k], nf, &off);
+    face_world(m, d, gi, m->vert_face[m->vert_faceadr[si] + k], nf, &off, cg);
     al[k] = -dot3(nf, nr);
     if (al[k] > mx) mx = al[k];
   }
@@ -1543,8 +1552,8 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   double poly[2][MAXP][3], ref[MPCR_FACE_MAXV][3];
   int np = m->face_vnum[inc_f], cur = 0;
   const int nrv = m->face_vnum[best_f];
-  for (int k = 0; k < np; k++) vert_world(m, d, gi, m->face_vert[m->face_vadr[inc_f] + k], poly[0][k]);
-  for (int k = 0; k < nrv; k++) vert_world(m, d, gr, m->face_vert[m->face_vadr[best_f] + k], ref[k]);
+  for (int k = 0; k < np; k++) vert_world(m, d, gi, m->face_vert[m->face_vadr[inc_f] + k], poly[0][k], cg);
+  for (int k = 0; k < nrv; k++) vert_world(m, d, gr, m->face_vert[m->face_vadr[best_f] + k], ref[k], cg);
   g_mpr_stats[11]++;
   g_mpr_stats[12] += nrv;
   g_mpr_stats[13] += np;
@@ -1589,10 +1598,10 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
        it ends on, a path that fp32 and fp64 take differently) */
     g_mpr_stats[5]++;
     double P[3], pos[3];
-    vert_world(m, d, gi, si, P);
+    vert_world(m, d, gi, si, P, cg);
     const double dk = dot3(nr, P) - offr;
     if (!(dk < margin)) return 0;
-    for (int c = 0; c < 3; c++) pos[c] = P[c] - 0.5 * dk * nr[c];
+    for (int c = 0; c < 3; c++) pos[c] = P[c] + cg[c] - 0.5 * dk * nr[c];
     set_contact(&out[0], dk, pos, cn);
     PROBE(8, 2);
     return 1;
@@ -1638,7 +1647,7 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
     if (dup) continue;
     const int k = idx[s];
     double pos[3];
-    for (int c = 0; c < 3; c++) pos[c] = pts[k][c] - 0.5 * dist[k] * nr[c];
+    for (int c = 0; c < 3; c++) pos[c] = pts[k][c] + cg[c] - 0.5 * dist[k] * nr[c];
     set_contact(&out[s], dist[k], pos, cn);
   }
   return 1;
