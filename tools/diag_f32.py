@@ -1,17 +1,20 @@
-"""Where does fp32 arithmetic move a well-conditioned candidate?  (CPU
-diagnostic, no GPU)
+"""Which mechanism moves a well-conditioned candidate?  (diagnostic)
 
-The fp32 build of the oracle (oracle/oracle_f32.c) is a proxy for the
-kernel's own rounding: on a dual-arm batch this lists the candidates that
-probe A calls well-conditioned (tests/parity_util.py) but whose fp32 cost
-misses 1e-4, then replays each in fp64 step by step and evaluates every step
-in both precisions from the same fp64 state: the first step whose fp32 qacc
-leaves the fp64 one by far more than rounding the state to fp32 does, and
-the contacts that differ there, name the mechanism.
+CPU mode (default, no GPU): the fp32 build of the oracle (oracle/oracle_f32.c)
+stands in for the kernel's own rounding.  GPU mode (--gpu): the kernel
+itself -- the batch of the GPU parity tests (projected on the GPU), costs
+from the rollout kernel, per-step evaluations from the plant
+(mpcr_plant_step_debug, the same kernel with n = 1, H = 1).
 
-    python tools/diag_f32.py [model=dual_arm] [n=1024] [H=100] [seed=4] [max_cands=12]
-Env ORACLE_MASK: the oracle's EXACT_* mask for both builds (default 4 = the
-kernel's stop rules).
+Lists the candidates that probe A calls well-conditioned
+(tests/parity_util.py) but whose fp32 / GPU cost misses 1e-4, then replays
+each in fp64 step by step and evaluates every step in both precisions from
+the same fp64 state: the outlier step (fp32 qacc error far above its
+per-step floor and far above what rounding the state moves) and the contacts
+that differ there name the mechanism; a tally closes the run.
+
+    python tools/diag_f32.py [--gpu] [model=dual_arm] [n=1024] [H=100] [seed=4] [max_cands=12]
+Env ORACLE_MASK: the oracle's EXACT_* mask (default 4 = the kernel's stop rules).
 """
 import os
 import sys
@@ -33,12 +36,16 @@ from manipulator_mujoco_amd.projection import ProjectionFilter  # noqa: E402
 TYPES = {0: "plane", 2: "sphere", 3: "capsule", 5: "cylinder", 6: "box", 7: "mesh"}
 
 
-def batch(m, n, H, seed):
+def batch_xi(n, H, seed, device="cpu"):
     _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
-    f = ProjectionFilter(P, Pd, Pdd, 6, torch.device("cpu"))
+    f = ProjectionFilter(P, Pd, Pdd, 6, torch.device(device))
     rng = np.random.default_rng(20250629 + seed)
-    xi = f(torch.tensor(rng.normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32)),
-           f.boundary(pu.Q0, np.zeros(6), np.zeros(6), n), 10).numpy()
+    xi = torch.tensor(rng.normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32), device=device)
+    return f(xi, f.boundary(pu.Q0, np.zeros(6), np.zeros(6), n), 10).cpu().numpy(), Pd
+
+
+def batch(m, n, H, seed, device="cpu"):
+    xi, Pd = batch_xi(n, H, seed, device)
     return np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
 
 
@@ -47,6 +54,11 @@ def pair_name(m, p):
     g1, g2 = int(m.pair_geom1[p]), int(m.pair_geom2[p])
     return (f"{G[g1]}:{TYPES.get(int(m.geom_type[g1]), m.geom_type[g1])}-"
             f"{G[g2]}:{TYPES.get(int(m.geom_type[g2]), m.geom_type[g2])}")
+
+
+def pair_kind(m, p):
+    t1, t2 = int(m.geom_type[m.pair_geom1[p]]), int(m.geom_type[m.pair_geom2[p]])
+    return f"{TYPES.get(t1, t1)}-{TYPES.get(t2, t2)}"
 
 
 def replay(m, td_row, H):
@@ -67,8 +79,36 @@ def replay(m, td_row, H):
     return out
 
 
+def contact_diffs(m, d64, d32, quiet=False):
+    """Pairs whose contacts differ between the two evaluations of one step."""
+    p64, p32 = list(d64["con_pair"]), list(d32["con_pair"])
+    culprits = set()
+    for p in sorted(set(p64) | set(p32)):
+        k64 = [k for k in range(len(p64)) if p64[k] == p]
+        k32 = [k for k in range(len(p32)) if p32[k] == p]
+        if len(k64) != len(k32):
+            if not quiet:
+                print(f"   pair {p} {pair_name(m, p)} func {m.pair_func[p]}: contacts 64 {len(k64)} 32 {len(k32)} "
+                      f"d64 {[round(float(d64['con_dist'][k]), 6) for k in k64]} "
+                      f"d32 {[round(float(d32['con_dist'][k]), 6) for k in k32]}")
+            culprits.add(p)
+            continue
+        for k, j in zip(k64, k32):
+            dn = np.abs(d64["con_normal"][k] - d32["con_normal"][j]).max()
+            dp = np.abs(d64["con_pos"][k] - d32["con_pos"][j]).max()
+            dd = abs(d64["con_dist"][k] - d32["con_dist"][j])
+            if dn > 1e-4 or dp > 1e-5 or dd > 1e-6:
+                if not quiet:
+                    print(f"   pair {p} {pair_name(m, p)} func {m.pair_func[p]}: depth {d64['con_dist'][k]:.5f} "
+                          f"n64 {np.round(d64['con_normal'][k], 4)} n32 {np.round(d32['con_normal'][j], 4)} "
+                          f"dpos {dp:.1e} ddist {dd:.1e}")
+                culprits.add(p)
+    return culprits
+
+
 def main():
-    a = sys.argv[1:]
+    a = [x for x in sys.argv[1:] if not x.startswith("--")]
+    gpu = "--gpu" in sys.argv
     name = a[0] if a else "dual_arm"
     n = int(a[1]) if len(a) > 1 else 1024
     H = int(a[2]) if len(a) > 2 else 100
@@ -76,68 +116,66 @@ def main():
     maxc = int(a[4]) if len(a) > 4 else 12
     mask = int(os.environ.get("ORACLE_MASK", 4))
     m = models.load(name, 0.05)
-    td = batch(m, n, H, seed)
+    if gpu:
+        from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine, Plant
+        xi, Pd = batch_xi(n, H, seed, "cuda:0")
+        td = np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
+        e = Engine(m, H, n, Pd)
+        g = e.trace(xi, MPCR_LAYOUT_XI, pu.Q0, pu.W, pu.PT, pu.QT)["cost4"][:, 0].astype(np.float64)
+        plant = Plant(m)
+        label = "GPU"
+    else:
+        td = batch(m, n, H, seed)
+        label = "fp32 oracle"
     t0 = time.time()
     with oracle.exact(mask):
         o, sens = pu.conditioning(m, td)
     print(f"{name} {n} x {H} seed {seed} mask {mask}: conditioning in {time.time() - t0:.0f} s")
     well = (sens < pu.TOL / 10) & ~pu.grazing(m, o)
     pf, pb = o["probe_f4"][:, 0], o["probe_b"]
-    fmiss = np.where(well & (pf >= pu.TOL))[0]
+    rel = np.abs(g - o["cost4"][:, 0]) / np.abs(o["cost4"][:, 0]) if gpu else pf
+    miss = np.where(well & (rel >= pu.TOL))[0]
     print(f"well {int(well.sum())}; probe B well-misses {int((well & (pb >= pu.TOL)).sum())}; "
-          f"probe F (fp32) well-misses {len(fmiss)}, worst {pf[well].max():.2e}")
-    order = fmiss[np.argsort(-pf[fmiss])]
-    print("fp32 well-misses (worst first):", " ".join(f"{i}:{pf[i]:.1e}" for i in order))
+          f"probe F (fp32 oracle) well-misses {int((well & (pf >= pu.TOL)).sum())}; {label} well-misses {len(miss)}, "
+          f"worst {rel[well].max():.2e}")
+    order = miss[np.argsort(-rel[miss])]
+    print(f"{label} well-misses (worst first):", " ".join(f"{i}:{rel[i]:.1e}" for i in order))
     tally = {}
     with oracle.exact(mask):
         for c in order[:maxc]:
             states = replay(m, td[c], H)
-            # the outlier step: fp32 error far above its per-step floor (the
-            # stiff implicit solve leaves ~2e-6 relative on every step) and
-            # far above what rounding the state moves
+            v = td[c].reshape(6, H)
             evals = []
             for t, (qp, qv, ws) in enumerate(states):
                 d64 = oracle.step_debug(m, qp, qv, ws)
-                d32 = oracle.step_debug(m, qp, qv, ws, precision="fp32")
+                if gpu:
+                    plant.set_state(qpos=qp, qvel=qv, qacc_warmstart=ws)
+                    d32 = plant.step_debug(v[:, t])
+                else:
+                    d32 = oracle.step_debug(m, qp, qv, ws, precision="fp32")
                 r32 = [np.asarray(x, dtype=np.float32).astype(np.float64) for x in (qp, qv, ws)]
                 dr = oracle.step_debug(m, *r32)
                 scale = max(1.0, np.abs(d64["qacc"]).max())
                 e32 = np.abs(d32["qacc"] - d64["qacc"]).max() / scale
                 er = np.abs(dr["qacc"] - d64["qacc"]).max() / scale
                 evals.append((t, e32, er, d64, d32))
-            floor = float(np.median([e[1] for e in evals]))
-            cand = [e for e in evals if e[1] > max(1e-5, 10 * floor) and e[1] > 30 * max(e[2], 1e-8)]
-            hit = max(cand, key=lambda e: e[1]) if cand else None
-            if hit is None:
-                print(f"cand {c} (fp32 {pf[c]:.1e}): no single step stands out (accumulated rounding)")
+            # the outlier step: error far above its per-step floor (the stiff
+            # implicit solve leaves ~1e-6 relative on every step) and far above
+            # what rounding the state moves
+            floor = float(np.median([e_[1] for e_ in evals]))
+            cand = [e_ for e_ in evals if e_[1] > max(1e-5, 10 * floor) and e_[1] > 30 * max(e_[2], 1e-8)]
+            if not cand:
+                print(f"cand {c} ({label} {rel[c]:.1e}): no outlier step (per-step floor {floor:.1e}: accumulated)")
                 tally["accumulated"] = tally.get("accumulated", 0) + 1
                 continue
-            t, e32, er, d64, d32 = hit
-            print(f"cand {c} (fp32 {pf[c]:.1e}): step {t} qacc err {e32:.1e} (per-step floor {floor:.1e}, "
-                  f"state rounding {er:.1e}, {len(cand)} outlier steps), "
-                  f"ncon 64 {d64['ncon']} 32 {d32['ncon']}, nefc {d64['nefc']}/{d32['nefc']}")
-            p64, p32 = list(d64["con_pair"]), list(d32["con_pair"])
-            culprits = set()
-            for p in sorted(set(p64) | set(p32)):
-                k64 = [k for k in range(len(p64)) if p64[k] == p]
-                k32 = [k for k in range(len(p32)) if p32[k] == p]
-                if len(k64) != len(k32):
-                    print(f"   pair {p} {pair_name(m, p)} func {m.pair_func[p]}: contacts 64 {len(k64)} 32 {len(k32)} "
-                          f"d64 {[round(float(d64['con_dist'][k]), 6) for k in k64]} "
-                          f"d32 {[round(float(d32['con_dist'][k]), 6) for k in k32]}")
-                    culprits.add(p)
-                    continue
-                for k, j in zip(k64, k32):
-                    dn = np.abs(d64["con_normal"][k] - d32["con_normal"][j]).max()
-                    dp = np.abs(d64["con_pos"][k] - d32["con_pos"][j]).max()
-                    dd = abs(d64["con_dist"][k] - d32["con_dist"][j])
-                    if dn > 1e-4 or dp > 1e-5 or dd > 1e-6:
-                        print(f"   pair {p} {pair_name(m, p)} func {m.pair_func[p]}: depth {d64['con_dist'][k]:.5f} "
-                              f"n64 {np.round(d64['con_normal'][k], 4)} n32 {np.round(d32['con_normal'][j], 4)} "
-                              f"dpos {dp:.1e} ddist {dd:.1e}")
-                        culprits.add(p)
-            key = ", ".join(sorted({pair_name(m, p).split("-")[0].split(":")[1] + "-" +
-                                    pair_name(m, p).split("-")[1].split(":")[1] for p in culprits})) or "solver only"
+            first = cand[0]
+            t, e32, er, d64, d32 = max(cand, key=lambda e_: e_[1])
+            print(f"cand {c} ({label} {rel[c]:.1e}): worst step {t} qacc err {e32:.1e} (floor {floor:.1e}, state "
+                  f"rounding {er:.1e}; {len(cand)} outlier steps, first {first[0]}), ncon 64 {d64['ncon']} "
+                  f"32 {d32['ncon']}, nefc {d64['nefc']}/{d32['nefc']}, iters {d64['info'][0]:.0f}/{d32['info'][0]:.0f} "
+                  f"ls {d64['info'][5]:.0f}/{d32['info'][5]:.0f}")
+            culprits = contact_diffs(m, d64, d32)
+            key = ", ".join(sorted({pair_kind(m, p) for p in culprits})) or "solver only"
             tally[key] = tally.get(key, 0) + 1
     print("mechanisms:", tally)
 

@@ -127,3 +127,7 @@ if [[ $STEPS == *traffic* ]]; then  # HBM traffic attribution (build_variants/t_
   done
 fi
 echo "[session] done"
+if [[ $STEPS == *mech* ]]; then  # which mechanism moves each well-conditioned GPU miss (tools/diag_f32.py --gpu)
+  run mech_c4 600 python -u tools/diag_f32.py --gpu dual_arm 4096 100 4 ${MECH_K:-40}
+  run mech_c3 400 python -u tools/diag_f32.py --gpu scene_mjx 4096 50 3 ${MECH_K:-40}
+fi
