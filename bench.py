@@ -60,7 +60,12 @@ def flops_per_step(m, nefc_mean, model_name=None):
     nb_moving = int(sum(1 for b in range(1, m.nbody) if m.body_weldid[b] != 0))
     names = {0: "plane_capsule", 1: "plane_box", 2: "capsule_capsule", 3: "capsule_box", 4: "box_box", 9: "convex_cull",
              10: "plane_convex"}
-    coll = sum(fm["collision_per_pair"][names[int(f)]] for f in m.pair_func)
+    nex = fm.get("narrow_executed_per_step", {}).get(model_name) if model_name else None
+    if nex:  # executed primitive narrow-phase calls only (culled pairs are not credited)
+        coll = sum(fm["collision_per_pair"][k] * v for k, v in nex.items())
+        coll += sum(fm["collision_per_pair"][names[int(f)]] for f in m.pair_func if names[int(f)] not in nex)
+    else:
+        coll = sum(fm["collision_per_pair"][names[int(f)]] for f in m.pair_func)
     ex = fm["convex_executed_per_step"].get(model_name) if model_name else None
     if ex:  # executed MPR solves and polyhedron manifolds only (culled pairs are not credited)
         coll += ex["mpr_calls"] * fm["collision_per_pair"]["convex"] + ex["hits"] * fm["poly_manifold_per_hit"]

@@ -1722,6 +1722,15 @@ static void col_plane_convex(const mpcr_model_t* m, odata* d, int pair, int gp, 
   set_contact(out, dist, pos, n);
 }
 
+/* diagnostic (oracle_narrow_stats): narrow-phase calls executed per pair
+   function (after the culls), per thread -- what bench/flops_model.json
+   credits per step */
+static __thread long g_narrow_stats[16];
+void oracle_narrow_stats(long* out, int reset) {
+  if (out) memcpy(out, g_narrow_stats, sizeof(g_narrow_stats));
+  if (reset) memset(g_narrow_stats, 0, sizeof(g_narrow_stats));
+}
+
 static void collision(const mpcr_model_t* m, odata* d) {
   d->ncon = m->ncon;
   for (int p = 0; p < m->npair; p++) {
@@ -1757,6 +1766,7 @@ static void collision(const mpcr_model_t* m, odata* d) {
       }
     }
     const double *s1 = m->geom_size[g1], *s2 = m->geom_size[g2];
+    g_narrow_stats[m->pair_func[p] & 15]++;
     switch (m->pair_func[p]) {
       case MPCR_COL_PLANE_CAPSULE: col_plane_capsule(d, g1, g2, s2, out); break;
       case MPCR_COL_PLANE_BOX: col_plane_box(d, g1, g2, s2, out); break;

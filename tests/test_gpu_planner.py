@@ -176,6 +176,45 @@ def _dual_arm_loop(graph, n, H, ticks):
     return p, outs, starts, dist
 
 
+def _check_selected_costs(p, outs, starts, H):
+    """Each tick's selected candidate (best_vels) rolled out by the fp64 oracle
+    from the tick's start costs what the GPU reported for it (cost[-1]), to
+    1e-4 or twice the largest spread of 8 fp32-sized per-step noise draws
+    (tests/parity_util.py)."""
+    import parity_util as pu
+    m = p.model
+    rels = []
+    for out, q0 in zip(outs, starts):
+        td = np.asarray(out[4], dtype=np.float64).T.reshape(1, 6 * H)
+        a = pu.oracle.rollout(m, td, q0, pu.W, PT, QT, want_theta=False)["cost4"][0, 0]
+        sens = 0.0
+        for sd in range(1, 9):
+            b = pu.oracle.rollout(m, td, q0, pu.W, PT, QT, want_theta=False, noise=1e-6, seed=sd)["cost4"][0, 0]
+            sens = max(sens, abs(a - b) / abs(a))
+        rel = abs(float(out[0][-1]) - a) / abs(a)
+        assert rel < max(pu.TOL, 2 * sens), (rel, sens, float(out[0][-1]), a)
+        rels.append(rel)
+    return rels
+
+
+@pytest.mark.parametrize("n,ticks", [(8192, 2), (1024, 3)])
+def test_dual_arm_c5_real_sizes(torch_cuda, n, ticks):
+    """C5 at its real sizes: the dual-arm tick of 8192 x 50
+    x 3 CEM iterations (BASELINE.json configs[4], one GPU) and the 8-GPU rank
+    share of 1024 x 50 (the two-wave dual-arm kernel), graph-captured: graph
+    replay equals eager bit for bit, and every tick's selected cost matches
+    the fp64 oracle's rollout of the selected trajectory
+    (SBP/mpc_planner.py:172-180: compute_cem then the plant step)."""
+    H = 50
+    pg, og, sg, dg = _dual_arm_loop(True, n, H, ticks)
+    _, oe, se, de = _dual_arm_loop(False, n, H, ticks)
+    for a, b in zip(og, oe):
+        _same(a, b)
+    assert pg._graphs is not None and dg == de
+    rels = _check_selected_costs(pg, og, sg, H)
+    print(f"C5 {n} x {H} x 3: selected cost vs oracle per tick {[f'{r:.1e}' for r in rels]}, eef_dist {dg}")
+
+
 def test_dual_arm_closed_loop_c5(torch_cuda):
     """C5 (the dual-arm receding-horizon loop, maxiter_cem = 3 per
     tick, HIP-graph-captured) at a small N: 5 ticks of graph replay equal 5
@@ -191,17 +230,5 @@ def test_dual_arm_closed_loop_c5(torch_cuda):
     for a, b in zip(og, oe):
         _same(a, b)
     assert pg._graphs is not None and dg == de
-    m = pg.model
-    for out, q0 in zip(og, sg):
-        td = np.asarray(out[4], dtype=np.float64).T.reshape(1, 6 * H)
-        a = pu.oracle.rollout(m, td, q0, pu.W, PT, QT, want_theta=False)["cost4"][0, 0]
-        # one candidate: its spread under 8 fp32-sized per-step noise draws
-        # (tests/parity_util.py); the GPU is one more draw, held to twice the
-        # largest of the 8
-        sens = 0.0
-        for sd in range(1, 9):
-            b = pu.oracle.rollout(m, td, q0, pu.W, PT, QT, want_theta=False, noise=1e-6, seed=sd)["cost4"][0, 0]
-            sens = max(sens, abs(a - b) / abs(a))
-        rel = abs(float(out[0][-1]) - a) / abs(a)
-        assert rel < max(pu.TOL, 2 * sens), (rel, sens, float(out[0][-1]), a)
+    _check_selected_costs(pg, og, sg, H)
     print(f"C5 loop eef_dist per tick: {[round(x, 4) for x in dg]}")
