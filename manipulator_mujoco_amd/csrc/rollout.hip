@@ -2543,7 +2543,7 @@ __device__ __forceinline__ mfx16 mfma_rows32(const S& s, const float* gx, int ne
 template <int NVW, int NBW, int NGW, bool WIDE, int WPC = 1>
 __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES / SmemN::CPW) MPCR_ROLLOUT_ATTR rollout_kernel(RolloutArgs args,
                                                                         const DevModel* __restrict__ mptr) {
-  static_assert(WPC == 1 || (WPC == 2 && SmemN::CPW == 1), "two waves per candidate: CPW 1");
+  static_assert(WPC == 1 || (WPC == 2 && (WIDE || SmemN::CPW == 1)), "two waves per candidate: CPW 1");
   using S = typename std::conditional<WIDE, typename std::conditional<WPC == 2, SmemW2, SmemW>::type,
                                       typename std::conditional<WPC == 2, SmemN2, SmemN>::type>::type;
   const int wv = WPC == 2 ? (int)(threadIdx.x >> 6) : 0;
@@ -4227,11 +4227,16 @@ void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigne
 #endif
   if (wide)
     hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), 0, st, a, dm);
-  else if (SmemN::CPW == 1 && (int)grid <= wpc2_max_n())
-    hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);
-  else
+  else {
+    if constexpr (SmemN::CPW == 1) {
+      if ((int)grid <= wpc2_max_n()) {
+        hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);
+        return;
+      }
+    }
     hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false>), dim3((grid + SmemN::CPW - 1) / SmemN::CPW), dim3(WAVE),
                        dyn_lds, st, a, dm);
+  }
 }
 
 hipError_t rollout_occupancy(int* info, size_t dyn_lds) {

@@ -131,3 +131,11 @@ if [[ $STEPS == *mech* ]]; then  # which mechanism moves each well-conditioned G
   run mech_c4 600 python -u tools/diag_f32.py --gpu dual_arm 4096 100 4 ${MECH_K:-40}
   run mech_c3 400 python -u tools/diag_f32.py --gpu scene_mjx 4096 50 3 ${MECH_K:-40}
 fi
+if [[ $STEPS == *ab* ]]; then  # interleaved A/B timing of build_variants/*.so (C3 unless MODEL/N/H say otherwise)
+  for round in 1 2 3; do
+    for so in build_variants/*.so; do
+      run ab_${round}_$(basename $so .so) 120 python tools/ab_time.py "$so"
+    done
+  done
+  grep -h "median" $OUT/ab_*.log | sort > $OUT/ab_summary.txt
+fi
