@@ -121,7 +121,8 @@ def main():
         xi, Pd = batch_xi(n, H, seed, "cuda:0")
         td = np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
         e = Engine(m, H, n, Pd)
-        g = e.trace(xi, MPCR_LAYOUT_XI, pu.Q0, pu.W, pu.PT, pu.QT)["cost4"][:, 0].astype(np.float64)
+        g4 = e.trace(xi, MPCR_LAYOUT_XI, pu.Q0, pu.W, pu.PT, pu.QT)["cost4"].astype(np.float64)
+        g = g4[:, 0]
         plant = Plant(m)
         label = "GPU"
     else:
@@ -139,6 +140,15 @@ def main():
           f"probe F (fp32 oracle) well-misses {int((well & (pf >= pu.TOL)).sum())}; {label} well-misses {len(miss)}, "
           f"worst {rel[well].max():.2e}")
     order = miss[np.argsort(-rel[miss])]
+    # the fp32 oracle's components on the same inputs (is the GPU nearer the
+    # fp32 restatement than the fp64 one?)
+    with oracle.exact(mask):
+        run = oracle.Runner(m, pu.WORKERS, pu.Q0, pu.W, pu.PT, pu.QT, precision="fp32")
+        f4 = run.rollout(td[order]).astype(np.float64) if len(order) else np.zeros((0, 4))
+        run.close()
+    for k, c in enumerate(order[:maxc]):
+        print(f"  cand {c}: (cost, g, r, c) fp64 {np.round(o['cost4'][c], 4)} fp32 oracle {np.round(f4[k], 4)}"
+              + (f" GPU {np.round(g4[c], 4)}" if gpu else ""))
     print(f"{label} well-misses (worst first):", " ".join(f"{i}:{rel[i]:.1e}" for i in order))
     tally = {}
     with oracle.exact(mask):
