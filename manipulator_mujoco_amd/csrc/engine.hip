@@ -20,6 +20,19 @@
 #include "rollout.h"
 
 // extra dynamic LDS per narrow-kernel block (occupancy experiments only)
+// horizon segments of dual-arm rollouts (rollout_launch): steps per segment
+// (0 = one launch) and candidate groups on their own streams
+#ifndef MPCR_SEG_STEPS_DEFAULT
+#define MPCR_SEG_STEPS_DEFAULT 0
+#endif
+#ifndef MPCR_SEG_GROUPS_DEFAULT
+#define MPCR_SEG_GROUPS_DEFAULT 2
+#endif
+#define MPCR_SEG_MAXG 4
+static int env_int_or(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
 #ifndef MPCR_N_DYN_LDS
 #define MPCR_N_DYN_LDS 0
 #endif
@@ -75,6 +88,12 @@ struct mpcr_engine {
   short* d_hints = nullptr;      // max_n x NHINT x 2 (dual-arm class): hull-climb starts
   unsigned* d_pace = nullptr;    // MPCR_PACE_SLOTS: the rollout kernel's per-wave-slot progress (pacing)
   float* d_mslab = nullptr;      // (max_n + 1) x NVW x LD: the dual-arm class's mass matrices
+  // horizon segments of the dual-arm class (rollout_launch): steps per
+  // segment, candidate groups and their streams / fork-join events
+  float* d_seg = nullptr;        // max_n x SEG_STRIDE
+  int seg_steps = 0, seg_groups = 1;
+  hipStream_t seg_stream[MPCR_SEG_MAXG] = {};
+  hipEvent_t seg_event[MPCR_SEG_MAXG + 1] = {};
   // convex hulls (dual-arm class)
   float4* d_hull_vert = nullptr;
   int2* d_hull_info = nullptr;
@@ -922,6 +941,22 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     mpcr_engine_free(e);
     return fail(MPCR_EHIP, "model upload failed");
   }
+  if (e->wide) {
+    // horizon segments (MPCR_SEG_STEPS / MPCR_SEG_GROUPS override the defaults)
+    e->seg_steps = env_int_or("MPCR_SEG_STEPS", MPCR_SEG_STEPS_DEFAULT);
+    e->seg_groups = std::max(1, std::min(MPCR_SEG_MAXG, env_int_or("MPCR_SEG_GROUPS", MPCR_SEG_GROUPS_DEFAULT)));
+    if (e->seg_steps > 0 && e->seg_steps < horizon) {
+      bool ok = hipMalloc(&e->d_seg, sizeof(float) * (size_t)max_n * SEG_STRIDE) == hipSuccess;
+      for (int g = 0; ok && e->seg_groups > 1 && g < e->seg_groups; g++)
+        ok = hipStreamCreateWithFlags(&e->seg_stream[g], hipStreamNonBlocking) == hipSuccess;
+      for (int g = 0; ok && e->seg_groups > 1 && g <= e->seg_groups; g++)
+        ok = hipEventCreateWithFlags(&e->seg_event[g], hipEventDisableTiming) == hipSuccess;
+      if (!ok) {
+        mpcr_engine_free(e);
+        return fail(MPCR_ENOMEM, "horizon-segment state allocation failed");
+      }
+    }
+  }
   *out = e;
   return MPCR_OK;
 }
@@ -943,6 +978,11 @@ extern "C" void mpcr_engine_free(mpcr_engine* e) {
   (void)hipFree(e->d_hints);
   (void)hipFree(e->d_pace);
   (void)hipFree(e->d_mslab);
+  (void)hipFree(e->d_seg);
+  for (int g = 0; g < MPCR_SEG_MAXG; g++)
+    if (e->seg_stream[g]) (void)hipStreamDestroy(e->seg_stream[g]);
+  for (int g = 0; g <= MPCR_SEG_MAXG; g++)
+    if (e->seg_event[g]) (void)hipEventDestroy(e->seg_event[g]);
   (void)hipFree(e->d_face_plane);
   (void)hipFree(e->d_face_vinfo);
   (void)hipFree(e->d_face_vert);
@@ -1008,9 +1048,14 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.H = e->H;
   a.nbasis = e->nbasis;
   a.index_base = l.index_base;
+  a.nctrl = e->host.nctrl;
+  a.nslot = e->host.nslot;
+  a.seg_state = e->d_seg;
+  a.seg = e->d_seg ? e->seg_steps : 0;
   std::memcpy(a.par, l.par, sizeof(a.par));
   if (l.key && l.reset_key) hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, l.key, ~0ull);
-  rollout_launch(e->wide, a, (const DevModel*)e->d_model, l.n, MPCR_N_DYN_LDS, st);
+  rollout_launch(e->wide, a, (const DevModel*)e->d_model, l.n, MPCR_N_DYN_LDS, st, e->seg_groups, e->seg_stream,
+                 e->seg_event);
   HIPCHK(hipGetLastError());
   return MPCR_OK;
 }

@@ -35,6 +35,11 @@ enum { DBG_NCON = 0, DBG_NEFC = 1, DBG_CON = 2, DBG_MAXCON = 48, DBG_ROW = DBG_C
 enum { ST_QPOS = 0, ST_QVEL = DX_NQ, ST_QWS = ST_QVEL + DX_NV, ST_QACC = ST_QWS + DX_NV, ST_EEF = ST_QACC + DX_NV,
        ST_N = ST_EEF + 8 };
 
+// horizon-segment state per candidate (RolloutArgs::seg_state): qpos (DX_NQ),
+// qvel and the warm start (32 each), then 6 registers x 64 lanes (cost_g,
+// cost_r, cost_c, status, rows summed, rows max)
+constexpr int SEG_QPOS = 0, SEG_QVEL = DX_NQ, SEG_QWS = DX_NQ + 32, SEG_REG = DX_NQ + 64, SEG_STRIDE = SEG_REG + 6 * 64;
+
 // pacing table: (XCC 8 x SE 8 x SH 2 x CU 16 x SIMD 4) groups of 16 wave slots
 constexpr unsigned MPCR_PACE_SLOTS = 8u * 8u * 2u * 16u * 4u * 16u;
 
@@ -58,6 +63,14 @@ struct RolloutArgs {
   // MPCR_PACE_SLOTS words; the kernel's pacing reads its SIMD's 16 slots
   unsigned* pace;
   float* mslab;  // (n + 1) x NVW x LD: the mass matrix of the dual-arm class (SmemT::M_SLAB)
+  // horizon segments (dual-arm class, one wave per candidate): this launch
+  // runs steps [t0, t1) of every candidate; a segment that does not start at
+  // 0 resumes from seg_state, one that does not end at H saves to it and
+  // writes no outputs (the engine launches the segments in stream order:
+  // kernel boundaries order them, rollout_launch)
+  float* seg_state;  // n x SEG_STRIDE: qpos | qvel | qws | per-lane registers
+  int t0, t1, seg;   // segment [t0, t1); seg = steps per segment for rollout_launch (0: one launch)
+  int nctrl, nslot;  // the model's (host side: per-candidate strides of grouped launches)
   float* dbg;  // parity debugging (mpcr_plant_step_debug): candidate 0's last step, DBG_* layout
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs
@@ -237,8 +250,13 @@ static_assert(sizeof(SmemW) <= 152448 / 8, "dual-arm LDS image must fit 8 blocks
 // launchers (defined in rollout.hip): the rollout kernel variant for the
 // model class over `grid` blocks of one wave; dyn_lds extra bytes per block
 // (occupancy experiments only)
+// Dual-arm batches of the one-wave variant with a.seg > 0 and H > a.seg run as
+// horizon segments of a.seg steps over `groups` candidate groups, group g on
+// gstream[g] (forked from st by gev[0] and joined back by gev[1 + g]); every
+// group's segments in stream order.  The launches of different groups overlap,
+// so one segment's tail is filled by the other groups' work.
 void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigned grid, size_t dyn_lds,
-                    hipStream_t st);
+                    hipStream_t st, int groups = 0, hipStream_t* gstream = nullptr, hipEvent_t* gev = nullptr);
 // resident blocks per CU, static LDS bytes, VGPRs: narrow (0..2), wide (3..5)
 hipError_t rollout_occupancy(int* info, size_t dyn_lds);
 int rollout_set_wpc2_max_n(int n);  // two waves per candidate up to n (narrow variant); returns the previous

@@ -2559,6 +2559,11 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
   if (S::CPW == 1 && !live) return;
   const int bi = live ? b : args.n - 1;  // an empty group replays a real candidate, writes nothing
   const int H = args.H;
+  // horizon segment of this launch (dual-arm one-wave variant only)
+  constexpr bool SEG = WIDE && WPC == 1 && S::CPW == 1;
+  const int t_begin = SEG ? args.t0 : 0, t_end = SEG ? args.t1 : H;
+  const bool resume = SEG && t_begin > 0, suspend = SEG && t_end < H;
+  float* const segs = SEG ? args.seg_state + (size_t)b * SEG_STRIDE : nullptr;
   const int nv = m->nv, nb = m->nbody, nc = m->nctrl;
   float* const gx = S::JL < S::MAXEFC ? args.jx + (size_t)b * (S::MAXEFC - S::JL) * S::LDJ : nullptr;
   short* const hx = S::WIDE ? args.hints + (size_t)b * S::NHINT * 2 : nullptr;
@@ -2574,11 +2579,19 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
   if constexpr (S::WIDE) {
     // a rollout starts its hull climbs afresh; the plant keeps them across
     // steps (reset by mpcr_plant_set_state), so k plant steps = a k-step rollout
-    if (!from_state) {
+    if (!from_state && !resume) {
       int* h = reinterpret_cast<int*>(args.hints + (size_t)b * S::NHINT * 2);
       for (int i = lane; i < S::NHINT; i += S::HL) h[i] = -1;  // both sides -1
     }
   }
+  if (resume) {  // a later horizon segment: the state the previous one saved
+    for (int i = lane; i < S::NQW; i += S::HL) s.qpos[i] = i < DX_NQ ? segs[SEG_QPOS + i] : 0.f;
+    if (lane < NVW) {
+      s.qvel[lane] = segs[SEG_QVEL + lane];
+      s.qws[lane] = segs[SEG_QWS + lane];
+      s.qacc[lane] = 0.f;
+    }
+  } else {
   for (int i = lane; i < S::NQW; i += S::HL)
     s.qpos[i] = i < m->nq ? (from_state ? args.state[ST_QPOS + i] : m->qpos_init[i]) : 0.f;
   if (lane < NVW) {
@@ -2587,6 +2600,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     s.qws[lane] = v && from_state ? args.state[ST_QWS + lane] : 0.f;
     s.qacc[lane] = 0.f;
   }
+  }
   sync();
   if (lane == 0) {  // normalise the target quaternion once
     const float* q = &s.par[PAR_QT];
@@ -2594,7 +2608,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     s.par[PAR_QT] = q[0] / qn; s.par[PAR_QT + 1] = q[1] / qn; s.par[PAR_QT + 2] = q[2] / qn;
     s.par[PAR_QT + 3] = q[3] / qn;
   }
-  if (lane < nc && !from_state) s.qpos[m->ctrl_qposadr[lane]] = s.par[PAR_Q0 + lane];
+  if (lane < nc && !from_state && !resume) s.qpos[m->ctrl_qposadr[lane]] = s.par[PAR_Q0 + lane];
   sync();
   }
   if constexpr (WPC == 2) block_sync();
@@ -2607,7 +2621,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
   const float* tdp;
   if (args.layout == 0) {
     float* tdw = (args.thetadot && live ? args.thetadot : args.tdscratch) + (size_t)b * nc * H;
-    for (int idx = lane; run_main && idx < nc * H; idx += S::HL) {
+    for (int idx = lane; run_main && !resume && idx < nc * H; idx += S::HL) {
       const int j = idx / H, tt = idx - j * H;
       const float* pd = args.pdot + (size_t)tt * args.nbasis;
       const float* xj = args.input + ((size_t)bi * nc + j) * args.nbasis;
@@ -2624,7 +2638,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
   } else {
     tdp = args.input + (size_t)bi * nc * H;
   }
-  float vnext = lane < nc ? tdp[lane * H] : 0.f;
+  float vnext = lane < nc ? tdp[lane * H + t_begin] : 0.f;
 #else
   // lane j < nctrl keeps joint j's Bernstein coefficients in registers for
   // the whole horizon (nbasis <= 12, checked by the engine)
@@ -2641,6 +2655,11 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
 #pragma unroll
     for (int c = 0; c < 4; c++) shist.v[j][c] = 0.f;
   int status = 0, nefc_sum = 0, nefc_max = 0;
+  if (resume) {  // this lane's accumulators as the previous segment left them
+    const float* rg = segs + SEG_REG + lane;
+    cost_g = rg[0]; cost_r = rg[64]; cost_c = rg[128];
+    status = __float_as_int(rg[192]); nefc_sum = __float_as_int(rg[256]); nefc_max = __float_as_int(rg[320]);
+  }
   // this lane's controlled joint addresses, held across the horizon (read
   // every step; the per-step model launder would otherwise reload them)
   const int ctrl_qa = lane < nc ? m->ctrl_qposadr[lane] : 0, ctrl_da = lane < nc ? m->ctrl_dofadr[lane] : 0;
@@ -2707,7 +2726,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       }
     }
   };
-  for (int t = 0; t < H; t++) {
+  for (int t = t_begin; t < t_end; t++) {
     // Launder the model pointer every step: otherwise the compiler hoists
     // every loop-invariant model load out of the horizon loop and keeps them
     // all live across the whole step (244 VGPRs + SGPR spills).  The loads
@@ -4138,6 +4157,20 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       }
     }
   }
+  if (suspend) {  // not the last segment: save the state and the accumulators, no outputs
+    for (int i = lane; i < DX_NQ; i += S::HL) segs[SEG_QPOS + i] = i < S::NQW ? s.qpos[i] : 0.f;
+    if (lane < NVW) {
+      segs[SEG_QVEL + lane] = s.qvel[lane];
+      segs[SEG_QWS + lane] = s.qws[lane];
+    }
+    float* rg = segs + SEG_REG + lane;
+    rg[0] = cost_g; rg[64] = cost_r; rg[128] = cost_c;
+    rg[192] = __int_as_float(status); rg[256] = __int_as_float(nefc_sum); rg[320] = __int_as_float(nefc_max);
+#if MPCR_PACE
+    if (pace && lane == pace_own) __hip_atomic_store(pace + lane, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+    return;
+  }
   // ---- final reductions, outputs ----------------------------------------------
   cost_c = hsum<S::CPW>(cost_c);
   if constexpr (WPC == 2) {  // the collision wave's cost_c and truncation flag
@@ -4218,16 +4251,71 @@ static const int g_wpc2w_max_n = env_int("MPCR_WPC2W_MAX_N", 1024);
 static int wpc2w_max_n() { return min(g_wpc2w_max_n, wpc2_max_n()); }
 #endif
 
-void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigned grid, size_t dyn_lds,
-                    hipStream_t st) {
+// RolloutArgs of candidates [off, off + n) of a launch: the per-candidate
+// pointers advanced by off (the kernel indexes them by its block)
+static RolloutArgs group_args(const RolloutArgs& a, int off, int n) {
+  RolloutArgs g = a;
+  const size_t o = (size_t)off;
+  g.n = n;
+  g.index_base = a.index_base + off;
+  const size_t in_row = a.layout == 0 ? (size_t)a.nctrl * a.nbasis : (size_t)a.nctrl * a.H;
+  g.input = a.input + o * in_row;
+  g.cost4 = a.cost4 + 4 * o;
+  const size_t th_row = (size_t)a.nctrl * a.H;
+  if (a.theta) g.theta = a.theta + o * th_row;
+  if (a.thetadot) g.thetadot = a.thetadot + o * th_row;
+  if (a.status) g.status = a.status + o;
+  if (a.trace_eef) g.trace_eef = a.trace_eef + o * a.H * 7;
+  if (a.trace_slots) g.trace_slots = a.trace_slots + o * a.H * a.nslot;
+  g.jx = a.jx + o * (SmemW::MAXEFC - SmemW::JL) * SmemW::LDJ;
+  g.hints = a.hints + o * SmemW::NHINT * 2;
+  g.mslab = a.mslab + o * SmemW::NVW * SmemW::LD;
+  g.tdscratch = a.tdscratch + o * th_row;
+  g.slot_prev = a.slot_prev + o * (a.nslot > 0 ? a.nslot : 1);
+  g.seg_state = a.seg_state + o * SEG_STRIDE;
+  return g;
+}
+
+void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsigned grid, size_t dyn_lds,
+                    hipStream_t st, int groups, hipStream_t* gstream, hipEvent_t* gev) {
+  RolloutArgs a = a0;
+  a.t0 = 0;
+  a.t1 = a.H;
 #if MPCR_W_WPC2
   if (wide && (int)grid <= wpc2w_max_n())
     hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);
   else
 #endif
-  if (wide)
-    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), 0, st, a, dm);
-  else {
+  if (wide) {
+    if (a.seg > 0 && a.seg < a.H && a.seg_state && !a.plant && !a.dbg) {
+      // horizon segments over candidate groups on their own streams: each
+      // group's segments in its stream's order, the groups overlapping
+      const int G = groups > 1 && gstream && gev && (int)grid >= 2 * groups ? groups : 1;
+      if (G > 1) {
+        (void)hipEventRecord(gev[0], st);
+        for (int g = 0; g < G; g++) (void)hipStreamWaitEvent(gstream[g], gev[0], 0);
+      }
+      const int per = ((int)grid + G - 1) / G;
+      for (int g = 0; g < G; g++) {
+        const int off = g * per, ng = min(per, (int)grid - off);
+        if (ng <= 0) break;
+        RolloutArgs ga = G > 1 ? group_args(a, off, ng) : a;
+        hipStream_t gs = G > 1 ? gstream[g] : st;
+        for (int t0 = 0; t0 < a.H; t0 += a.seg) {
+          ga.t0 = t0;
+          ga.t1 = min(a.H, t0 + a.seg);
+          hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(ng), dim3(WAVE), 0, gs, ga, dm);
+        }
+      }
+      if (G > 1)
+        for (int g = 0; g < G; g++) {
+          (void)hipEventRecord(gev[1 + g], gstream[g]);
+          (void)hipStreamWaitEvent(st, gev[1 + g], 0);
+        }
+    } else {
+      hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), 0, st, a, dm);
+    }
+  } else {
     if constexpr (SmemN::CPW == 1) {
       if ((int)grid <= wpc2_max_n()) {
         hipLaunchKernelGGL((rollout_kernel<16, 16, 24, false, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);

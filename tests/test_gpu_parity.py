@@ -425,3 +425,32 @@ def test_two_wave_variant_is_bitwise_one_wave(torch_cuda, name, n):
         lib.mpcr_set_two_wave_max_n(prev)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("seg,groups", [(25, 1), (50, 2), (20, 4)])
+def test_dual_arm_horizon_segments_bitwise(torch_cuda, monkeypatch, seg, groups):
+    """Dual-arm rollouts as horizon segments (rollout_launch: each segment
+    resumes from the state the previous one saved, candidate groups on their
+    own streams) are bitwise the one-launch rollouts: costs, theta, thetadot,
+    status and the fused best key."""
+    torch = torch_cuda
+    n, H = 2048 + 37, 100  # ragged: groups of unequal size
+    m = models.load("dual_arm", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
+    out = []
+    for steps, g in ((0, 1), (seg, groups)):
+        monkeypatch.setenv("MPCR_SEG_STEPS", str(steps))
+        monkeypatch.setenv("MPCR_SEG_GROUPS", str(g))
+        e = Engine(m, H, n, Pd)
+        st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+        th = torch.empty((n, 6 * H), device="cuda:0")
+        td = torch.empty((n, 6 * H), device="cuda:0")
+        key = torch.empty(1, dtype=torch.int64, device="cuda:0")
+        c = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, theta=th, thetadot=td, best_key=key, status=st,
+                           index_base=5).clone()
+        torch.cuda.synchronize()
+        out.append((c, th, td, st, key))
+        del e
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)

@@ -139,3 +139,16 @@ if [[ $STEPS == *ab* ]]; then  # interleaved A/B timing of build_variants/*.so (
   done
   grep -h "median" $OUT/ab_*.log | sort > $OUT/ab_summary.txt
 fi
+if [[ $STEPS == *seg* ]]; then  # dual-arm horizon segments x candidate groups (env of the engine), C4 and C5 sizes
+  for round in 1 2; do
+    for sg in "0 1" "50 1" "25 1" "50 2" "25 2" "20 4" "25 4" "10 4"; do
+      set -- $sg
+      MPCR_SEG_STEPS=$1 MPCR_SEG_GROUPS=$2 MODEL=dual_arm N=4096 H=100 R=5 run seg_${round}_c4_$1_$2 200 python tools/ab_time.py manipulator_mujoco_amd/libmpcr.so
+    done
+    for sg in "0 1" "25 2" "25 4" "10 4"; do
+      set -- $sg
+      MPCR_SEG_STEPS=$1 MPCR_SEG_GROUPS=$2 MODEL=dual_arm N=8192 H=50 R=5 run seg_${round}_c5_$1_$2 200 python tools/ab_time.py manipulator_mujoco_amd/libmpcr.so
+    done
+  done
+  for f in $OUT/seg_*.log; do echo "$(basename $f .log) $(grep median $f)"; done > $OUT/seg_summary.txt
+fi
