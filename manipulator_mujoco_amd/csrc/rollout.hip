@@ -2157,8 +2157,18 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
 
 // cost: complete, or (narrow kernel, full == false) without its constant
 // part q0 (the active rows' 0.5 D jar^2 + the Gauss term), which the bracket
-// never reads: the line search adds it once for the final two points
-struct LsPt { float alpha, cost, d0, d1; bool full; };
+// never reads: the line search adds it once for the final two points.
+// T: the precision of a point's step size, cost and derivatives and of the
+// bracket arithmetic -- fp64 in the dual-arm class (LsReal): the point's cost
+// alpha^2 q2 + alpha q1 + q0 cancels a ~1e4 constant to compare candidates
+// that differ in the last fp32 bits, and the bracket's Newton steps
+// alpha - d0 / d1 divide two such differences; in fp32 those decisions
+// halved the dual arm's parity (78 -> 37 well-conditioned
+// misses of the fp32 restatement against fp64).  The row sums stay fp32.
+template <class T>
+struct LsPtT { T alpha, cost, d0, d1; bool full; };
+template <class S>
+using LsReal = typename std::conditional<S::WIDE, double, float>::type;
 
 // elliptic rows: efc_src = (5 << 24) | (contact << 14) | (pair << 4) | side
 __device__ __forceinline__ bool ell_row(int src) { return (src >> 24) == 5; }
@@ -2166,16 +2176,21 @@ __device__ __forceinline__ bool ell_head(int src) { return (src >> 24) == 5 && (
 __device__ __forceinline__ int ell_pair(int src) { return (src >> 4) & 1023; }
 
 
-template <class S>
-__device__ __forceinline__ void ls_rows(const S& s, int lane, float alpha, float& q0, float& q1, float& q2) {
+// the row's side of its kink at the step size alpha (in alpha's precision)
+template <class T>
+__device__ __forceinline__ bool ls_neg(float jar, float jv, T alpha) {
+  return (T)jar + alpha * (T)jv < (T)0;
+}
+
+template <class S, class T>
+__device__ __forceinline__ void ls_rows(const S& s, int lane, T alpha, float& q0, float& q1, float& q2) {
   q0 = q1 = q2 = 0.f;
   for (int r = lane; r < s.nefc; r += S::HL) {
     float jar = s.efc_jar[r], jv = s.efc_jv[r];
-    float x = jar + alpha * jv;
     if constexpr (S::WIDE) {
       if (ell_row(s.efc_src[r])) continue;
     }
-    if (((s.efc_src[r] >> 24) == 1) || x < 0.f) {
+    if (((s.efc_src[r] >> 24) == 1) || ls_neg(jar, jv, alpha)) {
       float D = s.efc_D[r];
       q0 += 0.5f * D * jar * jar;
       q1 += D * jv * jar;
@@ -2184,37 +2199,38 @@ __device__ __forceinline__ void ls_rows(const S& s, int lane, float alpha, float
   }
 }
 
-__device__ __forceinline__ LsPt ls_make(float alpha, float q0, float q1, float q2) {
-  LsPt p;
+template <class T>
+__device__ __forceinline__ LsPtT<T> ls_make(T alpha, T q0, T q1, T q2) {
+  LsPtT<T> p;
   p.alpha = alpha;
   p.cost = alpha * alpha * q2 + alpha * q1 + q0;
-  p.d0 = 2.f * alpha * q2 + q1;
-  p.d1 = 2.f * q2 + (q2 == 0.f ? kMinVal : 0.f);
+  p.d0 = (T)2 * alpha * q2 + q1;
+  p.d1 = (T)2 * q2 + (q2 == (T)0 ? (T)kMinVal : (T)0);
   p.full = true;
   return p;
 }
 
-template <class S, bool Q0 = true>
-__device__ __forceinline__ LsPt ls_eval(const S& s, int lane, const float qg[3], float alpha) {
+template <class S, bool Q0 = true, class T = LsReal<S>>
+__device__ __forceinline__ LsPtT<T> ls_eval(const S& s, int lane, const float qg[3], T alpha) {
   float q0, q1, q2;
   ls_rows(s, lane, alpha, q0, q1, q2);
   q0 = Q0 ? hsum<S::CPW>(q0) + qg[0] : 0.f;
   q1 = hsum<S::CPW>(q1) + qg[1];
   q2 = hsum<S::CPW>(q2) + qg[2];
-  LsPt p = ls_make(alpha, q0, q1, q2);
+  LsPtT<T> p = ls_make<T>(alpha, q0, q1, q2);
   p.full = Q0;
   return p;
 }
 // the deferred constant parts of two line-search points in one row pass
-template <class S>
-__device__ __forceinline__ void ls_finish(const S& s, int lane, const float qg[3], LsPt& a, LsPt& b) {
+template <class S, class T>
+__device__ __forceinline__ void ls_finish(const S& s, int lane, const float qg[3], LsPtT<T>& a, LsPtT<T>& b) {
   float qa = 0.f, qb = 0.f;
   for (int r = lane; r < s.nefc; r += S::HL) {
     const float jar = s.efc_jar[r], jv = s.efc_jv[r];
     const bool eq = (s.efc_src[r] >> 24) == 1;
     const float c0 = 0.5f * s.efc_D[r] * jar * jar;
-    if (eq || jar + a.alpha * jv < 0.f) qa += c0;
-    if (eq || jar + b.alpha * jv < 0.f) qb += c0;
+    if (eq || ls_neg(jar, jv, a.alpha)) qa += c0;
+    if (eq || ls_neg(jar, jv, b.alpha)) qb += c0;
   }
   qa = hsum<S::CPW>(qa) + qg[0];
   qb = hsum<S::CPW>(qb) + qg[0];
@@ -2224,11 +2240,11 @@ __device__ __forceinline__ void ls_finish(const S& s, int lane, const float qg[3
 
 // three line-search points in one pass over the rows; the 9 reductions are
 // independent so their DPP chains interleave
-template <class S, bool Q0 = true>
-__device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3], float a0, float a1, float a2,
-                                         LsPt& p0, LsPt& p1, LsPt& p2) {
+template <class S, bool Q0 = true, class T = LsReal<S>>
+__device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3], T a0, T a1, T a2,
+                                         LsPtT<T>& p0, LsPtT<T>& p1, LsPtT<T>& p2) {
   float q[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const float al[3] = {a0, a1, a2};
+  const T al[3] = {a0, a1, a2};
   for (int r = lane; r < s.nefc; r += S::HL) {
     const float jar = s.efc_jar[r], jv = s.efc_jv[r], D = s.efc_D[r];
     const bool eq = (s.efc_src[r] >> 24) == 1;
@@ -2238,14 +2254,14 @@ __device__ __forceinline__ void ls_eval3(const S& s, int lane, const float qg[3]
     const float c0 = 0.5f * D * jar * jar, c1 = D * jv * jar, c2 = 0.5f * D * jv * jv;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      if (eq || jar + al[k] * jv < 0.f) { q[3 * k] += c0; q[3 * k + 1] += c1; q[3 * k + 2] += c2; }
+      if (eq || ls_neg(jar, jv, al[k])) { q[3 * k] += c0; q[3 * k + 1] += c1; q[3 * k + 2] += c2; }
     }
   }
 #pragma unroll
   for (int k = 0; k < 9; k++) q[k] = (Q0 || k % 3) ? hsum<S::CPW>(q[k]) + qg[k % 3] : 0.f;
-  p0 = ls_make(a0, q[0], q[1], q[2]);
-  p1 = ls_make(a1, q[3], q[4], q[5]);
-  p2 = ls_make(a2, q[6], q[7], q[8]);
+  p0 = ls_make<T>(a0, q[0], q[1], q[2]);
+  p1 = ls_make<T>(a1, q[3], q[4], q[5]);
+  p2 = ls_make<T>(a2, q[6], q[7], q[8]);
   p0.full = p1.full = p2.full = Q0;
 }
 
@@ -2286,9 +2302,11 @@ __device__ __forceinline__ float cone_update(const float x[3], float mu, float f
 }
 
 // cost and its first two derivatives along x + alpha v (zones at alpha)
-__device__ __forceinline__ void cone_line(const float x0[3], const float v[3], float alpha, float mu, float fri,
+template <class A>
+__device__ __forceinline__ void cone_line(const float x0[3], const float v[3], A alpha, float mu, float fri,
                                           const float D[3], float& c0, float& c1, float& c2) {
-  const float x[3] = {x0[0] + alpha * v[0], x0[1] + alpha * v[1], x0[2] + alpha * v[2]};
+  const float x[3] = {(float)((A)x0[0] + alpha * (A)v[0]), (float)((A)x0[1] + alpha * (A)v[1]),
+                      (float)((A)x0[2] + alpha * (A)v[2])};
   const float N = mu * x[0], U0 = fri * x[1], U1 = fri * x[2], W0 = fri * v[1], W1 = fri * v[2];
   const float T = sqrtf(U0 * U0 + U1 * U1);
   if (N >= mu * T || (T <= 0.f && N >= 0.f)) { c0 = c1 = c2 = 0.f; return; }
@@ -2312,8 +2330,8 @@ __device__ __forceinline__ const float* jrow_ptr(const S& s, const float* gx, in
 }
 
 // line-search extra terms of the elliptic contacts at three step sizes
-template <class S>
-__device__ __forceinline__ void ls_cones3(const S& s, const DevModel* __restrict__ m, int lane, const float al[3],
+template <class S, class T>
+__device__ __forceinline__ void ls_cones3(const S& s, const DevModel* __restrict__ m, int lane, const T al[3],
                                           float e[9]) {
 #pragma unroll
   for (int k = 0; k < 9; k++) e[k] = 0.f;
@@ -2335,11 +2353,12 @@ __device__ __forceinline__ void ls_cones3(const S& s, const DevModel* __restrict
   for (int k = 0; k < 9; k++) e[k] = hsum<S::CPW>(e[k]);
 }
 
-__device__ __forceinline__ void ls_add(LsPt& p, float c0, float c1, float c2) {
-  p.cost += c0;
-  p.d0 += c1;
-  p.d1 = p.d1 - (p.d1 == kMinVal ? kMinVal : 0.f) + c2;
-  if (p.d1 == 0.f) p.d1 = kMinVal;
+template <class T>
+__device__ __forceinline__ void ls_add(LsPtT<T>& p, float c0, float c1, float c2) {
+  p.cost += (T)c0;
+  p.d0 += (T)c1;
+  p.d1 = p.d1 - (p.d1 == (T)kMinVal ? (T)kMinVal : (T)0) + (T)c2;
+  if (p.d1 == (T)0) p.d1 = (T)kMinVal;
 }
 
 // Re-derive the model pointer from the kernel argument through an opaque
@@ -3980,10 +3999,12 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           qg[1] = hsum<S::CPW>(lane < nv ? search * (ma - s.qfs[lane]) : 0.f);
           qg[2] = 0.5f * hsum<S::CPW>(search * mvv);
           sync();
-          LsPt p0 = ls_eval(s, lane, qg, 0.f);
+          using LT = LsReal<S>;
+          using LsPt = LsPtT<LT>;
+          LsPt p0 = ls_eval(s, lane, qg, (LT)0);
           const bool ell_ls = S::WIDE && m->cone == 1;
           if (ell_ls) {
-            const float al[3] = {0.f, 0.f, 0.f};
+            const LT al[3] = {0, 0, 0};
             float e[9];
             ls_cones3(s, m, lane, al, e);
             ls_add(p0, e[0], e[1], e[2]);
@@ -3991,7 +4012,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           constexpr bool LSQ0 = S::WIDE;  // narrow: q0 deferred to ls_finish
           LsPt lo = ls_eval<S, LSQ0>(s, lane, qg, p0.alpha - p0.d0 / p0.d1);
           if (ell_ls) {
-            const float al[3] = {lo.alpha, 0.f, 0.f};
+            const LT al[3] = {lo.alpha, 0, 0};
             float e[9];
             ls_cones3(s, m, lane, al, e);
             ls_add(lo, e[0], e[1], e[2]);
@@ -4013,12 +4034,16 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
             // bracket closed to fp32 resolution: further passes only move alpha
             // by rounding noise (gtol sits below fp32 resolution; without this the
             // dual arm ran ~20 passes per Newton iteration against ~2.4 in fp64)
-            if (fabsf(hi.alpha - lo.alpha) <= 1e-6f * fmaxf(fabsf(lo.alpha), fabsf(hi.alpha))) break;
+            {
+              const LT da = hi.alpha - lo.alpha, la = lo.alpha < 0 ? -lo.alpha : lo.alpha,
+                       ha = hi.alpha < 0 ? -hi.alpha : hi.alpha;
+              if ((da < 0 ? -da : da) <= (LT)1e-6f * (la > ha ? la : ha)) break;
+            }
             LsPt lo_next, hi_next, mid;
             ls_eval3<S, LSQ0>(s, lane, qg, lo.alpha - lo.d0 / lo.d1, hi.alpha - hi.d0 / hi.d1,
-                              0.5f * (lo.alpha + hi.alpha), lo_next, hi_next, mid);
+                              (LT)0.5 * (lo.alpha + hi.alpha), lo_next, hi_next, mid);
             if (ell_ls) {
-              const float al[3] = {lo_next.alpha, hi_next.alpha, mid.alpha};
+              const LT al[3] = {lo_next.alpha, hi_next.alpha, mid.alpha};
               float e[9];
               ls_cones3(s, m, lane, al, e);
               ls_add(lo_next, e[0], e[1], e[2]);
@@ -4037,14 +4062,14 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           }
           if constexpr (!LSQ0) ls_finish(s, lane, qg, lo, hi);
           const bool improved = lo.cost < p0.cost || hi.cost < p0.cost;
-          const float alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+          const LT alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
           if (args.dbg && b == 0 && t == H - 1 && lane == 0 && it == 0) {
-            args.dbg[DBG_INFO + 3] = p0.cost;
-            args.dbg[DBG_INFO + 4] = alpha;
-            args.dbg[DBG_INFO + 6] = fminf(lo.cost, hi.cost);
+            args.dbg[DBG_INFO + 3] = (float)p0.cost;
+            args.dbg[DBG_INFO + 4] = (float)alpha;
+            args.dbg[DBG_INFO + 6] = (float)(lo.cost < hi.cost ? lo.cost : hi.cost);
           }
           if (args.dbg && b == 0 && t == H - 1 && lane == 0) args.dbg[DBG_INFO + 7] = (float)(it + 1);
-          if (improved && lane < NVW) s.qacc[lane] = s.qacc[lane] + alpha * s.srch[lane];
+          if (improved && lane < NVW) s.qacc[lane] = (float)((LT)s.qacc[lane] + alpha * (LT)s.srch[lane]);
           prev_cost = cost;
           sync();
           STAMP(9);

@@ -1979,7 +1979,16 @@ static void make_constraint(const mpcr_model_t* m, odata* d) {
 /* ------------------------------------------------------------------------ */
 /* Newton solver (primal), one iteration + exact-quadratic line search       */
 
-typedef struct { double alpha, cost, d0, d1; } lspt;
+/* the line search's step sizes, point costs / derivatives and bracket
+   arithmetic: mpcr_hp stays double in the fp32 build too (oracle_f32.c), as
+   the dual-arm kernel keeps them in fp64 (rollout.hip LsReal: the point cost
+   alpha^2 q2 + alpha q1 + q0 cancels the constant q0 to compare candidates
+   that differ in the last fp32 bits); the row sums stay in the build's
+   precision */
+#ifndef MPCR_HP_DEFINED
+typedef double mpcr_hp;
+#endif
+typedef struct { mpcr_hp alpha, cost, d0, d1; } lspt;
 
 static void mulM(const mpcr_model_t* m, const odata* d, const double* x, double* y) {
   for (int i = 0; i < m->nv; i++) {
@@ -2062,7 +2071,7 @@ static void eval_jar(const mpcr_model_t* m, const odata* d, const double* x, dou
 
 /* cost and its first two alpha-derivatives of the elliptic contact at row r
    along jar + alpha jv (the zones re-evaluated at alpha) */
-static void ell_line(const odata* d, int r, const double* jar, const double* jv, double alpha, double c[3]) {
+static void ell_line(const odata* d, int r, const double* jar, const double* jv, mpcr_hp alpha, double c[3]) {
   double x[3], v[3];
   for (int k = 0; k < 3; k++) { x[k] = jar[r + k] + alpha * jv[r + k]; v[k] = jv[r + k]; }
   double mu = d->efc_mu[r], N = mu * x[0], N1 = mu * v[0], U[2], W[2], T = 0, UW = 0, WW = 0;
@@ -2093,10 +2102,10 @@ static void ell_line(const odata* d, int r, const double* jar, const double* jv,
   c[2] = Dm * (phi1 * phi1 + phi * phi2);
 }
 
-static lspt ls_eval(const odata* d, const double qg[3], const double* jar, const double* jv, double alpha) {
+static lspt ls_eval(const odata* d, const double qg[3], const double* jar, const double* jv, mpcr_hp alpha) {
   double q0 = qg[0], q1 = qg[1], q2 = qg[2], e[3] = {0, 0, 0};
   for (int r = 0; r < d->nefc; r++) {
-    double x = jar[r] + alpha * jv[r];
+    mpcr_hp x = jar[r] + alpha * jv[r];
     if (d->efc_eq[r] == 2) {
       double c[3];
       ell_line(d, r, jar, jv, alpha, c);
@@ -2115,7 +2124,7 @@ static lspt ls_eval(const odata* d, const double qg[3], const double* jar, const
   p.alpha = alpha;
   p.cost = alpha * alpha * q2 + alpha * q1 + q0 + e[0];
   p.d0 = 2 * alpha * q2 + q1 + e[1];
-  p.d1 = 2 * q2 + e[2];
+  p.d1 = 2 * (mpcr_hp)q2 + e[2];
   if (p.d1 == 0) p.d1 = MINVAL;
   return p;
 }
@@ -2245,7 +2254,7 @@ static void solve(const mpcr_model_t* m, odata* d) {
       swap = s1 || s2 || s3 || s4;
     }
     int improved = lo.cost < p0.cost || hi.cost < p0.cost;
-    double alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
+    mpcr_hp alpha = lo.cost < hi.cost ? lo.alpha : hi.alpha;
     if (it == 0) { d->dbg[3] = p0.cost; d->dbg[4] = alpha; d->dbg[6] = fmin(lo.cost, hi.cost); }
     d->dbg[7] = it + 1;
     if (improved) {

@@ -16,6 +16,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+typedef double mpcr_hp; /* the line-search bookkeeping stays fp64 (mpcr_oracle.c lspt) */
+#define MPCR_HP_DEFINED
 #define double float
 #define mpcr_model_t mpcr_model_f32_t
 #include "../include/mpcr_model.h"

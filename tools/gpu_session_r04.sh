@@ -152,3 +152,10 @@ if [[ $STEPS == *seg* ]]; then  # dual-arm horizon segments x candidate groups (
   done
   for f in $OUT/seg_*.log; do echo "$(basename $f .log) $(grep median $f)"; done > $OUT/seg_summary.txt
 fi
+if [[ $STEPS == *bitwise* ]]; then  # the narrow kernel bitwise against the previous build (build_variants/ship.so)
+  for M in scene_mjx ur5e_hande_mjx; do
+    SAVE=$OUT/bw_old_$M.npz MODEL=$M N=4096 R=2 run bw_old_$M 120 python tools/ab_time.py build_variants/ship.so
+    SAVE=$OUT/bw_new_$M.npz MODEL=$M N=4096 R=2 run bw_new_$M 120 python tools/ab_time.py manipulator_mujoco_amd/libmpcr.so
+    run bw_cmp_$M 60 python -c "import numpy as np; a=np.load('$OUT/bw_old_$M.npz', allow_pickle=False); b=np.load('$OUT/bw_new_$M.npz', allow_pickle=False); print('$M bitwise', all(np.array_equal(a[k], b[k]) for k in ('c4','th','st')))"
+  done
+fi
