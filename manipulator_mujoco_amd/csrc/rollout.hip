@@ -1671,7 +1671,10 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
           float gm = -1e30f;
 #pragma unroll
           for (int k = 0; k < 3; k++) gm = fmaxf(gm, fabsf(a[k] + t * dd[k]) - h[k]);
-          if (gm < gbest) { gbest = gm; tbest = t; }
+          // a flat minimum (the segment parallel to a face: every kink as
+          // deep) keeps the first candidate -- a later one must be deeper by
+          // more than 1 um, so fp32 and fp64 pick the same point (the oracle's rule)
+          if (gm < gbest - 1e-6f) { gbest = gm; tbest = t; }
         }
       }
       ts = tbest;

@@ -760,7 +760,10 @@ static void col_capsule_box(const odata* d, int gc, int gb, const double* sc, co
         double e = fabs(a[k] + cand[c] * dd[k]) - h[k];
         if (e > gm) gm = e;
       }
-      if (gm < gbest) { gbest = gm; tbest = cand[c]; }
+      /* a flat minimum (the segment parallel to a face: every kink as deep)
+         keeps the first candidate: a later one must be deeper by more than
+         1 um (otherwise rounding picks a point anywhere along the segment) */
+      if (gm < gbest - 1e-6) { gbest = gm; tbest = cand[c]; }
     }
     ts = tbest;
     for (int k = 0; k < 3; k++) p[k] = a[k] + ts * dd[k];
