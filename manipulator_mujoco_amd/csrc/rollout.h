@@ -95,6 +95,12 @@ struct RolloutArgs {
 #ifndef MPCR_N_NQ
 #define MPCR_N_NQ 20
 #endif
+// polyhedron manifold: a penetration deeper than POLY_DEEP m between hulls of
+// at most POLY_ALLF faces together scans every face for the SAT axis instead
+// of the cone about MPR's normal (the oracle's poly_manifold, same constants)
+constexpr float POLY_DEEP = 5e-3f;
+constexpr int POLY_ALLF = 512;
+
 template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false,
           int JL_ = MAXEFC_, int CPW_ = 1, int MAXACT_ = DX_MAXACT, bool SPLIT_ = false>
 struct __align__(16) SmemT {
@@ -162,6 +168,7 @@ struct __align__(16) SmemT {
         struct {                        // collision:
           int cvx[CVXN];                // the compacted convex-pair list
           alignas(16) float polyw[2][WIDE ? PMAXW : 1][4];  // polyhedron-manifold clip polygon (double buffered)
+          float satsep[WIDE ? POLY_ALLF : 1];  // a deep polyhedron pair's SAT separation of every face
         };
       };
       float efc_D[MAXEFC];
@@ -240,8 +247,8 @@ using SmemW2 = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, 
 static_assert(sizeof(SmemW2) <= 152448 / 4, "two-wave dual-arm image: 4 blocks per CU");
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD + SmemN::NVW, "Hessian + J^T f scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
-static_assert(SmemW::JL * SmemW::LDJ * 4 >= SmemW::CVXN * 4 + 2 * SmemW::PMAXW * 16 + 16,
-              "convex-pair list and clip polygon inside the J rows");
+static_assert(SmemW::JL * SmemW::LDJ * 4 >= SmemW::CVXN * 4 + 2 * SmemW::PMAXW * 16 + 16 + POLY_ALLF * 4,
+              "convex-pair list, clip polygon and SAT separations inside the J rows");
 #if !defined(MPCR_N_LDS_UNCHECKED)
 static_assert(sizeof(SmemW) <= 152448 / 8, "dual-arm LDS image must fit 8 blocks per CU");
 #endif

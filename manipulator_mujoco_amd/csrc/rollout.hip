@@ -1241,7 +1241,55 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
   const int s1 = __shfl(sv, 0), s2 = __shfl(sv, 1);
   PSTAMP(m, 23);
   const int2 i1 = m->vert_finfo[s1], i2 = m->vert_finfo[s2];
-  const int c1 = min(i1.y, WAVE), c2 = min(i2.y, WAVE - c1), ns = c1 + c2;
+  // a deep penetration between small hulls: every face is a candidate (MPR's
+  // normal, which seeds the cone below, is that deep the portal face MPR
+  // ended on -- fp32 and fp64 ended 70 degrees apart on the Hand-E's
+  // interpenetrating finger pads)
+  const int nf1 = m->geom_facenum[g1], nf2 = m->geom_facenum[g2];
+  const bool allf = depth > POLY_DEEP && nf1 + nf2 <= POLY_ALLF;
+  float bsep = 0.f;
+  int fr = -1;
+  bool rtwo = false, found = false;
+  if (allf) {
+    // SAT separation of every face (lane = face, rounds of 64) into LDS,
+    // the wave max, then the lowest face index within the max's tie band
+    const int fa1 = m->geom_faceadr[g1], fa2 = m->geom_faceadr[g2], nf = nf1 + nf2;
+    float mxa = -3e38f;
+#pragma unroll 1
+    for (int b0 = 0; b0 < nf; b0 += WAVE) {
+      const int k = b0 + lane;
+      float sp = -3e38f;
+      if (k < nf) {
+        const bool two = k >= nf1;
+        const int g = two ? g2 : g1, go = two ? g1 : g2, f = two ? fa2 + k - nf1 : fa1 + k;
+        float nw[3], off, pt[3];
+        face_rel(m, s, g, f, c, nw, off);
+        const float mn[3] = {-nw[0], -nw[1], -nw[2]};
+        int h = two ? h0 : h1;
+        support_geom(m, s, go, mn, pt, h, c);
+        sp = nw[0] * pt[0] + nw[1] * pt[1] + nw[2] * pt[2] - off;
+        s.satsep[k] = sp;
+      }
+      mxa = fmaxf(mxa, wmax(sp));
+    }
+    sync();
+    float fmin = 3e38f;
+#pragma unroll 1
+    for (int b0 = 0; b0 < nf; b0 += WAVE) {
+      const int k = b0 + lane;
+      const bool nb = k < nf && near_max(s.satsep[k], mxa);
+      const int f = k >= nf1 ? fa2 + k - nf1 : fa1 + k;
+      fmin = fminf(fmin, -wmax(nb ? -(float)f : -3e38f));
+    }
+    found = fmin < 3e38f;
+    if (found) {
+      fr = (int)fmin;
+      rtwo = !(fr >= fa1 && fr < fa1 + nf1);
+      bsep = s.satsep[rtwo ? nf1 + fr - fa2 : fr - fa1];
+    }
+    sync();  // satsep shares bytes with the clip buffer below
+  }
+  const int c1 = allf ? 0 : min(i1.y, WAVE), c2 = allf ? 0 : min(i2.y, WAVE - c1), ns = c1 + c2;
   // candidate reference faces, at most 64 (one per lane), in the oracle's
   // order: g1's on s1, g2's on s2, then every face whose outward normal lies
   // within the Gauss-map cone of n (g1) / -n (g2), face index order, those
@@ -1257,7 +1305,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
   int nc = ns;
   const int vf1 = lane < c1 ? m->vert_face[i1.x + lane] : -1, vf2 = lane < c2 ? m->vert_face[i2.x + lane] : -1;
 #pragma unroll 1
-  for (int sd = 0; sd < 2; sd++) {
+  for (int sd = 0; sd < 2 && !allf; sd++) {
     const int g = sd ? g2 : g1;
     const int cs = sd ? c2 : c1, vfs = sd ? vf2 : vf1;
     const float sg = sd ? -1.f : 1.f;
@@ -1292,7 +1340,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
   // SAT separation along each candidate's outward normal
   float sep = -3e38f;
   int fid = -1, two = 0;
-  if (lane < nc) {
+  if (!allf && lane < nc) {
     if (lane < ns) {
       two = lane >= c1;
       fid = m->vert_face[two ? i2.x + lane - c1 : i1.x + lane];
@@ -1311,19 +1359,22 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
   }
   // the maximum's tie band: the lowest face index (a flush face pair has the
   // same separation from either side)
-  const float mx = wmax(sep);
-  const bool nb = lane < nc && near_max(sep, mx);
-  const float fmn = -wmax(nb ? -(float)fid : -3e38f);
-  const unsigned long long bm = __ballot(nb && (float)fid == fmn);
-  const int kb = bm ? __builtin_ctzll(bm) : 0;
-  const float bsep = __shfl(sep, kb);
+  if (!allf) {
+    const float mx = wmax(sep);
+    const bool nb = lane < nc && near_max(sep, mx);
+    const float fmn = -wmax(nb ? -(float)fid : -3e38f);
+    const unsigned long long bm = __ballot(nb && (float)fid == fmn);
+    const int kb = bm ? __builtin_ctzll(bm) : 0;
+    found = bm != 0;
+    bsep = __shfl(sep, kb);
+    fr = __shfl(fid, kb);
+    rtwo = __shfl(two, kb) != 0;
+  }
   PSTAMP(m, 25);
-  if (!bm || -bsep > 1.05f * depth + 1e-5f) {  // an edge axis: MPR's single contact
+  if (!found || -bsep > 1.05f * depth + 1e-5f) {  // an edge axis: MPR's single contact
     if (lane == q) nsl = 1;
     return;
   }
-  const int fr = __shfl(fid, kb);
-  const bool rtwo = __shfl(two, kb) != 0;
   const int gr = rtwo ? g2 : g1, gi = rtwo ? g1 : g2;
   float nr[3], offr;
   face_rel(m, s, gr, fr, c, nr, offr);

@@ -1406,6 +1406,13 @@ static void col_plane_mesh(const mpcr_model_t* m, odata* d, int pair, int gp, in
    MJX unpinned (DESIGN.md §Dual-arm class). */
 
 #define POLY_CONE_COS 0.94 /* ~20 degrees: the candidate faces' Gauss-map cone about MPR's normal */
+/* a penetration deeper than POLY_DEEP between hulls of at most POLY_ALLF
+   faces together scans every face (MJX's SAT): MPR's normal that seeds the
+   cone is, that deep, the portal face it ended on -- fp32 and fp64 took
+   portals 70 degrees apart on the Hand-E's interpenetrating finger pads and
+   so different candidate lists (round 4) */
+#define POLY_DEEP 5e-3
+#define POLY_ALLF 512
 
 /* world outward normal and offset (n . (x - c) = off) of face f of geom g,
    relative to the point c (the manifold works relative to g2's centre, as
@@ -1492,12 +1499,19 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
      MJX's SAT scans every face; the cone keeps the axis search independent of
      which of two near-flush face pairs MPR's portal ended on.  SAT separation
      along each outward face normal */
-  const int c1 = m->vert_facenum[s1] < 64 ? m->vert_facenum[s1] : 64;
-  const int c2 = m->vert_facenum[s2] < 64 - c1 ? m->vert_facenum[s2] : 64 - c1;
-  int fid[64], side[64], nc = 0;
+  const int allf = depth > POLY_DEEP && m->geom_facenum[g1] + m->geom_facenum[g2] <= POLY_ALLF;
+  const int c1 = allf ? 0 : (m->vert_facenum[s1] < 64 ? m->vert_facenum[s1] : 64);
+  const int c2 = allf ? 0 : (m->vert_facenum[s2] < 64 - c1 ? m->vert_facenum[s2] : 64 - c1);
+  int fid[POLY_ALLF], side[POLY_ALLF], nc = 0;
   for (int k = 0; k < c1; k++) { fid[nc] = m->vert_face[m->vert_faceadr[s1] + k]; side[nc++] = 0; }
   for (int k = 0; k < c2; k++) { fid[nc] = m->vert_face[m->vert_faceadr[s2] + k]; side[nc++] = 1; }
-  for (int sd = 0; sd < 2; sd++) {
+  if (allf) { /* every face of g1, then of g2 */
+    for (int sd = 0; sd < 2; sd++) {
+      const int g = sd ? g2 : g1, fa = m->geom_faceadr[g];
+      for (int f = fa; f < fa + m->geom_facenum[g]; f++) { fid[nc] = f; side[nc++] = sd; }
+    }
+  }
+  for (int sd = 0; sd < 2 && !allf; sd++) {
     const int g = sd ? g2 : g1, fa = m->geom_faceadr[g], cs = sd ? c2 : c1;
     const int ls = sd ? m->vert_faceadr[s2] : m->vert_faceadr[s1];
     for (int f = fa; f < fa + m->geom_facenum[g] && nc < 64; f++) {
@@ -1512,7 +1526,7 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   g_mpr_stats[9] += nc;
   g_mpr_stats[10] += m->geom_facenum[g1] + m->geom_facenum[g2];
   g_mpr_stats[15] += c1 + c2;
-  double sep[64];
+  double sep[POLY_ALLF];
   double mx = -1e300;
   for (int k = 0; k < nc; k++) {
     const int two = side[k], g = two ? g2 : g1, go = two ? g1 : g2;
