@@ -17,18 +17,21 @@ noise does not model the rounding inside a step (a stiff contact solve
 amplifies it 10-100x beyond the state's own rounding, tools/diag_parity.py),
 so probe F runs the same restatement in fp32 (oracle/oracle_f32.c, scalar
 and sequential: a different decomposition from the kernel's) and counts
-how often fp32 arithmetic alone moves a well-conditioned candidate by 1e-4.
-Then
+how often fp32 arithmetic alone moves a well-conditioned candidate by 1e-4
+-- reported beside the GPU's count, no longer part of the allowance
+(round 4, VERDICT r3: the dual arm's fp32 misses were traced to the line
+search's fp32 bookkeeping and to MPR-seeded SAT candidates of deep pairs,
+both fixed).  Then
 
 * well-conditioned candidates (probe A moves the cost < TOL / 10, no masked
   slot within 1e-5 m of zero): the GPU may miss 1e-4 on no more of them
-  than probe B or probe F does, up to 3 binomial sigma;
+  than probe B does, up to 3 binomial sigma;
 * all candidates: no more misses than probe A has against the oracle, up to
   3 binomial sigma + 1 %;
 * median error at fp32 level;
 * the selection (SBP/mjx_planner.py:395 argmin): the GPU's pick has the
-  oracle's minimum cost to within both candidates' conditioning (probes A,
-  B and F), the GPU's
+  oracle's minimum cost to within both candidates' conditioning (probes A
+  and B), the GPU's
   cost of its pick is within its conditioning of the oracle's, and the
   indices agree unless the oracle's own best two are that close.
 """
@@ -78,7 +81,7 @@ def conditioning(m, td, seed=0):
     # probe F: the same restatement computed in fp32 (oracle_f32.c) -- how far
     # fp32 arithmetic alone moves each candidate.  State noise (probes A, B)
     # misses the rounding inside stiff contact solves
-    run = oracle.Runner(m, WORKERS, Q0, W, PT, QT, precision="fp32")
+    run = oracle.Runner(m, WORKERS, Q0, W, PT, QT, precision="fp32", exact_mask=4)  # the kernel's stop rules
     try:
         o["probe_f4"] = _rel(a, run.rollout(td).astype(np.float64))
     finally:
@@ -115,10 +118,10 @@ def check(m, g_cost, o, sens, label="", strict_well=True):
                  probe_f_well_miss=int((well & (pf >= TOL)).sum()),
                  max_rel_well=float(rel[well].max()) if well.any() else 0.0,
                  max_rel_well_probe_f=float(pf[well].max()) if well.any() else 0.0)
-    bw = max(stats["probe_b_well_miss"], stats["probe_f_well_miss"]) / max(nw, 1)
+    bw = stats["probe_b_well_miss"] / max(nw, 1)
     stats["well_miss_allowed"] = float((bw + _sigma3(bw, nw)) * max(nw, 1))
     ig, io = int(np.argmin(g)), int(np.argmin(oc))
-    ug, uo = max(TOL, sens[ig], pb[ig], pf[ig]), max(TOL, sens[io], pb[io], pf[io])
+    ug, uo = max(TOL, sens[ig], pb[ig]), max(TOL, sens[io], pb[io])
     stats.update(sel_gpu=ig, sel_oracle=io, sel_rel=float(rel[ig]), sel_gap=float((oc[ig] - oc[io]) / abs(oc[io])),
                  sel_cond=float(ug), sel_probe_f=float(pf[ig]))
     _log(label, stats)
@@ -197,7 +200,7 @@ def check_components(m, g_cost4, o, label="", g_slots=None, strict=True):
                   probe_b_well_miss=int((well & (pb >= TOL)).sum()), probe_f_well_miss=int((well & (pf >= TOL)).sum()),
                   max_rel_well=float(rel[well].max()) if well.any() else 0.0,
                   max_rel_well_probe_f=float(pf[well].max()) if well.any() else 0.0)
-        bw = max(st["probe_b_well_miss"], st["probe_f_well_miss"]) / max(nw, 1)
+        bw = st["probe_b_well_miss"] / max(nw, 1)
         st["well_miss_allowed"] = float((bw + _sigma3(bw, nw)) * max(nw, 1))
         out[name] = st
     bad = np.zeros(0, int)
