@@ -23,7 +23,7 @@
 // horizon segments of dual-arm rollouts (rollout_launch): steps per segment
 // (0 = one launch) and candidate groups on their own streams
 #ifndef MPCR_SEG_STEPS_DEFAULT
-#define MPCR_SEG_STEPS_DEFAULT 0
+#define MPCR_SEG_STEPS_DEFAULT 25
 #endif
 #ifndef MPCR_SEG_GROUPS_DEFAULT
 #define MPCR_SEG_GROUPS_DEFAULT 2
@@ -91,7 +91,7 @@ struct mpcr_engine {
   // horizon segments of the dual-arm class (rollout_launch): steps per
   // segment, candidate groups and their streams / fork-join events
   float* d_seg = nullptr;        // max_n x SEG_STRIDE
-  int seg_steps = 0, seg_groups = 1;
+  int seg_steps = 0, seg_groups = 1, seg_min_n = 0;
   hipStream_t seg_stream[MPCR_SEG_MAXG] = {};
   hipEvent_t seg_event[MPCR_SEG_MAXG + 1] = {};
   // convex hulls (dual-arm class)
@@ -946,6 +946,12 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     e->seg_steps = env_int_or("MPCR_SEG_STEPS", MPCR_SEG_STEPS_DEFAULT);
     e->seg_groups = std::max(1, std::min(MPCR_SEG_MAXG, env_int_or("MPCR_SEG_GROUPS", MPCR_SEG_GROUPS_DEFAULT)));
     if (e->seg_steps > 0 && e->seg_steps < horizon) {
+      // a batch the device holds in one round gains nothing: its blocks all
+      // start together (the one-wave variant's resident blocks per CU x CUs)
+      int occ[6] = {0, 0, 0, 0, 0, 0}, ncu = 0;
+      if (rollout_occupancy(occ, MPCR_N_DYN_LDS) == hipSuccess &&
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
+        e->seg_min_n = occ[3] * ncu;
       bool ok = hipMalloc(&e->d_seg, sizeof(float) * (size_t)max_n * SEG_STRIDE) == hipSuccess;
       for (int g = 0; ok && e->seg_groups > 1 && g < e->seg_groups; g++)
         ok = hipStreamCreateWithFlags(&e->seg_stream[g], hipStreamNonBlocking) == hipSuccess;
@@ -1052,6 +1058,7 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
   a.nslot = e->host.nslot;
   a.seg_state = e->d_seg;
   a.seg = e->d_seg ? e->seg_steps : 0;
+  a.seg_min_n = e->seg_min_n;
   std::memcpy(a.par, l.par, sizeof(a.par));
   if (l.key && l.reset_key) hipLaunchKernelGGL(fill_u64, dim3(1), dim3(1), 0, st, l.key, ~0ull);
   rollout_launch(e->wide, a, (const DevModel*)e->d_model, l.n, MPCR_N_DYN_LDS, st, e->seg_groups, e->seg_stream,

@@ -71,6 +71,7 @@ struct RolloutArgs {
   float* seg_state;  // n x SEG_STRIDE: qpos | qvel | qws | per-lane registers
   int t0, t1, seg;   // segment [t0, t1); seg = steps per segment for rollout_launch (0: one launch)
   int nctrl, nslot;  // the model's (host side: per-candidate strides of grouped launches)
+  int seg_min_n;     // segments only for batches above this (the one-wave variant's resident blocks)
   float* dbg;  // parity debugging (mpcr_plant_step_debug): candidate 0's last step, DBG_* layout
   // per-call parameters: by value (par) or, for graph-captured ticks, read
   // from device memory (dpar, same layout) when the launch runs
@@ -98,8 +99,12 @@ struct RolloutArgs {
 // polyhedron manifold: a penetration deeper than POLY_DEEP m between hulls of
 // at most POLY_ALLF faces together scans every face for the SAT axis instead
 // of the cone about MPR's normal (the oracle's poly_manifold, same constants)
+#ifndef MPCR_POLY_ALLF
+#define MPCR_POLY_ALLF 512  // 0: the cone always (timing experiments only)
+#endif
 constexpr float POLY_DEEP = 5e-3f;
-constexpr int POLY_ALLF = 512;
+constexpr int POLY_ALLF = MPCR_POLY_ALLF > 0 ? MPCR_POLY_ALLF : 1;
+constexpr bool POLY_ALLF_ON = MPCR_POLY_ALLF > 0;
 
 template <int NVW_, int NBW_, int NGW_, int MAXEFC_ = DX_MAXEFC, int LDJ_ = NVW_ + 4, bool CPREV_GLOBAL_ = false,
           int JL_ = MAXEFC_, int CPW_ = 1, int MAXACT_ = DX_MAXACT, bool SPLIT_ = false>

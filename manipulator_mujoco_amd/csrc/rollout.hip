@@ -1246,7 +1246,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
   // ended on -- fp32 and fp64 ended 70 degrees apart on the Hand-E's
   // interpenetrating finger pads)
   const int nf1 = m->geom_facenum[g1], nf2 = m->geom_facenum[g2];
-  const bool allf = depth > POLY_DEEP && nf1 + nf2 <= POLY_ALLF;
+  const bool allf = POLY_ALLF_ON && depth > POLY_DEEP && nf1 + nf2 <= POLY_ALLF;
   float bsep = 0.f;
   int fr = -1;
   bool rtwo = false, found = false;
@@ -2221,8 +2221,11 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
 // misses of the fp32 restatement against fp64).  The row sums stay fp32.
 template <class T>
 struct LsPtT { T alpha, cost, d0, d1; bool full; };
+#ifndef MPCR_W_LS64
+#define MPCR_W_LS64 1  // 0: the dual-arm line search in fp32 (timing experiments only)
+#endif
 template <class S>
-using LsReal = typename std::conditional<S::WIDE, double, float>::type;
+using LsReal = typename std::conditional<S::WIDE && MPCR_W_LS64, double, float>::type;
 
 // elliptic rows: efc_src = (5 << 24) | (contact << 14) | (pair << 4) | side
 __device__ __forceinline__ bool ell_row(int src) { return (src >> 24) == 5; }
@@ -4366,7 +4369,7 @@ void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsign
   else
 #endif
   if (wide) {
-    if (a.seg > 0 && a.seg < a.H && a.seg_state && !a.plant && !a.dbg) {
+    if (a.seg > 0 && a.seg < a.H && a.seg_state && !a.plant && !a.dbg && (int)grid > a.seg_min_n) {
       // horizon segments over candidate groups on their own streams: each
       // group's segments in its stream's order, the groups overlapping
       const int G = groups > 1 && gstream && gev && (int)grid >= 2 * groups ? groups : 1;

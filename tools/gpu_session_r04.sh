@@ -159,3 +159,12 @@ if [[ $STEPS == *bitwise* ]]; then  # the narrow kernel bitwise against the prev
     run bw_cmp_$M 60 python -c "import numpy as np; a=np.load('$OUT/bw_old_$M.npz', allow_pickle=False); b=np.load('$OUT/bw_new_$M.npz', allow_pickle=False); print('$M bitwise', all(np.array_equal(a[k], b[k]) for k in ('c4','th','st')))"
   done
 fi
+if [[ $STEPS == *abc4* ]]; then  # dual-arm A/B of build_variants/*.so, one launch (no segments) and the default segments
+  for round in 1 2; do
+    for so in build_variants/*.so; do
+      MPCR_SEG_STEPS=0 MODEL=dual_arm N=4096 H=100 R=3 run abc4_${round}_$(basename $so .so)_noseg 200 python tools/ab_time.py "$so"
+    done
+  done
+  grep -h "median" $OUT/abc4_*.log | sort > $OUT/abc4_summary.txt
+  for f in $OUT/abc4_*.log; do echo "$(basename $f .log) $(grep median $f | sed 's/.*median/median/')"; done > $OUT/abc4_summary.txt
+fi
