@@ -119,6 +119,9 @@ def main():
     if gpu:
         from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine, Plant
         xi, Pd = batch_xi(n, H, seed, "cuda:0")
+        # the GPU-projected batch, for CPU experiments on the very same inputs (--xi)
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        np.save(os.path.join(ROOT, "gpurun_out", f"xi_{name}_{n}x{H}_s{seed}.npy"), xi)
         td = np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
         e = Engine(m, H, n, Pd)
         g4 = e.trace(xi, MPCR_LAYOUT_XI, pu.Q0, pu.W, pu.PT, pu.QT)["cost4"].astype(np.float64)
@@ -126,7 +129,13 @@ def main():
         plant = Plant(m)
         label = "GPU"
     else:
-        td = batch(m, n, H, seed)
+        xs = [x for x in sys.argv if x.startswith("--xi=")]
+        if xs:  # a batch saved by a --gpu run (the GPU-projected inputs)
+            xi = np.load(xs[0][5:])
+            _, _, Pd, _ = basis.planner_basis(H, 0.05)
+            td = np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
+        else:
+            td = batch(m, n, H, seed)
         label = "fp32 oracle"
     t0 = time.time()
     with oracle.exact(mask):
