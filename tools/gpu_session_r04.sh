@@ -168,3 +168,6 @@ if [[ $STEPS == *abc4* ]]; then  # dual-arm A/B of build_variants/*.so, one laun
   grep -h "median" $OUT/abc4_*.log | sort > $OUT/abc4_summary.txt
   for f in $OUT/abc4_*.log; do echo "$(basename $f .log) $(grep median $f | sed 's/.*median/median/')"; done > $OUT/abc4_summary.txt
 fi
+if [[ $STEPS == *steperr* ]]; then  # per-step error budget of the GPU's accumulated-drift misses (tools/step_errors.py)
+  run steperr_c4 400 python -u tools/step_errors.py dual_arm 4096 100 4 ${STEPERR_CANDS:-928 3593 3162 2818 3136 2429 3470 628 2863 93 2112}
+fi
