@@ -1,6 +1,6 @@
 """Per-step error budget of the kernel against the fp32 restatement (GPU
-diagnostic).  For the listed candidates of a batch saved by
-`tools/diag_f32.py --gpu` (gpurun_out/xi_<model>_<n>x<H>_s<seed>.npy), every
+diagnostic).  For the listed candidates of the GPU-projected batch of
+`tools/diag_f32.py --gpu` (the parity tests' inputs), every
 step is evaluated from the fp64 oracle's state three ways -- fp64 oracle,
 fp32 oracle (oracle_f32.c), the GPU plant -- and the relative errors of
 qacc_smooth (dynamics only), the constraint rows (D, aref) and qacc (after
@@ -33,8 +33,8 @@ def main():
     name, n, H, seed = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     cands = [int(x) for x in sys.argv[5:]]
     m = models.load(name, 0.05)
-    xi = np.load(os.path.join(ROOT, "gpurun_out", f"xi_{name}_{n}x{H}_s{seed}.npy"))
-    _, _, Pd, _ = basis.planner_basis(H, 0.05)
+    from diag_f32 import batch_xi
+    xi, Pd = batch_xi(n, H, seed, "cuda:0")  # the GPU-projected batch (as diag_f32 --gpu and the parity tests)
     td = np.einsum("tk,njk->njt", Pd, xi.reshape(n, 6, 11).astype(np.float64)).reshape(n, 6 * H)
     plant = Plant(m)
     with oracle.exact(4):
