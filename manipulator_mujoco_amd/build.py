@@ -63,14 +63,39 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def compile_lib(out: str, extra=(), verbose: bool = False) -> str:
-    """Compile every unit (FLAGS + its own + extra) and link the shared library."""
+# the fast-math device flags above, dropped by compile_lib(precise=True) for
+# accuracy experiments (tools/build_variant.py --precise)
+FAST_MATH = {"-freciprocal-math", "-fapprox-func", "-fassociative-math", "-fno-signed-zeros", "-fno-trapping-math"}
+
+
+def _drop_fast(flags):
+    out, skip = [], False
+    for i, f in enumerate(flags):
+        if skip:
+            skip = False
+            continue
+        if f == "-Xarch_device" and i + 1 < len(flags) and flags[i + 1] in FAST_MATH:
+            skip = True
+            continue
+        if f == "-fno-hip-fp32-correctly-rounded-divide-sqrt":
+            continue
+        out.append(f)
+    return out
+
+
+def compile_lib(out: str, extra=(), verbose: bool = False, precise: bool = False) -> str:
+    """Compile every unit (FLAGS + its own + extra) and link the shared library.
+    precise: without the fast-math device flags (IEEE division / sqrt, no
+    reassociation) -- accuracy experiments only."""
     import tempfile
     with tempfile.TemporaryDirectory() as tmp:
         objs = []
         for src, unit_flags in UNITS:
             obj = os.path.join(tmp, os.path.basename(src) + ".o")
-            cmd = [hipcc(), f"--offload-arch={ARCH}", "-c"] + FLAGS + list(unit_flags) + list(extra) + ["-o", obj, src]
+            fl = FLAGS + list(unit_flags)
+            if precise:
+                fl = _drop_fast(fl)
+            cmd = [hipcc(), f"--offload-arch={ARCH}", "-c"] + fl + list(extra) + ["-o", obj, src]
             if verbose:
                 cmd.append("-Rpass-analysis=kernel-resource-usage")
                 print(" ".join(cmd))

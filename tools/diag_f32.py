@@ -117,6 +117,9 @@ def main():
     mask = int(os.environ.get("ORACLE_MASK", 4))
     m = models.load(name, 0.05)
     if gpu:
+        if os.environ.get("MPCR_LIB"):  # a build variant (tools/build_variant.py)
+            from manipulator_mujoco_amd import _lib
+            _lib.LIB_PATH = os.path.abspath(os.environ["MPCR_LIB"])
         from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine, Plant
         xi, Pd = batch_xi(n, H, seed, "cuda:0")
         # the GPU-projected batch, for CPU experiments on the very same inputs (--xi)

@@ -171,3 +171,9 @@ fi
 if [[ $STEPS == *steperr* ]]; then  # per-step error budget of the GPU's accumulated-drift misses (tools/step_errors.py)
   run steperr_c4 400 python -u tools/step_errors.py dual_arm 4096 100 4 ${STEPERR_CANDS:-928 3593 3162 2818 3136 2429 3470 628 2863 93 2112}
 fi
+if [[ $STEPS == *mechvar* ]]; then  # GPU well-conditioned misses of each build_variants/*.so on the C4 batch
+  for so in build_variants/*.so; do
+    MPCR_LIB=$so run mechvar_$(basename $so .so) 400 python -u tools/diag_f32.py --gpu dual_arm 4096 100 4 ${MECH_K:-0}
+  done
+  grep -H "GPU well-misses" $OUT/mechvar_*.log | grep -v "worst first" > $OUT/mechvar_summary.txt
+fi
