@@ -2292,19 +2292,48 @@ static void solve(const mpcr_model_t* m, odata* d) {
 /* ------------------------------------------------------------------------ */
 /* step = forward + Euler (mj_step with eulerdamp disabled)                   */
 
+/* diagnostic (oracle_set_round32, tools/stage_precision.py): round the
+   outputs of the masked stages to fp32 -- which stage's fp32 precision moves
+   the trajectories (bits: 1 kinematics, 2 COM / cinert / cdof, 4 mass matrix,
+   8 contacts, 16 velocities, 32 passive + bias + actuator forces, 64
+   constraint rows, 128 qacc_smooth, 256 qacc, 512 Euler state) */
+static int g_round32 = 0;
+void oracle_set_round32(int mask) { g_round32 = mask; }
+static void r32v(double* x, int n) {
+  for (int i = 0; i < n; i++) x[i] = (double)(float)x[i];
+}
+#define R32(bit, arr, n) do { if (g_round32 & (bit)) r32v((double*)(arr), (n)); } while (0)
+
 static void forward(const mpcr_model_t* m, odata* d) {
   kinematics(m, d);
+  R32(1, d->xpos, 3 * m->nbody); R32(1, d->xquat, 4 * m->nbody); R32(1, d->xmat, 9 * m->nbody);
+  R32(1, d->xipos, 3 * m->nbody); R32(1, d->ximat, 9 * m->nbody); R32(1, d->xanchor, 3 * m->njnt);
+  R32(1, d->xaxis, 3 * m->njnt); R32(1, d->geom_xpos, 3 * m->ngeom); R32(1, d->geom_xmat, 9 * m->ngeom);
+  R32(1, d->site_xpos, 3 * m->nsite);
   com_pos(m, d);
+  R32(2, d->subtree_com, 3 * m->nbody); R32(2, d->cinert, 10 * m->nbody); R32(2, d->cdof, 6 * m->nv);
   crb(m, d);
+  if (g_round32 & 4) {
+    for (int i = 0; i < m->nv; i++) r32v(d->M[i], m->nv);
+    chol(d->L, d->M, m->nv);
+  }
   collision(m, d);
+  if (g_round32 & 8)
+    for (int c = 0; c < d->ncon; c++) { r32v(&d->con[c].dist, 1); r32v(d->con[c].pos, 3); r32v(d->con[c].frame, 9); }
   com_vel(m, d);
+  R32(16, d->cvel, 6 * m->nbody); R32(16, d->cdof_dot, 6 * m->nv);
   passive(m, d);
   rne(m, d);
   actuation(m, d);
+  R32(32, d->qfrc_passive, m->nv); R32(32, d->qfrc_bias, m->nv); R32(32, d->qfrc_actuator, m->nv);
   make_constraint(m, d);
+  if (g_round32 & 64)
+    for (int r = 0; r < d->nefc; r++) { r32v(d->efc_J[r], m->nv); r32v(&d->efc_D[r], 1); r32v(&d->efc_aref[r], 1); }
   for (int i = 0; i < m->nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
   chol_solve(d->qacc_smooth, d->L, d->qfrc_smooth, m->nv);
+  R32(128, d->qacc_smooth, m->nv);
   solve(m, d);
+  R32(256, d->qacc, m->nv);
 }
 
 static void euler(const mpcr_model_t* m, odata* d) {
@@ -2345,6 +2374,7 @@ static void euler(const mpcr_model_t* m, odata* d) {
     }
   }
   memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * m->nv);
+  R32(512, d->qpos, m->nq); R32(512, d->qvel, m->nv); R32(512, d->qacc_warmstart, m->nv);
 }
 
 /* ------------------------------------------------------------------------ */
