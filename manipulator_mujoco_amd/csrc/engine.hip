@@ -553,6 +553,24 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
       if (cross(tree_of_body(m.site_bodyid[m.ten_site[t][0]]), tree_of_body(m.site_bodyid[m.ten_site[t][1]])))
         d.eq_cross = 1;
   }
+  {  // compact mass matrix (dual-arm image, SmemT::Mc): each tree's dofs contiguous
+    int ts[DX_NTREE], te[DX_NTREE];
+    bool ok = true;
+    for (int t = 0; t < DX_NTREE; t++) ts[t] = te[t] = -1;
+    for (int i = 0; i < m.nv && ok; i++) {
+      const int b = d.dof_body[i], t = b >= 0 ? d.body_tree[b] : -1;
+      if (t < 0 || t >= DX_NTREE) { ok = false; break; }
+      if (ts[t] < 0) ts[t] = i;
+      else if (te[t] != i) ok = false;  // a tree's dofs interleaved with another's
+      te[t] = i + 1;
+    }
+    for (int i = 0; i < m.nv && ok; i++) {
+      const int t = d.body_tree[d.dof_body[i]];
+      d.mc_c0[i] = std::min(ts[t] & ~3, SmemW::NVW - SmemW::MCW);  // the window stays inside the NVW columns
+      if (te[t] - d.mc_c0[i] > SmemW::MCW) ok = false;
+    }
+    d.mc_n = ok && m.nv * SmemW::MCW <= SmemW::MC ? m.nv : 0;
+  }
   for (int i = 0; i < m.nq; i++) d.qpos_init[i] = (float)m.qpos_init[i];
   for (int i = 0; i < m.nv; i++) d.qvel_init[i] = (float)m.qvel_init[i];
   // collision geoms referenced by pairs

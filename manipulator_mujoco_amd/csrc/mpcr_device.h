@@ -103,6 +103,12 @@ struct DevModel {
   int eq_cross;                  // an equality / tendon row couples two trees (Newton stays dense)
   int impl_cross;                // implicitfast's D couples two trees (its solve stays dense)
   int blane_dof[64];             // lane 16 tree + k -> dof (-1: pad)
+  // compact mass matrix (dual-arm class, in LDS): row i keeps the 16 columns
+  // from mc_c0[i] (a multiple of 4) on, which cover its tree's dofs; mc_n:
+  // rows kept (0: M in the per-candidate HBM slab instead -- a tree's dofs
+  // not contiguous or wider than that window, or more rows than the image has)
+  int mc_n;
+  int mc_c0[DX_NV];
   float dof_armature[DX_NV], dof_damping[DX_NV], dof_invweight0[DX_NV];
 
   float qpos_init[DX_NQ];

@@ -102,6 +102,10 @@ struct RolloutArgs {
 #ifndef MPCR_POLY_ALLF
 #define MPCR_POLY_ALLF 512  // 0: the cone always (timing experiments only)
 #endif
+// compact mass-matrix rows in the dual-arm image (SmemT::Mc; the dual arm has 22 dofs)
+#ifndef MPCR_W_MC_ROWS
+#define MPCR_W_MC_ROWS 24
+#endif
 constexpr float POLY_DEEP = 5e-3f;
 constexpr int POLY_ALLF = MPCR_POLY_ALLF > 0 ? MPCR_POLY_ALLF : 1;
 constexpr bool POLY_ALLF_ON = MPCR_POLY_ALLF > 0;
@@ -139,10 +143,17 @@ struct __align__(16) SmemT {
   alignas(16) float srch[NVW];  // Newton search direction
   float com[DX_NTREE][4];
   float cdof[NVW][WIDE ? 6 : 8];
-  // the dual-arm class keeps M in a per-candidate HBM slab (RolloutArgs::mslab,
-  // L2-resident): 4.6 KB less LDS -> 8 blocks per CU instead of 7
+  // the dual-arm class keeps M compact in LDS (Mc: row i is the MCW = 16
+  // columns from DevModel::mc_c0[i] on, which hold its tree's; 1.4 KB for the
+  // dual arm's 22 dofs where the dense image was 4.6 KB), or -- a model whose
+  // trees do not fit that, DevModel::mc_n == 0 -- in a per-candidate HBM slab
+  // (RolloutArgs::mslab)
   static constexpr bool M_SLAB = NVW_ == 32;
-  alignas(16) float M[M_SLAB ? 1 : NVW][LD];
+  static constexpr int MCW = 16, MC = M_SLAB ? MPCR_W_MC_ROWS * MCW : 4;
+  union {
+    alignas(16) float M[M_SLAB ? 1 : NVW][M_SLAB ? 4 : LD];  // the dense image (single-arm variants)
+    alignas(16) float Mc[MC];
+  };
   alignas(16) float gxpos[NGW][4];   // gxpos+gxmat (dead during Newton) double as the
   float gxmat[NGW][12];  // Hessian solve's LDS scratch (NGW*16 >= NVW*LD)
   float cprev[CPREV_GLOBAL ? 1 : DX_NSLOT];  // previous-step masked slot distances (cost_c)
@@ -255,7 +266,9 @@ static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 static_assert(SmemW::JL * SmemW::LDJ * 4 >= SmemW::CVXN * 4 + 2 * SmemW::PMAXW * 16 + 16 + POLY_ALLF * 4,
               "convex-pair list, clip polygon and SAT separations inside the J rows");
 #if !defined(MPCR_N_LDS_UNCHECKED)
-static_assert(sizeof(SmemW) <= 152448 / 8, "dual-arm LDS image must fit 8 blocks per CU");
+// measured on MI355X (C4 shard, extra dynamic LDS per block): 8 blocks per CU
+// up to 18912 + 1536 B, 7 at 18912 + 2048 B
+static_assert(sizeof(SmemW) <= 20448, "dual-arm LDS image must fit 8 blocks per CU");
 #endif
 
 

@@ -2643,9 +2643,69 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
   const int nv = m->nv, nb = m->nbody, nc = m->nctrl;
   float* const gx = S::JL < S::MAXEFC ? args.jx + (size_t)b * (S::MAXEFC - S::JL) * S::LDJ : nullptr;
   short* const hx = S::WIDE ? args.hints + (size_t)b * S::NHINT * 2 : nullptr;
-  // mass-matrix rows: LDS, or the candidate's HBM slab (dual-arm class)
+  // mass matrix: the dense LDS image (single-arm variants), the compact LDS
+  // rows of the dual-arm class (DevModel::mc_row: row i holds its tree's
+  // columns; the others are 0 and rows past nv the identity), or -- a
+  // dual-arm-class model whose compact M does not fit -- the candidate's HBM slab
   float* const mrow0 = S::M_SLAB ? args.mslab + (size_t)b * NVW * S::LD : nullptr;
-#define MR(i) (S::M_SLAB ? mrow0 + (i) * S::LD : s.M[S::M_SLAB ? 0 : (i)])
+  const bool mcomp = S::M_SLAB && m->mc_n > 0;
+  constexpr int MCW = S::MCW;
+  auto m_get = [&](int i, int j) -> float {
+    if constexpr (S::M_SLAB) {
+      if (mcomp) {
+        if (i >= nv) return i == j ? 1.f : 0.f;
+        const unsigned c = (unsigned)(j - m->mc_c0[i]);
+        return c < (unsigned)MCW ? s.Mc[i * MCW + c] : 0.f;
+      }
+      return mrow0[i * S::LD + j];
+    } else {
+      return s.M[i][j];
+    }
+  };
+  auto m_set = [&](int i, int j, float v) {
+    if constexpr (S::M_SLAB) {
+      if (mcomp) {
+        const unsigned c = (unsigned)(j - m->mc_c0[i]);
+        if (i < nv && c < (unsigned)MCW) s.Mc[i * MCW + c] = v;
+        return;
+      }
+      mrow0[i * S::LD + j] = v;
+    } else {
+      s.M[i][j] = v;
+    }
+  };
+  // the window start of this lane's row (lane mod NVW), read once: the row
+  // accessors below run in the Newton loop, where a dependent model load in
+  // front of every LDS read cost more than the HBM slab's L2 reads had
+  const int mc0_lane = S::M_SLAB ? m->mc_c0[lane & (NVW - 1)] : 0;
+  // columns 4q .. 4q + 3 of row i = this lane's row (lane mod NVW)
+  auto m_quad = [&](int i, int q) -> float4 {
+    if constexpr (S::M_SLAB) {
+      if (mcomp) {
+        if (i >= nv) {
+          const int k = i - 4 * q;
+          return make_float4(k == 0 ? 1.f : 0.f, k == 1 ? 1.f : 0.f, k == 2 ? 1.f : 0.f, k == 3 ? 1.f : 0.f);
+        }
+        const unsigned c = (unsigned)(4 * q - mc0_lane);
+        const float4 v = *reinterpret_cast<const float4*>(&s.Mc[i * MCW + (c & (MCW - 4))]);
+        return c < (unsigned)MCW ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      return reinterpret_cast<const float4*>(mrow0 + i * S::LD)[q];
+    } else {
+      return reinterpret_cast<const float4*>(s.M[i])[q];
+    }
+  };
+  // (M vec)[i], i = this lane's row, < nv: dotN's fmaf chain; a compact row
+  // leaves out columns that are 0 (other trees') before and after its window,
+  // which leaves the sum bitwise unchanged
+  auto m_dot = [&](int i, const float* vec) -> float {
+    if constexpr (S::M_SLAB) {
+      if (mcomp) return dotN<MCW>(&s.Mc[i * MCW], vec + mc0_lane);
+      return dotN<NVW>(mrow0 + i * S::LD, vec);
+    } else {
+      return dotN<NVW>(s.M[i], vec);
+    }
+  };
 
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
   //      (plant mode: the caller's state, no init_pos override)
@@ -3263,13 +3323,13 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
         if (i < nv && j < nv) {
           if ((m->dof_chainmask[i] >> j) & 1u) {
             const float x = i == j ? P[v] + m->dof_armature[i] : P[v];
-            MR(i)[j] = x;
-            MR(j)[i] = x;
+            m_set(i, j, x);
+            m_set(j, i, x);
           } else if (!((m->dof_chainmask[j] >> i) & 1u)) {
-            MR(i)[j] = 0.f;
+            m_set(i, j, 0.f);
           }
         } else {
-          MR(i)[j] = i == j ? 1.f : 0.f;
+          m_set(i, j, i == j ? 1.f : 0.f);
         }
       }
       const uint32_t sub = mr < nv ? m->dof_submask[mr] : 0u;
@@ -3295,7 +3355,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       } else if (i == j) {
         v = 1.f;
       }
-      MR(i)[j] = v;
+      m_set(i, j, v);
     }
     }
     if (lane < nv) {
@@ -3336,11 +3396,11 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     if (S::CPW == 1 && blk_usable<NVW>(m)) {
       // M is block diagonal by kinematic tree: one chain for all trees
       if (lane >= nv && lane < NVW) s.qas[lane] = 0.f;
-      blk_solve<NVW>(m, [&](int i, int j) { return MR(i)[j]; }, s.qfs, s.qas, lane, &s.xpos[0][0]);
+      blk_solve<NVW>(m, [&](int i, int j) { return m_get(i, j); }, s.qfs, s.qas, lane, &s.xpos[0][0]);
     } else {
       float Lm[NVW];
 #pragma unroll
-      for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? MR(lane)[j] : 0.f;
+      for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? m_get(lane, j) : 0.f;
       // the dynamics region (xpos..fvec) is dead once M is assembled
       float x;
       if constexpr (NVW == 16 && MPCR_DPP_CHOL) {
@@ -3792,7 +3852,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
         // warm start: the better of qacc_warmstart and qacc_smooth
         if (!(m->disableflags & 4)) {
           // (the Gauss term of qacc_smooth itself is (M a_s - f_s)'(a_s - a_s) = 0)
-          const float maw = lane < nv ? dotN<NVW>(MR(lane), s.qws) : 0.f;
+          const float maw = lane < nv ? m_dot(lane, s.qws) : 0.f;
           const float gw = lane < nv ? (maw - s.qfs[lane]) * (s.qws[lane] - s.qas[lane]) : 0.f;
           float cw = 0.f, cs = 0.f;
           for (int r = lane; r < nefc; r += S::HL) {
@@ -3845,7 +3905,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           wt_newton++;
 #endif
           // Ma, jar, cost at the current qacc; per-row force and active D
-          const float ma = lane < nv ? dotN<NVW>(MR(lane), s.qacc) : 0.f;
+          const float ma = lane < nv ? m_dot(lane, s.qacc) : 0.f;
           float cc = 0.f;
           for (int r = lane; r < nefc; r += S::HL) {
             const float jar = jdot(s, gx, r, s.qacc) - s.efc_aref[r];
@@ -3891,7 +3951,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
             // H[gi][4 gq ..], the same products in the same row order as the
             // VALU build (the MFMA is a k-ordered fmaf chain), so H is
             // bitwise the VALU one
-            const float4 m4 = reinterpret_cast<const float4*>(MR(gi))[gq];
+            const float4 m4 = m_quad(gi, gq);
             mfx4 hacc = {m4.x, m4.y, m4.z, m4.w};
             mfx4 gacc = {0.f, 0.f, 0.f, 0.f};
             for (int r0 = 0; r0 < nefc; r0 += 4) {
@@ -3951,7 +4011,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
             constexpr int QPL = NVW / 4 / RPW;
             float4 hq[QPL];
 #pragma unroll
-            for (int k = 0; k < QPL; k++) hq[k] = reinterpret_cast<const float4*>(MR(gi))[gq + RPW * k];
+            for (int k = 0; k < QPL; k++) hq[k] = m_quad(gi, gq + RPW * k);
             if constexpr (MFMA_HESS_W) {
               // J^T D J on v_mfma_f32_32x32x2_f32: accumulator register 4k + e of
               // lane (gi, gq) is H[gi][4 (gq + 2k) + e] in the transposed view --
@@ -4047,7 +4107,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           if (lane < NVW) s.srch[lane] = search;
           sync();
           // Mv, jv, quadratic coefficients
-          const float mvv = lane < nv ? dotN<NVW>(MR(lane), s.srch) : 0.f;
+          const float mvv = lane < nv ? m_dot(lane, s.srch) : 0.f;
           for (int r = lane; r < nefc; r += S::HL) s.efc_jv[r] = jdot(s, gx, r, s.srch);
           const float sn = sqrtf(hsum<S::CPW>(search * search));
           const float gtol = m->tolerance * m->ls_tolerance * sn * m->meaninertia * (float)(nv > 1 ? nv : 1);
@@ -4178,13 +4238,13 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
         if (S::CPW == 1 && !m->impl_cross && blk_usable<NVW>(m)) {  // M + dt D block diagonal by tree
           if (lane < NVW) s.srch[lane] = lane < nv ? s.qfs[lane] + qc : 0.f;
           sync();
-          blk_solve<NVW>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], MR(i)[j]); }, s.srch, s.srch,
+          blk_solve<NVW>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], m_get(i, j)); }, s.srch, s.srch,
                          lane, &s.gxpos[0][0]);
           sync();
         } else {
           float Lm[NVW];
 #pragma unroll
-          for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? fmaf(dt, m->impl_D[lane][j], MR(lane)[j]) : 0.f;
+          for (int j = 0; j < NVW; j++) Lm[j] = lane < NVW ? fmaf(dt, m->impl_D[lane][j], m_get(lane, j)) : 0.f;
           chol_rows(Lm, lane);
           const float a = chol_solve<NVW, S::LD>(Lm, lane < nv ? s.qfs[lane] + qc : 0.f, lane, &s.gxpos[0][0]);
           if (lane < NVW) s.srch[lane] = lane < nv ? a : 0.f;
@@ -4298,7 +4358,6 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
 #endif
 }
 
-#undef MR
 
 // ---------------------------------------------------------------------------
 // launchers (the host side lives in another translation unit)
@@ -4327,6 +4386,10 @@ int rollout_set_wpc2_max_n(int n) {
 // results.  MPCR_WPC2W_MAX_N overrides.
 #ifndef MPCR_W_WPC2
 #define MPCR_W_WPC2 1
+#endif
+// extra dynamic LDS per one-wave dual-arm block (occupancy experiments only)
+#ifndef MPCR_W_DYN_LDS
+#define MPCR_W_DYN_LDS 0
 #endif
 #if MPCR_W_WPC2
 static const int g_wpc2w_max_n = env_int("MPCR_WPC2W_MAX_N", 1024);
@@ -4386,7 +4449,7 @@ void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsign
         for (int t0 = 0; t0 < a.H; t0 += a.seg) {
           ga.t0 = t0;
           ga.t1 = min(a.H, t0 + a.seg);
-          hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(ng), dim3(WAVE), 0, gs, ga, dm);
+          hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(ng), dim3(WAVE), MPCR_W_DYN_LDS, gs, ga, dm);
         }
       }
       if (G > 1)
@@ -4395,7 +4458,7 @@ void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsign
           (void)hipStreamWaitEvent(st, gev[1 + g], 0);
         }
     } else {
-      hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), 0, st, a, dm);
+      hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), MPCR_W_DYN_LDS, st, a, dm);
     }
   } else {
     if constexpr (SmemN::CPW == 1) {
@@ -4415,7 +4478,7 @@ hipError_t rollout_occupancy(int* info, size_t dyn_lds) {
   for (int v = 0; v < 2; v++) {
     int blocks = 0;
     hipFuncAttributes fa;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k[v], WAVE, v == 0 ? dyn_lds : 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k[v], WAVE, v == 0 ? dyn_lds : MPCR_W_DYN_LDS);
     if (e != hipSuccess) return e;
     e = hipFuncGetAttributes(&fa, k[v]);
     if (e != hipSuccess) return e;

@@ -60,7 +60,7 @@ def main():
         _lib.check(lib.mpcr_rollout_wavetime(e.handle, xi.ctypes.data, MPCR_LAYOUT_XI, n,
                                              q0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), f(w), f(pt), f(qt),
                                              buf.ctypes.data))
-    st = torch.zeros(n, dtype=torch.int32, device="cuda")  # per-candidate rows: max (bits 2-7), sum (8-)
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")  # per-candidate rows: max (bits 2-9), sum (10-)
     e.rollout_cost(torch.tensor(xi, device="cuda"), MPCR_LAYOUT_XI, q0, w, pt, qt, status=st)
     sv = st.cpu().numpy()
     rows_mean, rows_max = (sv >> 10) / H, (sv >> 2) & 255
