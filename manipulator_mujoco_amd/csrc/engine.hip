@@ -570,6 +570,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
       if (te[t] - d.mc_c0[i] > SmemW::MCW) ok = false;
     }
     d.mc_n = ok && m.nv * SmemW::MCW <= SmemW::MC ? m.nv : 0;
+    if (env_int_or("MPCR_M_SLAB", 0)) d.mc_n = 0;  // tests: the HBM-slab path on a model that fits
   }
   for (int i = 0; i < m.nq; i++) d.qpos_init[i] = (float)m.qpos_init[i];
   for (int i = 0; i < m.nv; i++) d.qvel_init[i] = (float)m.qvel_init[i];

@@ -216,10 +216,10 @@ struct __align__(16) SmemT {
 // 39, so the slab serves a minority of the rows), the contacts overlaid with
 // the Newton-only row arrays, the cost history and the Bernstein
 // coefficients in HBM: 9.3 KB of LDS -> 16 blocks per CU = 4 waves/SIMD at 128
-// VGPRs (was 17.3 KB and 178 VGPRs: 2 waves/SIMD).  Measured on MI355X: 12
-// resident blocks need <= 12704 B each (12832 B runs at the 11-block speed
-// although hipOccupancy reports 12), i.e. about 150 KB of the CU's 160 KB LDS
-// is allocatable to one kernel's blocks; 16 blocks therefore need <= 9520 B.
+// VGPRs (was 17.3 KB and 178 VGPRs: 2 waves/SIMD).  Measured on MI355X
+// (round 4, extra dynamic LDS on C3): 16 blocks per CU up to 10240 B each
+// (the CU's whole 160 KB), 15 at 10368 B; the image keeps 9520 B (the J rows
+// in LDS 40 -> 44 / 48 gained nothing).
 #ifndef MPCR_N_MAXEFC
 #define MPCR_N_MAXEFC DX_MAXEFC
 #endif

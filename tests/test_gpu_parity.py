@@ -456,3 +456,28 @@ def test_dual_arm_horizon_segments_bitwise(torch_cuda, monkeypatch, seg, groups)
         del e
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
+
+
+def test_dual_arm_compact_mass_matrix_bitwise_slab(torch_cuda, monkeypatch):
+    """The dual-arm mass matrix kept compact in LDS (16-column tree windows,
+    DevModel::mc_c0) gives bitwise the costs, theta, thetadot and status of
+    the dense per-candidate HBM slab (MPCR_M_SLAB=1, the path for models whose
+    trees do not fit the window): the window leaves out exact zeros only."""
+    torch = torch_cuda
+    n, H = 1536, 40
+    m = models.load("dual_arm", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 9, torch.device("cuda:0"))
+    out = []
+    for slab in ("0", "1"):
+        monkeypatch.setenv("MPCR_M_SLAB", slab)
+        e = Engine(m, H, n, Pd)
+        st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+        th = torch.empty((n, 6 * H), device="cuda:0")
+        td = torch.empty((n, 6 * H), device="cuda:0")
+        c = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, theta=th, thetadot=td, status=st).clone()
+        torch.cuda.synchronize()
+        out.append((c, th, td, st))
+        del e
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
