@@ -92,26 +92,29 @@ def _pmc_rows(path, kernel="rollout_kernel"):
     return out
 
 
-def pmc_traffic(path):
-    """HBM bytes per dispatch from a committed rocprofv3 --pmc CSV (FETCH_SIZE
-    doubled per the gfx950 note in MI355X_MICROARCH.md §HBM, plus WRITE_SIZE;
-    both KiB)."""
+def pmc_traffic(path, dispatches=1):
+    """HBM bytes per rollout call from a committed rocprofv3 --pmc CSV
+    (FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md §HBM, plus
+    WRITE_SIZE; both KiB): the mean per dispatch times the call's dispatches
+    (Engine.dispatches: the dual-arm shard runs as horizon segments)."""
     c = _pmc_rows(path)
     if "FETCH_SIZE" not in c and "WRITE_SIZE" not in c:
         return None
     kb = 2.0 * float(np.mean(c.get("FETCH_SIZE", [0.0]))) + float(np.mean(c.get("WRITE_SIZE", [0.0])))
-    return kb * 1024.0
+    return kb * 1024.0 * dispatches
 
 
-def pmc_valu(path, n, H, flops_step):
+def pmc_valu(path, n, H, flops_step, dispatches=1):
     """VALU instructions per candidate-step (over all of a candidate's waves:
-    the two-wave variant runs two) and the lane-flop efficiency flops / (64 x
-    VALU instructions) from a committed SQ counter CSV of the same workload."""
+    the two-wave variant runs two, a segmented call one per segment) and the
+    lane-flop efficiency flops / (64 x VALU instructions) from a committed SQ
+    counter CSV of the same workload (per-dispatch means times the call's
+    dispatches)."""
     c = _pmc_rows(path)
     if "SQ_INSTS_VALU" not in c:
         return None
-    insts = float(np.mean(c["SQ_INSTS_VALU"]))
-    waves = float(np.mean(c.get("SQ_WAVES", [n])))
+    insts = float(np.mean(c["SQ_INSTS_VALU"])) * dispatches
+    waves = float(np.mean(c.get("SQ_WAVES", [n]))) * dispatches
     per = insts / (n * H)
     rec = {"valu_insts_per_candidate_step": round(per, 1), "waves_per_candidate": round(waves / n, 2),
            "lane_flop_efficiency": round(flops_step / (64.0 * per), 4), "source": os.path.relpath(path, ROOT)}
@@ -457,8 +460,9 @@ def main():
             committed_counters("rollout", sfx) if default_prof else (None, None))
         pmc_sq, sq_src = (args.pmc_sq, "--pmc-sq " + args.pmc_sq) if args.pmc_sq else (
             committed_counters("sq", sfx) if default_prof else (None, None))
-        traffic = pmc_traffic(pmc) if pmc else None
-        valu = pmc_valu(pmc_sq, n, H, fps) if pmc_sq else None
+        ndisp = eng.dispatches(n)  # kernel dispatches per rollout call (horizon segments)
+        traffic = pmc_traffic(pmc, ndisp) if pmc else None
+        valu = pmc_valu(pmc_sq, n, H, fps, ndisp) if pmc_sq else None
         if valu is not None:
             valu["source"] = sq_src
         rec = {
@@ -484,7 +488,7 @@ def main():
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_VALU_TFLOPS, 5),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": pmc_src if traffic is not None else pmc_src or "not profiled in this run",
-                         "kernel": "rollout_kernel", "kernel_ms": round(kern_ms, 4),
+                         "kernel": "rollout_kernel", "dispatches_per_call": ndisp, "kernel_ms": round(kern_ms, 4),
                          "kernel_ms_mean": round(float(np.mean(kms)), 4),
                          "flops_per_step": fps, "hbm_algorithmic_bytes": hbm_launch,
                          "hbm_achieved_GBs": round(hbm_launch / (kern_ms * 1e-3) / 1e9, 2),

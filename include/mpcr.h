@@ -137,6 +137,12 @@ int mpcr_rollout_occupancy(int device, int* info);
    Process-wide (an atomic read by every engine's next launch; the
    environment is read once, when the library loads). */
 int mpcr_set_two_wave_max_n(int n);
+/* Kernel dispatches one mpcr_rollout_cost call over n candidates issues on
+   this engine (1, or -- dual-arm batches above the resident-block count --
+   one per horizon segment and candidate group, MPCR_SEG_STEPS /
+   MPCR_SEG_GROUPS): a profiler's per-dispatch counters times *out are per
+   call.  No GPU work. */
+int mpcr_engine_dispatches(const mpcr_engine* e, int n, int* out);
 
 /* Same as mpcr_rollout_cost with MPCR_F_DEVICE_PTRS, except that the
    per-call arguments are a device block read when the kernel runs:

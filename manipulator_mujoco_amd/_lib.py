@@ -27,7 +27,7 @@ EXPORTS = (
     "mpcr_rollout_cost", "mpcr_argmin", "mpcr_best_key_decode", "mpcr_topk", "mpcr_cem_create", "mpcr_cem_free",
     "mpcr_cem_factor", "mpcr_cem_sample_project", "mpcr_project", "mpcr_cem_update", "mpcr_rollout_cost_dp",
     "mpcr_plant_create", "mpcr_plant_free", "mpcr_plant_set_state", "mpcr_plant_get_state", "mpcr_plant_step",
-    "mpcr_rollout_occupancy", "mpcr_set_two_wave_max_n", "mpcr_comm_unique_id", "mpcr_comm_init", "mpcr_comm_free", "mpcr_comm_allreduce_key",
+    "mpcr_rollout_occupancy", "mpcr_set_two_wave_max_n", "mpcr_engine_dispatches", "mpcr_comm_unique_id", "mpcr_comm_init", "mpcr_comm_free", "mpcr_comm_allreduce_key",
     "mpcr_comm_allgather", "mpcr_comm_gather_elites",
 )
 _VOID = ("mpcr_last_error", "mpcr_model_free", "mpcr_engine_free", "mpcr_best_key_decode", "mpcr_cem_free",
@@ -84,6 +84,7 @@ def load():
     lib.mpcr_plant_step.argtypes = [vp, P(d), i, vp]
     lib.mpcr_rollout_occupancy.argtypes = [i, P(i)]
     lib.mpcr_set_two_wave_max_n.argtypes = [i]
+    lib.mpcr_engine_dispatches.argtypes = [vp, i, P(i)]
     lib.mpcr_plant_step_debug.argtypes = [vp, P(d), vp, i]
     lib.mpcr_plant_dbg_size.argtypes = []
     lib.mpcr_comm_unique_id.argtypes = [ctypes.c_char_p]

@@ -1088,6 +1088,19 @@ static int launch_rollout(mpcr_engine* e, const Launch& l, hipStream_t st) {
 
 extern "C" int mpcr_set_two_wave_max_n(int n) { return rollout_set_wpc2_max_n(n); }
 
+extern "C" int mpcr_engine_dispatches(const mpcr_engine* e, int n, int* out) {
+  if (!e || !out) return fail(MPCR_EINVAL, "null argument");
+  if (n < 0 || n > e->max_n) return fail(MPCR_EINVAL, "n=%d outside [0, max_n=%d]", n, e->max_n);
+  RolloutArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.H = e->H;
+  a.seg_state = e->d_seg;
+  a.seg = e->d_seg ? e->seg_steps : 0;
+  a.seg_min_n = e->seg_min_n;
+  *out = rollout_dispatches(e->wide, a, n, e->seg_groups, e->seg_stream[0] != nullptr);
+  return MPCR_OK;
+}
+
 extern "C" int mpcr_rollout_occupancy(int device, int* info) {
   if (!info) return fail(MPCR_EINVAL, "null argument");
   HIPCHK(hipSetDevice(device));

@@ -282,6 +282,9 @@ static_assert(sizeof(SmemW) <= 20448, "dual-arm LDS image must fit 8 blocks per 
 // so one segment's tail is filled by the other groups' work.
 void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigned grid, size_t dyn_lds,
                     hipStream_t st, int groups = 0, hipStream_t* gstream = nullptr, hipEvent_t* gev = nullptr);
+// kernel dispatches rollout_launch issues for the same arguments (gstream /
+// gev given: streams)
+int rollout_dispatches(bool wide, const RolloutArgs& a, unsigned grid, int groups, bool streams);
 // resident blocks per CU, static LDS bytes, VGPRs: narrow (0..2), wide (3..5)
 hipError_t rollout_occupancy(int* info, size_t dyn_lds);
 int rollout_set_wpc2_max_n(int n);  // two waves per candidate up to n (narrow variant); returns the previous

@@ -4421,21 +4421,40 @@ static RolloutArgs group_args(const RolloutArgs& a, int off, int n) {
   return g;
 }
 
+// whether rollout_launch runs a batch as horizon segments, and over how many
+// candidate groups (*G)
+static bool seg_plan(bool wide, const RolloutArgs& a, unsigned grid, int groups, bool streams, int* G) {
+  if (!wide) return false;
+#if MPCR_W_WPC2
+  if ((int)grid <= wpc2w_max_n()) return false;
+#endif
+  if (!(a.seg > 0 && a.seg < a.H && a.seg_state && !a.plant && !a.dbg && (int)grid > a.seg_min_n)) return false;
+  *G = groups > 1 && streams && (int)grid >= 2 * groups ? groups : 1;
+  return true;
+}
+
+int rollout_dispatches(bool wide, const RolloutArgs& a, unsigned grid, int groups, bool streams) {
+  int G = 1;
+  if (grid == 0) return 0;
+  if (!seg_plan(wide, a, grid, groups, streams, &G)) return 1;
+  return G * ((a.H + a.seg - 1) / a.seg);
+}
+
 void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsigned grid, size_t dyn_lds,
                     hipStream_t st, int groups, hipStream_t* gstream, hipEvent_t* gev) {
   RolloutArgs a = a0;
   a.t0 = 0;
   a.t1 = a.H;
+  int G = 1;
 #if MPCR_W_WPC2
   if (wide && (int)grid <= wpc2w_max_n())
     hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);
   else
 #endif
   if (wide) {
-    if (a.seg > 0 && a.seg < a.H && a.seg_state && !a.plant && !a.dbg && (int)grid > a.seg_min_n) {
+    if (seg_plan(wide, a, grid, groups, gstream && gev, &G)) {
       // horizon segments over candidate groups on their own streams: each
       // group's segments in its stream's order, the groups overlapping
-      const int G = groups > 1 && gstream && gev && (int)grid >= 2 * groups ? groups : 1;
       if (G > 1) {
         (void)hipEventRecord(gev[0], st);
         for (int g = 0; g < G; g++) (void)hipStreamWaitEvent(gstream[g], gev[0], 0);

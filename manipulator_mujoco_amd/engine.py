@@ -67,6 +67,15 @@ class Engine:
             pass
         self.handle = None
 
+    def dispatches(self, n: int) -> int:
+        """Kernel dispatches one rollout_cost over n candidates issues
+        (mpcr_engine_dispatches: horizon segments x candidate groups for large
+        dual-arm batches, else 1) -- per-dispatch profiler counters times this
+        are per call."""
+        out = ctypes.c_int()
+        check(_lib.load().mpcr_engine_dispatches(self.handle, int(n), ctypes.byref(out)))
+        return int(out.value)
+
     @staticmethod
     def _vec(x, n, dtype):
         a = np.zeros(n, dtype=dtype)

@@ -445,6 +445,10 @@ def test_dual_arm_horizon_segments_bitwise(torch_cuda, monkeypatch, seg, groups)
         monkeypatch.setenv("MPCR_SEG_STEPS", str(steps))
         monkeypatch.setenv("MPCR_SEG_GROUPS", str(g))
         e = Engine(m, H, n, Pd)
+        # one dispatch, or one per segment and group (mpcr_engine_dispatches;
+        # the batch is above the 2048 resident blocks, so it is segmented)
+        assert e.dispatches(n) == (1 if steps == 0 else g * -(-H // steps)), (steps, g)
+        assert e.dispatches(1024) == 1  # the two-wave variant: one round
         st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
         th = torch.empty((n, 6 * H), device="cuda:0")
         td = torch.empty((n, 6 * H), device="cuda:0")
