@@ -21,9 +21,13 @@
 
 // extra dynamic LDS per narrow-kernel block (occupancy experiments only)
 // horizon segments of dual-arm rollouts (rollout_launch): steps per segment
-// (0 = one launch) and candidate groups on their own streams
+// (0 = one launch) and candidate groups on their own streams.  Measured
+// (tools/seg_sweep_r04.sh; C4 shard 4096 x 100 / C5 rollout 8192 x 50, ms):
+// one launch 50.6 / 48.5; 2 groups x 25 steps 47.8 / 47.4, x 13-10 46.7 /
+// 45.8, x 7 46.3 / 45.0, x 5-3 46.4-46.6 / 45.1; 3 groups 47.3-49.5; 4
+// groups 65-67 (more streams than the process's 4 hardware queues)
 #ifndef MPCR_SEG_STEPS_DEFAULT
-#define MPCR_SEG_STEPS_DEFAULT 25
+#define MPCR_SEG_STEPS_DEFAULT 7
 #endif
 #ifndef MPCR_SEG_GROUPS_DEFAULT
 #define MPCR_SEG_GROUPS_DEFAULT 2
