@@ -36,9 +36,12 @@ enum { ST_QPOS = 0, ST_QVEL = DX_NQ, ST_QWS = ST_QVEL + DX_NV, ST_QACC = ST_QWS 
        ST_N = ST_EEF + 8 };
 
 // horizon-segment state per candidate (RolloutArgs::seg_state): qpos (DX_NQ),
-// qvel and the warm start (32 each), then 6 registers x 64 lanes (cost_g,
-// cost_r, cost_c, status, rows summed, rows max)
-constexpr int SEG_QPOS = 0, SEG_QVEL = DX_NQ, SEG_QWS = DX_NQ + 32, SEG_REG = DX_NQ + 64, SEG_STRIDE = SEG_REG + 6 * 64;
+// qvel and the warm start (32 each), every lane's cost_c (the outputs sum it
+// over lanes), then lane 0's cost_g, cost_r, status, rows summed, rows max
+// (the outputs read them from lane 0 only; the other lanes' copies are never
+// read): 672 B per candidate
+constexpr int SEG_QPOS = 0, SEG_QVEL = DX_NQ, SEG_QWS = DX_NQ + 32, SEG_COSTC = DX_NQ + 64, SEG_SCAL = DX_NQ + 128,
+              SEG_STRIDE = SEG_SCAL + 8;
 
 // pacing table: (XCC 8 x SE 8 x SH 2 x CU 16 x SIMD 4) groups of 16 wave slots
 constexpr unsigned MPCR_PACE_SLOTS = 8u * 8u * 2u * 16u * 4u * 16u;
@@ -68,7 +71,7 @@ struct RolloutArgs {
   // 0 resumes from seg_state, one that does not end at H saves to it and
   // writes no outputs (the engine launches the segments in stream order:
   // kernel boundaries order them, rollout_launch)
-  float* seg_state;  // n x SEG_STRIDE: qpos | qvel | qws | per-lane registers
+  float* seg_state;  // n x SEG_STRIDE: qpos | qvel | qws | cost_c per lane | lane 0 scalars
   int t0, t1, seg;   // segment [t0, t1); seg = steps per segment for rollout_launch (0: one launch)
   int nctrl, nslot;  // the model's (host side: per-candidate strides of grouped launches)
   int seg_min_n;     // segments only for batches above this (the one-wave variant's resident blocks)

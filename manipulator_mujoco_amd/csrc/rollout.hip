@@ -2791,10 +2791,11 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
 #pragma unroll
     for (int c = 0; c < 4; c++) shist.v[j][c] = 0.f;
   int status = 0, nefc_sum = 0, nefc_max = 0;
-  if (resume) {  // this lane's accumulators as the previous segment left them
-    const float* rg = segs + SEG_REG + lane;
-    cost_g = rg[0]; cost_r = rg[64]; cost_c = rg[128];
-    status = __float_as_int(rg[192]); nefc_sum = __float_as_int(rg[256]); nefc_max = __float_as_int(rg[320]);
+  if (resume) {  // the accumulators as the previous segment left them (lane 0's scalars on every lane)
+    cost_c = segs[SEG_COSTC + lane];
+    const float* sc = segs + SEG_SCAL;
+    cost_g = sc[0]; cost_r = sc[1];
+    status = __float_as_int(sc[2]); nefc_sum = __float_as_int(sc[3]); nefc_max = __float_as_int(sc[4]);
   }
   // this lane's controlled joint addresses, held across the horizon (read
   // every step; the per-step model launder would otherwise reload them)
@@ -4305,9 +4306,12 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       segs[SEG_QVEL + lane] = s.qvel[lane];
       segs[SEG_QWS + lane] = s.qws[lane];
     }
-    float* rg = segs + SEG_REG + lane;
-    rg[0] = cost_g; rg[64] = cost_r; rg[128] = cost_c;
-    rg[192] = __int_as_float(status); rg[256] = __int_as_float(nefc_sum); rg[320] = __int_as_float(nefc_max);
+    segs[SEG_COSTC + lane] = cost_c;
+    if (lane == 0) {
+      float* sc = segs + SEG_SCAL;
+      sc[0] = cost_g; sc[1] = cost_r;
+      sc[2] = __int_as_float(status); sc[3] = __int_as_float(nefc_sum); sc[4] = __int_as_float(nefc_max);
+    }
 #if MPCR_PACE
     if (pace && lane == pace_own) __hip_atomic_store(pace + lane, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
