@@ -1276,10 +1276,22 @@ static int mpr_impl(const mpcr_model_t* m, const odata* d, int g1, int g2, doubl
 
 static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int g2, const double n[3], double depth,
                          ocontact* out);
+static int caps_poly(const mpcr_model_t* m, odata* d, int g1, int g2, double depth, ocontact* out);
+/* Experiment (ORACLE_CAPS_SAT=1 in the environment; not in the kernel, off by
+   default): a capsule or cylinder penetrating a polyhedron deeper than
+   POLY_DEEP takes the polyhedron's face axis of least penetration (MJX's
+   capsule_convex SAT over face normals) instead of MPR's portal normal --
+   tools/diag_f32.py measures what it does to the fp32 restatement's misses */
+static int caps_sat_on(void) {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("ORACLE_CAPS_SAT"); v = e ? atoi(e) : 0; }
+  return v;
+}
 static void col_convex(const mpcr_model_t* m, odata* d, int pair, int g1, int g2, ocontact* out) {
   double depth, n[3], pos[3];
   if (!mpr(m, d, g1, g2, &depth, n, pos, d->hint[pair])) return;
   if (n[0] == 0 && n[1] == 0 && n[2] == 0) n[2] = 1; /* touching: any frame */
+  if (caps_sat_on() && depth > 5e-3 && caps_poly(m, d, g1, g2, depth, out)) return;
   /* polyhedron pairs: the face-clipping manifold when a face axis carries
      the contact, else MPR's single point */
   if (m->pair_ncon[pair] == 4 && depth > 0 && poly_manifold(m, d, pair, g1, g2, n, depth, out)) return;
@@ -2648,3 +2660,67 @@ void oracle_install_crash_bt(void) {
   signal(SIGBUS, oracle_crash_bt);
 }
 
+
+
+/* the experiment above (ORACLE_CAPS_SAT): capsule / cylinder against a
+   polyhedron (mesh hull or box with face tables), relative to the
+   polyhedron's centre; the face with the largest separation (lowest index
+   within the near_max band) carries one contact, unless it is more than 5 %
+   (+10 um) deeper than MPR's depth (an edge axis: MPR's point stays) */
+static int caps_poly(const mpcr_model_t* m, odata* d, int g1, int g2, double depth, ocontact* out) {
+  const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const int round1 = t1 == MPCR_GEOM_CAPSULE || t1 == MPCR_GEOM_CYLINDER;
+  const int round2 = t2 == MPCR_GEOM_CAPSULE || t2 == MPCR_GEOM_CYLINDER;
+  const int poly1 = (t1 == MPCR_GEOM_MESH || t1 == MPCR_GEOM_BOX) && m->geom_faceadr[g1] >= 0;
+  const int poly2 = (t2 == MPCR_GEOM_MESH || t2 == MPCR_GEOM_BOX) && m->geom_faceadr[g2] >= 0;
+  int gc, gp;
+  if (round1 && poly2) { gc = g1; gp = g2; }
+  else if (round2 && poly1) { gc = g2; gp = g1; }
+  else return 0;
+  const int nf = m->geom_facenum[gp], fa = m->geom_faceadr[gp];
+  if (nf <= 0 || nf > POLY_ALLF) return 0;
+  const double* cg = d->geom_xpos[gp];
+  const double* Rc = d->geom_xmat[gc];
+  const double ax[3] = {Rc[2], Rc[5], Rc[8]};
+  const double r = m->geom_size[gc][0], hl = m->geom_size[gc][1];
+  const double cc[3] = {d->geom_xpos[gc][0] - cg[0], d->geom_xpos[gc][1] - cg[1], d->geom_xpos[gc][2] - cg[2]};
+  const int cyl = m->geom_type[gc] == MPCR_GEOM_CYLINDER;
+  double sep[POLY_ALLF], mx = -1e300;
+  for (int k = 0; k < nf; k++) {
+    double nw[3], off;
+    face_world(m, d, gp, fa + k, nw, &off, cg);
+    const double na = dot3(nw, ax);
+    /* the round geom's support along -nw: its deepest point into the face plane */
+    double lo = dot3(nw, cc) - hl * fabs(na);
+    lo -= cyl ? r * sqrt(fmax(0.0, 1.0 - na * na)) : r;
+    sep[k] = lo - off;
+    if (sep[k] > mx) mx = sep[k];
+  }
+  int bf = -1;
+  for (int k = 0; k < nf && bf < 0; k++)
+    if (near_max(sep[k], mx)) bf = k;
+  if (bf < 0 || sep[bf] < -depth * 1.05 - 1e-5) return 0;
+  double nw[3], off;
+  face_world(m, d, gp, fa + bf, nw, &off, cg);
+  const double na = dot3(nw, ax);
+  /* the deepest point of the round geom (an end, or the nearer end's rim) */
+  const double sa = na > 0 ? -1.0 : (na < 0 ? 1.0 : 0.0);
+  double e[3], rim[3] = {0, 0, 0};
+  for (int k = 0; k < 3; k++) e[k] = cc[k] + sa * hl * ax[k];
+  if (cyl) {
+    double t[3];
+    for (int k = 0; k < 3; k++) t[k] = nw[k] - na * ax[k];
+    const double tl = norm3(t);
+    if (tl > 1e-12) for (int k = 0; k < 3; k++) rim[k] = -r * t[k] / tl;
+  } else {
+    for (int k = 0; k < 3; k++) rim[k] = -r * nw[k];
+  }
+  const double dist = sep[bf];
+  double pos[3], n[3];
+  for (int k = 0; k < 3; k++) {
+    pos[k] = e[k] + rim[k] - 0.5 * dist * nw[k] + cg[k];
+    n[k] = gp == g2 ? -nw[k] : nw[k]; /* geom1 -> geom2 */
+  }
+  set_contact(out, dist, pos, n);
+  return 1;
+}
