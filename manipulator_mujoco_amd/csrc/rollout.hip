@@ -1733,13 +1733,44 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
       for (int c = 0; c < 3; c++) pp[c] = a[c] + ts * dd[c];
       g = point_box(pp, h, nl, q);
     }
+    // the far end: on or in the box, the first point's face, the segment
+    // clipped to the face's extent (the oracle's col_capsule_box, round 4);
+    // outside, its own point_box
+    int fk = -1;
+    float fsg = 0.f;
+    if (g <= 0.f) {
+#pragma unroll
+      for (int c = 0; c < 3; c++)
+        if (nl[c] != 0.f) { fk = c; fsg = -nl[c]; }
+    }
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       if (k == 1) {
         float t = ts < 0.5f ? 1.f : 0.f;
+        if (fk >= 0) {
 #pragma unroll
-        for (int c = 0; c < 3; c++) pp[c] = a[c] + t * dd[c];
-        g = point_box(pp, h, nl, q);
+          for (int j = 0; j < 3; j++) {
+            if (j == fk || !(fabsf(dd[j]) > kMinVal)) continue;
+            const float x = a[j] + t * dd[j];
+            if (fabsf(x) > h[j]) {
+              const float tb = ((x > 0.f ? h[j] : -h[j]) - a[j]) / dd[j];
+              t = ts < t ? fminf(t, fmaxf(tb, ts)) : fmaxf(t, fminf(tb, ts));
+            }
+          }
+          float gf = 0.f;
+#pragma unroll
+          for (int c = 0; c < 3; c++) {
+            pp[c] = a[c] + t * dd[c];
+            nl[c] = c == fk ? -fsg : 0.f;
+            q[c] = c == fk ? fsg * h[c] : pp[c];
+            gf = c == fk ? fsg * pp[c] - h[c] : gf;
+          }
+          g = gf;
+        } else {
+#pragma unroll
+          for (int c = 0; c < 3; c++) pp[c] = a[c] + t * dd[c];
+          g = point_box(pp, h, nl, q);
+        }
       }
       float n[3], pl[3], tmp[3];
       mv(n, R2, nl);

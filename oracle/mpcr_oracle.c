@@ -769,11 +769,43 @@ static void col_capsule_box(const odata* d, int gc, int gb, const double* sc, co
     for (int k = 0; k < 3; k++) p[k] = a[k] + ts * dd[k];
     g = point_box(p, h, nl, q);
   }
+  /* The second contact (round 4): when the first point is on or in the box,
+     the far end takes the same box face -- its distance to that face's plane,
+     the segment clipped to the face's extent (the end moved back along the
+     segment to where it leaves the face rectangle) -- as MJX's capsule-convex
+     clipping keeps both contacts on one reference face.  Its own point_box
+     (round 3) switched between the face's normal and the direction to the box
+     edge as the end crossed the table's edge, a discontinuity fp32 and fp64
+     took differently (the fp32 restatement's C4
+     well-conditioned misses 12 -> 8).  A first point outside the box keeps
+     point_box for the far end. */
+  int fk = -1;
+  double fsg = 0;
+  if (g <= 0) {
+    for (int k = 0; k < 3; k++) if (nl[k] != 0) { fk = k; fsg = -nl[k]; }
+  }
   for (int s = 0; s < 2; s++) {
     double t = s == 0 ? ts : (ts < 0.5 ? 1.0 : 0.0);
     if (s == 1) {
-      for (int k = 0; k < 3; k++) p[k] = a[k] + t * dd[k];
-      g = point_box(p, h, nl, q);
+      if (fk >= 0) {
+        for (int j = 0; j < 3; j++) {
+          if (j == fk || fabs(dd[j]) <= MINVAL) continue;
+          const double x = a[j] + t * dd[j];
+          if (fabs(x) > h[j]) {
+            const double tb = ((x > 0 ? h[j] : -h[j]) - a[j]) / dd[j];
+            t = ts < t ? fmin(t, fmax(tb, ts)) : fmax(t, fmin(tb, ts));
+          }
+        }
+        for (int k = 0; k < 3; k++) p[k] = a[k] + t * dd[k];
+        nl[0] = nl[1] = nl[2] = 0;
+        nl[fk] = -fsg;
+        memcpy(q, p, 3 * sizeof(double));
+        q[fk] = fsg * h[fk];
+        g = fsg * p[fk] - h[fk];
+      } else {
+        for (int k = 0; k < 3; k++) p[k] = a[k] + t * dd[k];
+        g = point_box(p, h, nl, q);
+      }
     }
     double n[3], pl[3], pos[3];
     mulmv(n, Rb, nl);

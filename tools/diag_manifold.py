@@ -1,6 +1,7 @@
 """Diagnostic: the plane-mesh manifold on a dual-arm candidate whose large
-hulls touch the table (candidate 2986 of the seed-20250632 C4 batch, the
-slowest before the wave-cooperative manifold).  Plant (GPU, wide kernel) vs
+hulls touch the table (candidate 2989 of the seed-20250632 C4 batch; 2986,
+the slowest before the wave-cooperative manifold, until round 4's capsule-box
+rule changed its trajectory).  Plant (GPU, wide kernel) vs
 oracle, re-synced to the oracle's fp64 state every step: active contacts of
 the plane-mesh pairs and qacc."""
 import os
@@ -26,7 +27,7 @@ def candidate_td(idx, H=100, n=4096, seed=20250632):
     return q0, np.einsum("tk,jk->jt", Pd.astype(np.float32), xi.reshape(6, 11)).astype(np.float64)
 
 
-def run(idx=2986, H=100):
+def run(idx=2989, H=100):
     m = models.load("dual_arm", 0.05)
     q0, td = candidate_td(idx, H)
     big = {g for g in range(m.ngeom) if int(m.geom_type[g]) == 7 and int(m.geom_hullnum[g]) >= 600}
@@ -61,7 +62,7 @@ def run(idx=2986, H=100):
 
 
 if __name__ == "__main__":
-    rows, big, pairs = run(int(sys.argv[1]) if len(sys.argv) > 1 else 2986)
+    rows, big, pairs = run(int(sys.argv[1]) if len(sys.argv) > 1 else 2989)
     act = [r for r in rows if r["n_mesh"] > 0]
     best = [min(r["qacc_err"], r["qacc_err_f32"]) for r in rows]
     print(f"big hulls {big}, their plane pairs {pairs}; steps with big-hull plane contacts {len(act)}, "
