@@ -20,11 +20,18 @@ CSRC = os.path.join(HERE, "csrc")
 # and is allowed to reassociate fp32 (-fassociative-math needs no signed zeros
 # and no trapping; NaN / Inf semantics stay): 2.29 -> 2.25 ms, parity unchanged.
 # The CEM TU does not get it (top-k orders -0 before +0 like the reference).
+# rollout.hip is compiled twice: MPCR_TU=1, the single-arm kernels and the
+# launch logic, with those flags; MPCR_TU=2, the dual-arm kernels, with the
+# fast-math device flags dropped (_drop_fast: IEEE division / square root, no
+# reassociation) -- the latency-bound dual arm pays ~5 % (C4 45.9 -> 48.3 ms)
+# and its rollouts keep within the fp32 restatement's drift (C4 shard
+# well-conditioned misses 22 -> 8); the VALU-bound C3 would pay 16 %.
+_ROLLOUT_FLAGS = ["-Xarch_device", "-fno-slp-vectorize", "-Xarch_device", "-fassociative-math",
+                  "-Xarch_device", "-fno-signed-zeros", "-Xarch_device", "-fno-trapping-math"]
 UNITS = [(os.path.join(CSRC, "engine.hip"), []),
-         (os.path.join(CSRC, "rollout.hip"), ["-Xarch_device", "-fno-slp-vectorize",
-                                              "-Xarch_device", "-fassociative-math", "-Xarch_device", "-fno-signed-zeros",
-                                              "-Xarch_device", "-fno-trapping-math"])]
-SRC = [u for u, _ in UNITS]
+         (os.path.join(CSRC, "rollout.hip"), _ROLLOUT_FLAGS + ["-DMPCR_TU=1"]),
+         (os.path.join(CSRC, "rollout.hip"), ["PRECISE"] + _ROLLOUT_FLAGS + ["-DMPCR_TU=2"])]
+SRC = sorted({u for u, _ in UNITS})
 DEPS = SRC + [os.path.join(CSRC, f) for f in ("rollout.h", "cem.hip", "comm.hip", "mpcr_device.h")] + [
     os.path.join(os.path.dirname(HERE), "include", f) for f in ("mpcr.h", "mpcr_model.h")]
 OUT = os.path.join(HERE, "libmpcr.so")
@@ -90,10 +97,10 @@ def compile_lib(out: str, extra=(), verbose: bool = False, precise: bool = False
     import tempfile
     with tempfile.TemporaryDirectory() as tmp:
         objs = []
-        for src, unit_flags in UNITS:
-            obj = os.path.join(tmp, os.path.basename(src) + ".o")
-            fl = FLAGS + list(unit_flags)
-            if precise:
+        for i, (src, unit_flags) in enumerate(UNITS):
+            obj = os.path.join(tmp, f"{os.path.basename(src)}.{i}.o")
+            fl = FLAGS + [f for f in unit_flags if f != "PRECISE"]
+            if precise or "PRECISE" in unit_flags:
                 fl = _drop_fast(fl)
             cmd = [hipcc(), f"--offload-arch={ARCH}", "-c"] + fl + list(extra) + ["-o", obj, src]
             if verbose:

@@ -285,6 +285,11 @@ static_assert(sizeof(SmemW) <= 20448, "dual-arm LDS image must fit 8 blocks per 
 // so one segment's tail is filled by the other groups' work.
 void rollout_launch(bool wide, const RolloutArgs& a, const DevModel* dm, unsigned grid, size_t dyn_lds,
                     hipStream_t st, int groups = 0, hipStream_t* gstream = nullptr, hipEvent_t* gev = nullptr);
+// the dual-arm kernels' launches and occupancy (their own translation unit,
+// rollout.hip built with MPCR_TU = 2): wpc 1 (one wave per candidate, block
+// per candidate) or 2 (two waves); info[0..2] blocks per CU, LDS, VGPRs
+void rollout_wide_launch(int wpc, unsigned grid, hipStream_t st, const RolloutArgs& a, const DevModel* dm);
+hipError_t rollout_wide_occupancy(int* info);
 // kernel dispatches rollout_launch issues for the same arguments (gstream /
 // gev given: streams)
 int rollout_dispatches(bool wide, const RolloutArgs& a, unsigned grid, int groups, bool streams);

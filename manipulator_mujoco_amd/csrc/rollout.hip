@@ -4396,7 +4396,58 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
 
 // ---------------------------------------------------------------------------
 // launchers (the host side lives in another translation unit)
+//
+// This file is compiled twice (manipulator_mujoco_amd/build.py): MPCR_TU = 1
+// holds the single-arm kernels and the launch logic, with the fast-math
+// device flags (C3 is VALU-bound: 1.60 ms, 1.86 ms without them); MPCR_TU = 2
+// holds the dual-arm kernels, compiled without them (IEEE division / square
+// root, no reassociation): the latency-bound dual arm pays ~5 % and its fp32
+// rollouts stay within the scalar fp32 restatement's drift (C4 shard
+// well-conditioned misses 22 -> 8, worst 4.8e-3 -> 7.8e-4).
+// MPCR_TU undefined (0): everything in one unit.
+#ifndef MPCR_TU
+#define MPCR_TU 0
+#endif
 
+// Dual-arm batches up to min(this, the narrow threshold below) run two waves
+// per candidate too (rollout_kernel<32, 32, 72, true, 2>: collision, the MPR
+// flush and the manifolds beside the dynamics).  Its 29 KB image and 235
+// VGPRs leave 4 blocks per CU, so the default is 4 x 256 CUs: every candidate
+// resident in one round (measured on MI355X, H = 100: 1024 candidates 22.6 ->
+// 21.2 ms; 2048 would take two rounds, 24.5 -> 46.3 ms).  Bitwise the one-wave
+// results.  MPCR_WPC2W_MAX_N overrides.
+#ifndef MPCR_W_WPC2
+#define MPCR_W_WPC2 1
+#endif
+// extra dynamic LDS per one-wave dual-arm block (occupancy experiments only)
+#ifndef MPCR_W_DYN_LDS
+#define MPCR_W_DYN_LDS 0
+#endif
+
+#if MPCR_TU != 1
+// the dual-arm kernels' launches (rollout_launch's wide branch calls these)
+void rollout_wide_launch(int wpc, unsigned grid, hipStream_t st, const RolloutArgs& a, const DevModel* dm) {
+  if (wpc == 2)
+    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);
+  else
+    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), MPCR_W_DYN_LDS, st, a, dm);
+}
+hipError_t rollout_wide_occupancy(int* info) {
+  const void* k = reinterpret_cast<const void*>(&rollout_kernel<32, 32, 72, true>);
+  int blocks = 0;
+  hipFuncAttributes fa;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, WAVE, MPCR_W_DYN_LDS);
+  if (e != hipSuccess) return e;
+  e = hipFuncGetAttributes(&fa, k);
+  if (e != hipSuccess) return e;
+  info[0] = blocks;
+  info[1] = (int)fa.sharedSizeBytes;
+  info[2] = fa.numRegs;
+  return hipSuccess;
+}
+#endif
+
+#if MPCR_TU != 2
 // batches up to this many candidates run the narrow variant with two waves
 // per candidate (MPCR_WPC2_MAX_N overrides; 0 disables): below one
 // candidate per SIMD pair the second wave of a SIMD is otherwise idle
@@ -4411,21 +4462,6 @@ static int wpc2_max_n() { return g_wpc2_max_n.load(std::memory_order_relaxed); }
 int rollout_set_wpc2_max_n(int n) {
   return n >= 0 ? g_wpc2_max_n.exchange(n) : wpc2_max_n();
 }
-
-// Dual-arm batches up to min(this, the narrow threshold above) run two waves
-// per candidate too (rollout_kernel<32, 32, 72, true, 2>: collision, the MPR
-// flush and the manifolds beside the dynamics).  Its 29 KB image and 235
-// VGPRs leave 4 blocks per CU, so the default is 4 x 256 CUs: every candidate
-// resident in one round (measured on MI355X, H = 100: 1024 candidates 22.6 ->
-// 21.2 ms; 2048 would take two rounds, 24.5 -> 46.3 ms).  Bitwise the one-wave
-// results.  MPCR_WPC2W_MAX_N overrides.
-#ifndef MPCR_W_WPC2
-#define MPCR_W_WPC2 1
-#endif
-// extra dynamic LDS per one-wave dual-arm block (occupancy experiments only)
-#ifndef MPCR_W_DYN_LDS
-#define MPCR_W_DYN_LDS 0
-#endif
 #if MPCR_W_WPC2
 static const int g_wpc2w_max_n = env_int("MPCR_WPC2W_MAX_N", 1024);
 static int wpc2w_max_n() { return min(g_wpc2w_max_n, wpc2_max_n()); }
@@ -4483,7 +4519,7 @@ void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsign
   int G = 1;
 #if MPCR_W_WPC2
   if (wide && (int)grid <= wpc2w_max_n())
-    hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true, 2>), dim3(grid), dim3(2 * WAVE), 0, st, a, dm);
+    rollout_wide_launch(2, grid, st, a, dm);
   else
 #endif
   if (wide) {
@@ -4503,7 +4539,7 @@ void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsign
         for (int t0 = 0; t0 < a.H; t0 += a.seg) {
           ga.t0 = t0;
           ga.t1 = min(a.H, t0 + a.seg);
-          hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(ng), dim3(WAVE), MPCR_W_DYN_LDS, gs, ga, dm);
+          rollout_wide_launch(1, ng, gs, ga, dm);
         }
       }
       if (G > 1)
@@ -4512,7 +4548,7 @@ void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsign
           (void)hipStreamWaitEvent(st, gev[1 + g], 0);
         }
     } else {
-      hipLaunchKernelGGL((rollout_kernel<32, 32, 72, true>), dim3(grid), dim3(WAVE), MPCR_W_DYN_LDS, st, a, dm);
+      rollout_wide_launch(1, grid, st, a, dm);
     }
   } else {
     if constexpr (SmemN::CPW == 1) {
@@ -4527,20 +4563,18 @@ void rollout_launch(bool wide, const RolloutArgs& a0, const DevModel* dm, unsign
 }
 
 hipError_t rollout_occupancy(int* info, size_t dyn_lds) {
-  const void* k[2] = {reinterpret_cast<const void*>(&rollout_kernel<16, 16, 24, false>),
-                      reinterpret_cast<const void*>(&rollout_kernel<32, 32, 72, true>)};
-  for (int v = 0; v < 2; v++) {
-    int blocks = 0;
-    hipFuncAttributes fa;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k[v], WAVE, v == 0 ? dyn_lds : MPCR_W_DYN_LDS);
-    if (e != hipSuccess) return e;
-    e = hipFuncGetAttributes(&fa, k[v]);
-    if (e != hipSuccess) return e;
-    info[3 * v] = blocks;
-    info[3 * v + 1] = (int)fa.sharedSizeBytes;
-    info[3 * v + 2] = fa.numRegs;
-  }
-  return hipSuccess;
+  const void* k = reinterpret_cast<const void*>(&rollout_kernel<16, 16, 24, false>);
+  int blocks = 0;
+  hipFuncAttributes fa;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, WAVE, dyn_lds);
+  if (e != hipSuccess) return e;
+  e = hipFuncGetAttributes(&fa, k);
+  if (e != hipSuccess) return e;
+  info[0] = blocks;
+  info[1] = (int)fa.sharedSizeBytes;
+  info[2] = fa.numRegs;
+  return rollout_wide_occupancy(info + 3);
 }
+#endif  // MPCR_TU != 2
 
 }  // namespace mpcr
