@@ -20,15 +20,15 @@ and sequential: a different decomposition from the kernel's) and counts
 how often fp32 arithmetic alone moves a well-conditioned candidate by 1e-4.
 Round 4 traced the dual arm's excess of probe F over probe B to the line
 search's fp32 bookkeeping and to MPR-seeded SAT candidates of deep pairs and
-fixed both (84 -> 28 on the C4 shard); what remains is the fp32 step's own
-error, ~7e-7 of |qacc| per step on the GPU and in the fp32 build alike
-(tools/step_errors.py), about 3x the state perturbation probe B applies, so
-probe B alone under-counts an fp32 evaluation.  Then
+fixed both (84 -> 21 on the C4 shard), and compiled the dual-arm kernels
+without fast math, which brought the GPU below probe F and inside probe B's
+count (C4 shard 8 against probe B's 5 + 3 sigma = 11.7).
+Probe F is reported (probe_f_well_miss, well_miss_allowed_with_probe_f),
+not allowed.  Then
 
 * well-conditioned candidates (probe A moves the cost < TOL / 10, no masked
   slot within 1e-5 m of zero): the GPU may miss 1e-4 on no more of them
-  than probe B or probe F (the fp32 build, now the same mixed-precision
-  algorithm as the kernel) does, up to 3 binomial sigma;
+  than probe B does, up to 3 binomial sigma;
 * all candidates: no more misses than probe A has against the oracle, up to
   3 binomial sigma + 1 %;
 * median error at fp32 level;
@@ -121,10 +121,14 @@ def check(m, g_cost, o, sens, label="", strict_well=True):
                  probe_f_well_miss=int((well & (pf >= TOL)).sum()),
                  max_rel_well=float(rel[well].max()) if well.any() else 0.0,
                  max_rel_well_probe_f=float(pf[well].max()) if well.any() else 0.0)
-    bw = max(stats["probe_b_well_miss"], stats["probe_f_well_miss"]) / max(nw, 1)
+    # the allowance is probe B's count + 3 binomial sigma (round 4: probe F,
+    # the fp32 restatement, is reported beside it, no longer allowed -- the
+    # dual-arm kernels without fast math brought the C4 shard inside probe B)
+    bw = stats["probe_b_well_miss"] / max(nw, 1)
     stats["well_miss_allowed"] = float((bw + _sigma3(bw, nw)) * max(nw, 1))
-    stats["well_miss_allowed_probe_b_only"] = float(
-        (stats["probe_b_well_miss"] / max(nw, 1) + _sigma3(stats["probe_b_well_miss"] / max(nw, 1), nw)) * max(nw, 1))
+    stats["well_miss_allowed_probe_b_only"] = stats["well_miss_allowed"]
+    bf = max(stats["probe_b_well_miss"], stats["probe_f_well_miss"]) / max(nw, 1)
+    stats["well_miss_allowed_with_probe_f"] = float((bf + _sigma3(bf, nw)) * max(nw, 1))
     ig, io = int(np.argmin(g)), int(np.argmin(oc))
     ug, uo = max(TOL, sens[ig], pb[ig]), max(TOL, sens[io], pb[io])
     stats.update(sel_gpu=ig, sel_oracle=io, sel_rel=float(rel[ig]), sel_gap=float((oc[ig] - oc[io]) / abs(oc[io])),
@@ -205,7 +209,7 @@ def check_components(m, g_cost4, o, label="", g_slots=None, strict=True):
                   probe_b_well_miss=int((well & (pb >= TOL)).sum()), probe_f_well_miss=int((well & (pf >= TOL)).sum()),
                   max_rel_well=float(rel[well].max()) if well.any() else 0.0,
                   max_rel_well_probe_f=float(pf[well].max()) if well.any() else 0.0)
-        bw = max(st["probe_b_well_miss"], st["probe_f_well_miss"]) / max(nw, 1)
+        bw = st["probe_b_well_miss"] / max(nw, 1)  # probe B only (probe F reported)
         st["well_miss_allowed"] = float((bw + _sigma3(bw, nw)) * max(nw, 1))
         out[name] = st
     bad = np.zeros(0, int)
