@@ -15,9 +15,14 @@ iterations before timing.
 
 Scaling: --scaling weak (default): every rank owns --n candidates (N x 4096
 in total); --scaling strong: --n is the global batch, split over the ranks
-(C3's 4096 x 50 on 1..8 GPUs).
+(C3's 4096 x 50 on 1..8 GPUs).  The default line (C3, weak) also carries two
+sub-records measured by the same ranks in the same run: "strong" (C3's 4096
+x 50 global batch split over the ranks) and "c5" (BASELINE configs[4]: the
+closed-loop dual-arm MPC tick, 3 CEM iterations over a global 8192 x 50 batch
+split over the ranks, graph replay) -- the strong-scaling curves beside the
+weak one.  --config c5 makes the C5 tick the line itself.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4] [--scaling strong]
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5] [--scaling strong] [--no-sub]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 
@@ -52,6 +57,12 @@ CONFIGS = {
     "c4": dict(model="dual_arm", n=4096, H=100, exchange="elite",
                desc="dual-arm gripper scene (implicitfast, 14 actuators, connect equalities, convex-hull "
                     "meshes), Newton(100 it, 50 ls); C4 = 8 GPUs x 4096, elite exchange per step"),
+    # C5: a closed-loop MPC tick = compute_cem (3 CEM iterations over the GLOBAL
+    # 8192-candidate batch split over the ranks, graph replay) + the plant step
+    "c5": dict(model="dual_arm", n=8192, H=50, exchange="elite", iters=3,
+               desc="closed-loop receding-horizon MPC tick on the dual-arm scene: compute_cem with 3 CEM "
+                    "iterations (factor, MVN sample + projection, rollout + cost, elites, mean/cov) over a "
+                    "global 8192-candidate batch split over the ranks, HIP-graph replay, + the plant step"),
 }
 
 
@@ -114,9 +125,14 @@ def pmc_valu(path, n, H, flops_step, dispatches=1):
     if "SQ_INSTS_VALU" not in c:
         return None
     insts = float(np.mean(c["SQ_INSTS_VALU"])) * dispatches
-    waves = float(np.mean(c.get("SQ_WAVES", [n]))) * dispatches
+    wpd = float(np.mean(c.get("SQ_WAVES", [n])))
     per = insts / (n * H)
-    rec = {"valu_insts_per_candidate_step": round(per, 1), "waves_per_candidate": round(waves / n, 2),
+    #  waves per candidate *per call* summed over a segmented
+    # call's dispatches (a 7-step segment is one wave per candidate), and the
+    # waves of one dispatch, reported apart: round 4's "waves_per_candidate"
+    # meant the former for segmented calls and waves per candidate otherwise
+    rec = {"valu_insts_per_candidate_step": round(per, 1), "waves_per_candidate_per_call": round(wpd * dispatches / n, 2),
+           "waves_per_dispatch": round(wpd, 1), "dispatches_per_call": dispatches,
            "lane_flop_efficiency": round(flops_step / (64.0 * per), 4), "source": os.path.relpath(path, ROOT)}
     if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
         # SQ_ACTIVE_INST_VALU counts quad-cycles; GRBM_GUI_ACTIVE is summed over
@@ -261,6 +277,250 @@ def committed_counters(kind, sfx):
     return path, "committed 1-GPU profile of this build (" + os.path.relpath(path, ROOT) + ")"
 
 
+def synthetic_xi(n, H, seed):
+    """The bench's synthetic candidates: xi ~ N(0, 10.003 I), 10-iteration ADMM
+    projection (host, before any timing)."""
+    import torch
+
+    from manipulator_mujoco_amd import basis
+    from manipulator_mujoco_amd.projection import ProjectionFilter
+    _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
+    proj = ProjectionFilter(P, Pd, Pdd, 6, torch.device("cpu"))
+    rng = np.random.default_rng(seed)
+    return proj(torch.tensor(rng.normal(0, np.sqrt(10.003), (n, 66)).astype(np.float32)),
+                proj.boundary(Q0, np.zeros(6), np.zeros(6), n), 10)
+
+
+def _timed(step, steps, warmup, world, dev):
+    """warmup untimed steps, then `steps` timed between barrier + synchronize
+    on both sides; (wall seconds, median per-step ms of the HIP events) as the
+    max over ranks."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kms = [a.elapsed_time(b) for a, b in events]
+    t = torch.tensor([elapsed, float(np.median(kms))], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]), float(t[1]), kms
+
+
+def strong_subrecord(eng, dev, rank, world, H, steps, warmup, n_global=4096):
+    """C3's fixed global batch (4096 x 50, BASELINE configs[2]) split over the
+    ranks in the same run: the strong-scaling reading of
+    the multi-GPU line beside its weak one.  Same candidates as
+    `--scaling strong` (the global draw, this rank's rows), selection by the
+    8-byte MIN all-reduce of the best key."""
+    import torch
+
+    from manipulator_mujoco_amd import dist as md
+    from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI
+    lo, hi = md.shard(n_global, rank, world)
+    n = hi - lo
+    xi = synthetic_xi(n_global, H, 20250629 + 3)[lo:hi].contiguous().to(dev)
+    cost4 = torch.empty((n, 4), dtype=torch.float32, device=dev)
+    theta = torch.empty((n, 6 * H), dtype=torch.float32, device=dev)
+    thetadot = torch.empty((n, 6 * H), dtype=torch.float32, device=dev)
+    key = torch.empty(1, dtype=torch.int64, device=dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        eng.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, cost4=cost4, theta=theta, thetadot=thetadot,
+                         best_key=key, index_base=lo)
+        if ev is not None:
+            ev[1].record()
+        if world > 1:
+            md.allreduce_min_key(key)
+
+    elapsed, kern_ms, _ = _timed(step, steps, warmup, world, dev)
+    idx, best = md.decode_key(int(key.item()))
+    return {"scaling": "strong", "workload": f"C3 scene_mjx, {n_global} candidates x {H} steps in total, split "
+                                             f"over {world} GPU(s)",
+            "global_batch": n_global, "candidates_per_gpu": n, "steps": steps, "warmup": warmup,
+            "value": round(n_global * steps / elapsed, 1), "unit": "rollouts/s",
+            "ms_per_step": round(1e3 * elapsed / steps, 4), "kernel_ms": round(kern_ms, 4),
+            "best": {"index": idx, "cost": best}}
+
+
+def c5_run(rank, world, local, dev, n_global, H, iters, ticks, warmup, capture_exchange):
+    """C5 (BASELINE configs[4]): closed-loop MPC ticks on the dual-arm scene.
+    A tick = compute_cem (SBP/mjx_planner.py:364-406: `iters` CEM iterations
+    over the global batch, each rank its n_global / world share, sampling
+    keyed by the global index, elites exchanged; the iterations replayed from
+    HIP graphs) + the plant step with the mean of best_vels[1:H-2]
+    (SBP/mpc_planner.py:151-233, headless).  Returns the timing and, for the
+    roofline, the rollout call timed eagerly on the last tick's samples."""
+    import torch
+    import torch.distributed as dist
+
+    from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Plant
+    from manipulator_mujoco_amd.planner import cem_planner
+    p = cem_planner(num_dof=6, num_batch=n_global, num_steps=H, timestep=0.05, maxiter_cem=iters, num_elite=0.05,
+                    w_pos=W[0], w_rot=W[1], w_col=W[2], maxiter_projection=10, model_path="dual_arm", device=local,
+                    graph=True, group=dist.group.WORLD if world > 1 else None, return_rollouts=False,
+                    capture_exchange=capture_exchange, verbose=False)
+    plant = Plant(p.model, device=local)
+    qpos = plant.qpos.copy()
+    qpos[:6] = Q0
+    plant.set_state(qpos=qpos)
+    plant.forward()
+    state = {"mean": np.zeros(p.nvar), "out": None}
+
+    def tick(ev=None):
+        if ev is not None:
+            ev[0].record()
+        out = p.compute_cem(state["mean"], plant.qpos[:6], plant.qvel[:6], plant.qacc[:6], PT, QT)
+        state["mean"] = out[6]
+        plant.step(np.mean(out[4][1:H - 2], axis=0))
+        if ev is not None:
+            ev[1].record()
+        state["out"] = out
+
+    elapsed, tick_ms, _ = _timed(tick, ticks, warmup, world, dev)
+    # the dominant kernel: the rank's rollout call on the last iteration's
+    # samples, eagerly, HIP events on its stream (graph replays cannot be split)
+    n = p.n_local
+    st = torch.zeros(n, dtype=torch.int32, device=dev)
+    kms = []
+    for k in range(ticks + 1):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        p.engine.rollout_cost_dp(p._xf, MPCR_LAYOUT_XI, p._par, p._costs[0], theta=p._theta[0],
+                                 thetadot=p._thetadot[0], index_base=p.index_base, status=st)
+        b.record()
+        torch.cuda.synchronize()
+        if k:
+            kms.append(a.elapsed_time(b))
+    out = state["out"]
+    nefc_mean = float((st >> 10).double().mean().item()) / H
+    return {"elapsed": elapsed, "tick_ms": tick_ms, "kernel_ms": float(np.median(kms)), "n_local": n,
+            "nefc_mean": nefc_mean, "model": p.model, "engine": p.engine,
+            "best_cost": [float(x) for x in np.asarray(out[0])],
+            "best_cost_grc": [float(out[1]), float(out[2]), float(out[3])],
+            "eef_dist": float(np.linalg.norm(plant.site_xpos_tcp - np.asarray(PT))),
+            "capture": "the whole tick, RCCL all-gathers included" if (world > 1 and capture_exchange and
+                                                                        dist.get_backend() == "nccl")
+            else ("each CEM iteration's device segment; the elite exchange eager between replays" if world > 1
+                  else "the whole tick (one rank: no exchange)")}
+
+
+def c5_subrecord(rank, world, local, dev, steps, warmup):
+    """C5 beside the default line: the global 8192 x 50 x 3
+    tick over however many ranks this run has -- the strong-scaling curve the
+    north star's ">= 6x further at 8 GPUs" is about.  The exchange runs
+    eagerly between graph replays here (the RCCL-captured tick is
+    `--config c5 --c5-capture-exchange`)."""
+    cfg = CONFIGS["c5"]
+    r = c5_run(rank, world, local, dev, cfg["n"], cfg["H"], cfg["iters"], steps, warmup, capture_exchange=False)
+    return {"scaling": "strong", "workload": f"C5 dual_arm closed-loop tick: {cfg['iters']} CEM iterations over "
+                                             f"{cfg['n']} candidates x {cfg['H']} steps in total, split over "
+                                             f"{world} GPU(s), + the plant step",
+            "global_batch": cfg["n"], "candidates_per_gpu": r["n_local"], "ticks": steps, "warmup": warmup,
+            "value": round(cfg["n"] * cfg["iters"] * steps / r["elapsed"], 1), "unit": "rollouts/s",
+            "ms_per_tick": round(1e3 * r["elapsed"] / steps, 3), "rollout_kernel_ms": round(r["kernel_ms"], 3),
+            "best_cost": r["best_cost"], "graph": r["capture"]}
+
+
+def init_device(args, world, local):
+    """This rank's GPU (local rank; with --backend gloo ranks may share one)
+    and, for world > 1, the process group."""
+    import torch
+    import torch.distributed as dist
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"local rank {local} has no GPU of its own ({ndev} visible); use --backend gloo to share")
+    gpu = local % max(ndev, 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    backend = None
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        backend = dist.get_backend()
+    return gpu, dev, ndev, backend
+
+
+def main_c5(args, cfg):
+    """--config c5: the closed-loop tick as the line (strong scaling: the
+    global batch is fixed, split over the ranks)."""
+    import torch.distributed as dist
+
+    from manipulator_mujoco_amd import basis, models
+    from manipulator_mujoco_amd import dist as md
+    rank, world, local = md.env_rank()
+    n_global, H, iters = args.n or cfg["n"], args.horizon or cfg["H"], cfg["iters"]
+    cpu_rec = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the scalar C restatement on host cores, a bounded sample of the
+        # workload's rollouts (the dual arm is ~100x C3's CPU cost per rollout)
+        usable, ncpu, model, aff, quota = _host_cpu()
+        threads = args.cpu_threads or usable
+        sample = synthetic_xi(args.cpu_sample or 256, H, 20250629 + 5).numpy()
+        m = models.load(cfg["model"], 0.05)
+        _, _, Pd, _ = basis.planner_basis(H, 0.05)
+        v32, reps = cpu_baseline(m, sample, H, Pd, threads, reps=3, precision="fp32")
+        cpu_rec = {"value": round(v32, 1), "unit": "rollouts/s", "cores": threads, "kind": "port",
+                   "sample": f"{sample.shape[0]} dual-arm candidates x {H} steps (rollout + cost only, no CEM "
+                             f"step); fp32 scalar C restatement (oracle/oracle_f32.c), {threads} threads, median "
+                             f"of {len(reps)} repetitions",
+                   "reps": reps, "host": {"usable_cores": usable, "affinity_cores": aff, "cgroup_cpu_quota": quota,
+                                          "nproc": ncpu, "cpu_model": model}}
+    gpu, dev, ndev, backend = init_device(args, world, local)
+    r = c5_run(rank, world, local, dev, n_global, H, iters, args.steps, args.warmup, args.c5_capture_exchange)
+    if rank == 0:
+        coll = {"nccl": "RCCL (xGMI)", "gloo": "gloo (host-staged)"}.get(backend, str(backend))
+        fps = flops_per_step(r["model"], r["nefc_mean"], "dual_arm")
+        achieved_tf = fps * H * r["n_local"] / (r["kernel_ms"] * 1e-3) / 1e12
+        hbm_launch = r["n_local"] * (66 * 4 + 16 + 2 * 6 * H * 4 + 4)
+        rec = {
+            "metric": METRIC, "value": round(n_global * iters * args.steps / r["elapsed"], 1), "unit": "rollouts/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * r["elapsed"] / args.steps, 4), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic closed loop (CEM from a zero mean, Philox samples keyed by the global candidate "
+                    "index; target (-0.3, -0.3, 0.5), qt (0, 1, 0, 0))",
+            "config": {"workload": f"C5 {cfg['model']}: {cfg['desc']}; {n_global} x {H} x {iters} per tick",
+                       "global_batch": n_global, "candidates_per_gpu": r["n_local"], "horizon": H, "cem_iters": iters,
+                       "parallelism": f"dp{world} (candidate shards; elite exchange)", "world_size_seen": world,
+                       "backend": backend or "single process", "gpus_visible": ndev,
+                       "graph": r["capture"],
+                       "exchange": "none (one rank)" if world == 1 else
+                       f"local top-E + {coll} all-gather of (xi, cost) rows + global top-E per iteration; "
+                       f"best key MIN all-reduce + broadcast of the best row per tick"},
+            "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_F32_VALU_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_F32_VALU_TFLOPS, 5), "traffic": None,
+                         "traffic_source": "not profiled in this run", "kernel": "rollout_kernel",
+                         "kernel_ms": round(r["kernel_ms"], 4),
+                         "kernel_timing": "the rank's rollout call on the last tick's samples, eager, HIP events "
+                                          "(graph replays are timed whole)",
+                         "flops_per_step": fps, "hbm_algorithmic_bytes": hbm_launch},
+            "best": {"cost_per_iteration": r["best_cost"], "cost_grc": r["best_cost_grc"]},
+            "eef_dist_after": r["eef_dist"], "mean_constraint_rows": round(r["nefc_mean"], 2),
+        }
+        if cpu_rec is not None:
+            rec["cpu_baseline"] = cpu_rec
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -288,6 +548,10 @@ def main():
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="N > 1: nccl (= RCCL over xGMI, one GPU per rank) or gloo (host-staged; ranks may share "
                          "a GPU, device = local rank mod the visible GPUs: rehearses the multi-rank path on one GPU)")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="default line only: skip the strong (C3 4096 global) and C5 sub-records")
+    ap.add_argument("--c5-capture-exchange", action="store_true",
+                    help="c5: capture the RCCL elite all-gathers in the tick's graph (default: eager between replays)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -297,6 +561,8 @@ def main():
     if args.launch_selftest:
         return launch_selftest()
     cfg = CONFIGS[args.config]
+    if args.config == "c5":
+        return main_c5(args, cfg)
     args.model = args.model or cfg["model"]
     args.n = args.n or cfg["n"]
     args.horizon = args.horizon or cfg["H"]
@@ -309,7 +575,6 @@ def main():
     from manipulator_mujoco_amd import dist as md
     from manipulator_mujoco_amd.cem import topk
     from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Engine
-    from manipulator_mujoco_amd.projection import ProjectionFilter
 
     rank, world, local = md.env_rank()
 
@@ -321,14 +586,10 @@ def main():
         n, n_total, base = args.n, args.n * world, rank * args.n
     m = models.load(args.model, 0.05)
     _, P, Pd, Pdd = basis.planner_basis(H, 0.05)
-    cpu = torch.device("cpu")
-    proj = ProjectionFilter(P, Pd, Pdd, 6, cpu)
     # synthetic inputs, generated on the host (same bytes on every run); strong
     # scaling draws the global batch and takes this rank's rows
-    rng = np.random.default_rng(20250629 + 3 + (0 if args.scaling == "strong" else rank))
     n_draw = n_total if args.scaling == "strong" else n
-    xi_all = proj(torch.tensor(rng.normal(0, np.sqrt(10.003), (n_draw, 66)).astype(np.float32)),
-                  proj.boundary(Q0, np.zeros(6), np.zeros(6), n_draw), 10)
+    xi_all = synthetic_xi(n_draw, H, 20250629 + 3 + (0 if args.scaling == "strong" else rank))
     xi_host = xi_all[base:base + n] if args.scaling == "strong" else xi_all
     cpu_rec = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -362,19 +623,7 @@ def main():
                    "host": {"usable_cores": usable, "affinity_cores": aff, "cgroup_cpu_quota": quota, "nproc": ncpu,
                             "cpu_model": model}}
 
-    ndev = torch.cuda.device_count()
-    if args.backend == "nccl" and world > 1 and local >= ndev:
-        raise SystemExit(f"local rank {local} has no GPU of its own ({ndev} visible); use --backend gloo to share")
-    gpu = local % max(ndev, 1)
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    backend = None
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-        backend = dist.get_backend()
+    gpu, dev, ndev, backend = init_device(args, world, local)
     xi = xi_host.to(dev)
     eng = Engine(m, H, n, Pd, device=gpu)
     cost4 = torch.empty((n, 4), dtype=torch.float32, device=dev)
@@ -408,25 +657,7 @@ def main():
     for _ in range(args.warmup):
         step()
     elites["count"] = 0
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kms = [a.elapsed_time(b) for a, b in events]
-    kern_ms = float(np.median(kms))
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms, kms = _timed(step, args.steps, 0, world, dev)
     idx, best = md.decode_key(int(key.item()))
     trunc = int((status & 1).sum().item())
     nefc_mean = float((status >> 10).double().mean().item()) / H
@@ -440,6 +671,13 @@ def main():
         first = np.where(act.any(axis=1), act.argmax(axis=1), -1)
         contact = {"candidates_with_active_robot_contact": int(act.any(axis=1).sum()), "of": int(n),
                    "first_active_step_median": float(np.median(first[first >= 0])) if (first >= 0).any() else None}
+
+    # the default line (C3, weak) also carries the strong-scaling reading of
+    # the same ranks and the C5 tick
+    subs = {}
+    if args.config == "c3" and args.scaling == "weak" and args.n == cfg["n"] and not args.no_sub:
+        subs["strong"] = strong_subrecord(eng, dev, rank, world, H, args.steps, args.warmup)
+        subs["c5"] = c5_subrecord(rank, world, local, dev, min(args.steps, 5), 2)
 
     if rank == 0:
         coll = {"nccl": "RCCL (xGMI)", "gloo": "gloo (host-staged)"}.get(backend, str(backend))
@@ -510,6 +748,7 @@ def main():
             rec["contacts"] = contact
         if cpu_rec is not None:
             rec["cpu_baseline"] = cpu_rec
+        rec.update(subs)
         print(json.dumps(rec))
     if world > 1:
         dist.destroy_process_group()

@@ -52,7 +52,16 @@
 extern "C" {
 #endif
 
-#define MPCR_ABI_VERSION 1
+/* ABI version.  2 (round 4): the status word's max-rows field widened to 8
+   bits, so rows-summed moved from bit 8 to bit 10 (version 1: 6 bits << 2,
+   sum << 8).  Decode with the accessors below, not raw shifts. */
+#define MPCR_ABI_VERSION 2
+
+/* the per-candidate status word of mpcr_rollout_cost / _dp */
+#define MPCR_STATUS_TRUNCATED(s) ((s) & 1)                  /* constraint rows truncated  */
+#define MPCR_STATUS_NONFINITE(s) (((s) >> 1) & 1)           /* non-finite state           */
+#define MPCR_STATUS_MAX_ROWS(s) (((s) >> 2) & 255)          /* busiest step's rows (<= 255) */
+#define MPCR_STATUS_ROWS_SUM(s) ((unsigned)(s) >> 10)       /* rows summed over the horizon */
 
 enum {
   MPCR_OK = 0,

@@ -1355,13 +1355,13 @@ extern "C" int mpcr_rollout_trace(mpcr_engine* e, const float* input, int layout
 // diagnostic build only: per-phase s_memtime cycles summed over all waves
 extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layout, int n, const double* q0,
                                     const float* w, const float* ptgt, const float* qtgt,
-                                    unsigned long long* phases16 /* 32 slots */) {
+                                    unsigned long long* phases16 /* 64 slots: wave 0, wave 1 (WPC = 2) */) {
   HIPCHK(hipSetDevice(e->device));
   const int nc = e->host.nctrl;
   const size_t cols = layout == MPCR_LAYOUT_XI ? (size_t)nc * e->nbasis : (size_t)nc * e->H;
   unsigned long long* d_prof = nullptr;
-  HIPCHK(hipMalloc(&d_prof, 32 * sizeof(unsigned long long)));
-  HIPCHK(hipMemset(d_prof, 0, 32 * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&d_prof, 64 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(d_prof, 0, 64 * sizeof(unsigned long long)));
   e->dev.prof = d_prof;  // wave-level counters for this launch only
   HIPCHK(hipMemcpy(e->d_model, &e->dev, sizeof(DevModel), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(e->d_in, input, sizeof(float) * n * cols, hipMemcpyHostToDevice));
@@ -1378,7 +1378,7 @@ extern "C" int mpcr_rollout_profile(mpcr_engine* e, const float* input, int layo
   fill_par(a.par, nc, q0, w, ptgt, qtgt);
   rollout_launch(e->wide, a, (const DevModel*)e->d_model, n, MPCR_N_DYN_LDS, nullptr);
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(phases16, d_prof, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(phases16, d_prof, 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   e->dev.prof = nullptr;
   HIPCHK(hipMemcpy(e->d_model, &e->dev, sizeof(DevModel), hipMemcpyHostToDevice));
   (void)hipFree(d_prof);

@@ -32,9 +32,10 @@ namespace mpcr {
     prof_acc[i] += now_ - prof_last;                          \
     prof_last = now_;                                         \
   } while (0)
+// (a candidate's second wave, WPC = 2, into slots 32..63: per-wave critical paths)
 #define PROF_FLUSH                                                          \
   if (lane == 0 && args.prof)                                               \
-    for (int i_ = 0; i_ < 32; i_++) atomicAdd(&args.prof[i_], prof_acc[i_]);
+    for (int i_ = 0; i_ < 32; i_++) atomicAdd(&args.prof[i_ + 32 * (threadIdx.x >> 6)], prof_acc[i_]);
 // wave-level event counter (first active lane adds 1; -DMPCR_PROFILE_COUNTS
 // only: the shared atomics distort the cycle shares)
 #ifdef MPCR_PROFILE_COUNTS
@@ -50,7 +51,7 @@ namespace mpcr {
 #define PSTAMP(m, i)                                                                       \
   do {                                                                                     \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();                          \
-    if ((m)->prof && (int)__lane_id() == 0) atomicAdd((m)->prof + (i), now_ - pst_);       \
+    if ((m)->prof && (int)__lane_id() == 0) atomicAdd((m)->prof + (i) + 32 * (threadIdx.x >> 6), now_ - pst_); \
     pst_ = now_;                                                                           \
   } while (0)
 #else
@@ -1273,18 +1274,22 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
       mxa = fmaxf(mxa, wmax(sp));
     }
     sync();
+    // the key 2 f + side keeps the side with the face: two geoms of one mesh
+    // share their face range, and on equal faces g1's wins, the
+    // oracle's first-listed candidate
     float fmin = 3e38f;
 #pragma unroll 1
     for (int b0 = 0; b0 < nf; b0 += WAVE) {
       const int k = b0 + lane;
       const bool nb = k < nf && near_max(s.satsep[k], mxa);
-      const int f = k >= nf1 ? fa2 + k - nf1 : fa1 + k;
-      fmin = fminf(fmin, -wmax(nb ? -(float)f : -3e38f));
+      const int key = k >= nf1 ? 2 * (fa2 + k - nf1) + 1 : 2 * (fa1 + k);
+      fmin = fminf(fmin, -wmax(nb ? -(float)key : -3e38f));
     }
     found = fmin < 3e38f;
     if (found) {
-      fr = (int)fmin;
-      rtwo = !(fr >= fa1 && fr < fa1 + nf1);
+      const int key = (int)fmin;
+      fr = key >> 1;
+      rtwo = (key & 1) != 0;
       bsep = s.satsep[rtwo ? nf1 + fr - fa2 : fr - fa1];
     }
     sync();  // satsep shares bytes with the clip buffer below

@@ -74,12 +74,16 @@ class cem_planner:  # noqa: N801 (reference name)
     return_rollouts     False: the 9-tuple's thetadot/theta (iters x N x 6H,
                         what the closed loop discards) are returned as None
                         instead of being copied to the host every tick
+    capture_exchange    with graph=True and an RCCL group, capture the elite
+                        all-gathers in the tick's graph (default); False
+                        captures each iteration's device segment and runs the
+                        exchange eagerly between the replays (as with gloo)
     """
 
     def __init__(self, num_dof=None, num_batch=None, num_steps=None, timestep=None, maxiter_cem=None,
                  num_elite=None, w_pos=None, w_rot=None, w_col=None, maxiter_projection=None, *,
                  model_path=None, device=None, seed=0, elite_from_filtered=False, graph=False, group=None,
-                 gather_rollouts=False, return_rollouts=True, verbose=True):
+                 gather_rollouts=False, return_rollouts=True, capture_exchange=True, verbose=True):
         import torch
         import torch.distributed as tdist
 
@@ -99,6 +103,7 @@ class cem_planner:  # noqa: N801 (reference name)
         self.graph = bool(graph)
         self.gather_rollouts = bool(gather_rollouts)
         self.return_rollouts = bool(return_rollouts)
+        self.capture_exchange = bool(capture_exchange)
         # CEM constants (:84-97)
         self.v_max, self.a_max, self.p_max = 0.8, 1.8, np.pi
         self.alpha_mean, self.alpha_cov, self.lamda = 0.6, 0.6, 10.0
@@ -215,7 +220,7 @@ class cem_planner:  # noqa: N801 (reference name)
             torch.cuda.current_stream(self.device).wait_stream(s)
             torch.cuda.synchronize(self.device)
             graphs = []
-            if not self.exchange or self._exchange_capturable():
+            if not self.exchange or (self.capture_exchange and self._exchange_capturable()):
                 # the whole tick in one graph; with an RCCL group the elite
                 # all-gathers are captured too (device buffers, stream-ordered)
                 g = torch.cuda.CUDAGraph()

@@ -328,6 +328,29 @@ def test_poly_manifold_clips_to_the_smaller_face(tmp_path):
         assert abs(dist + depth) < 1e-8 and abs(abs(n[2]) - 1) < 1e-12
 
 
+SHARED_MESH_DEEP = """
+    <body name="a" pos="0 0 0.2" euler="0.3 0 0"><freejoint/><geom name="a" type="mesh" mesh="cube"/></body>
+    <body name="b" pos="0.01 0 0.30454"><freejoint/><geom name="b" type="mesh" mesh="cube"/></body>"""
+
+
+def test_poly_manifold_deep_pair_of_one_mesh(tmp_path):
+    """Two geoms of one mesh share its face range (the compiler caches hulls
+    per mesh), 8 mm deep, so the all-face SAT runs: the winning axis is g2's
+    bottom face (b), not g1's face of the same index (the kernel
+    credited it to g1 and fell back to MPR's single contact).  The tilted
+    cube's top edge clipped to b's bottom face: two contacts, normal +z."""
+    m = _scene(tmp_path, SHARED_MESH_DEEP)
+    ga, gb = m.names["geom"].index("a"), m.names["geom"].index("b")
+    assert m.geom_faceadr[ga] == m.geom_faceadr[gb] >= 0
+    c = _active(m)
+    ab = c.get(("a", "b")) or c.get(("b", "a"))
+    assert ab is not None and len(ab) == 2
+    depth = 0.05 * (np.cos(0.3) + np.sin(0.3)) + 0.05 - (0.30454 - 0.2)
+    for dist, _, n in ab:
+        assert abs(dist + depth) < 1e-6 and abs(abs(n[2]) - 1) < 1e-12
+    assert sorted(round(p[0], 6) for _, p, _ in ab) == [-0.04, 0.05]  # the edge clipped to b's face
+
+
 def test_plane_cylinder_four_points(tmp_path):
     """Plane-cylinder (MuJoCo's mjc_PlaneCylinder restated): an upright
     cylinder 3 mm into the floor gets the deepest rim point, the two rim points

@@ -70,3 +70,38 @@ def test_bench_self_launch_two_ranks_equal_one_gpu():
     assert two["best"] == one["best"]
     assert two["elites"]["cost_sum"] == one["elites"]["cost_sum"]
     assert two["elites"]["first"] == one["elites"]["first"]
+
+
+SUB = ["--config", "c3", "--candidates", "4096", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+       "--no-contact-report"]
+
+
+def test_bench_default_line_carries_strong_and_c5_at_two_ranks():
+    """The default line's sub-records: at world 2 (gloo,
+    two ranks sharing the box's GPU) the C3 strong reading (4096 global, 2048
+    per rank) selects the same best candidate as one process, and the C5 tick
+    (8192 global, 4096 per rank, 3 CEM iterations, graph replay with the
+    exchange between replays) ends with the same per-iteration best costs."""
+    one = _run([sys.executable, "bench.py"] + SUB)
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                "--backend", "gloo"] + SUB)
+    for rec, w in ((one, 1), (two, 2)):
+        st, c5 = rec["strong"], rec["c5"]
+        assert st["scaling"] == "strong" and st["global_batch"] == 4096 and st["candidates_per_gpu"] == 4096 // w
+        assert c5["scaling"] == "strong" and c5["global_batch"] == 8192 and c5["candidates_per_gpu"] == 8192 // w
+        assert st["value"] > 0 and c5["value"] > 0 and len(c5["best_cost"]) == 3
+    assert two["strong"]["best"] == one["strong"]["best"]
+    # weak: each rank's own 4096 (rank 0's draw is the strong global batch)
+    assert one["strong"]["best"] == one["best"]
+    assert two["c5"]["best_cost"] == one["c5"]["best_cost"], (one["c5"], two["c5"])
+
+
+def test_bench_c5_line():
+    """--config c5: the closed-loop tick as the line (strong scaling), the
+    rollout kernel's roofline from an eager call of the rank's share."""
+    rec = _run([sys.executable, "bench.py", "--config", "c5", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"])
+    assert rec["scaling"] == "strong" and rec["config"]["global_batch"] == 8192
+    assert rec["config"]["cem_iters"] == 3 and len(rec["best"]["cost_per_iteration"]) == 3
+    assert rec["roofline"]["kernel_ms"] > 0 and 0 < rec["roofline"]["frac"] < 1
+    assert abs(rec["value"] - 8192 * 3 * 2 / (2 * rec["ms_per_step"] * 1e-3)) < 0.01 * rec["value"]

@@ -126,6 +126,11 @@ SYNTHETIC = {
     <body name="y" pos="0 0 0.097" euler="0.05 0 0"><freejoint/><geom name="y" type="cylinder" size="0.05 0.1"/></body>
     <body name="p" pos="0.5 0 0.015" euler="0 1.5 0"><freejoint/><geom name="p" type="capsule" size="0.02 0.1"/></body>
     <body name="q" pos="0.05 0.3 0.05"><freejoint/><geom name="q" type="cylinder" size="0.03 0.06"/></body>""",
+    # two geoms of one mesh (one face range), 8 mm deep: the all-face SAT's
+    # winner is g2's face (ADVICE r4; oracle pinned in tests/test_dual_arm.py)
+    "shared_mesh_deep": """
+    <body name="a" pos="0 0 0.2" euler="0.3 0 0"><freejoint/><geom name="a" type="mesh" mesh="cube"/></body>
+    <body name="b" pos="0.01 0 0.30454"><freejoint/><geom name="b" type="mesh" mesh="cube"/></body>""",
 }
 
 

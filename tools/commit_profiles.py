@@ -2,10 +2,13 @@
 profiles/ and record, in profiles/<tag>_pmc_manifest.json, the libmpcr.so
 source hash of the build they were taken from (manipulator_mujoco_amd.build
 .source_hash) -- bench.py attaches committed counters only to a run of that
-same build.  Run here after the GPU session, with the sources the
-session ran unchanged.
+same build.  The hash is the one the session itself recorded
+(gpurun_out/<tag>/source_hash.txt, tools/gpu_session_r05.sh); the script
+refuses to commit when the checkout no longer hashes to it (an
+edit between the session and this script would attach the counters to a
+build they were not taken from).
 
-    python tools/commit_profiles.py r04
+    python tools/commit_profiles.py r05
 """
 import json
 import os
@@ -25,11 +28,17 @@ PASSES = {"pmc1": "pmc_rollout_fetch", "pmc2": "pmc_rollout_write", "pmc3": "pmc
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else "r04"
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r05"
     src = os.path.join(ROOT, "gpurun_out", tag)
     man_path = os.path.join(ROOT, "profiles", f"{tag}_pmc_manifest.json")
     man = json.load(open(man_path)) if os.path.exists(man_path) else {}
     h = build.source_hash()
+    hf = os.path.join(src, "source_hash.txt")
+    if not os.path.exists(hf):
+        sys.exit(f"{hf} missing: the session did not record the build it ran")
+    ran = open(hf).read().strip()
+    if ran != h:
+        sys.exit(f"the session ran build {ran}, the checkout is {h}: not committing its counters")
     merged = {}
     for d, name in PASSES.items():
         f = os.path.join(src, d, "run_counter_collection.csv")

@@ -47,38 +47,53 @@ def main():
         xi = np.ascontiguousarray(xi[[int(i) for i in os.environ["SUBSET"].split(",")]])
         n = xi.shape[0]
     e = Engine(m, H, n, Pd)
-    ph = (ctypes.c_ulonglong * 32)()
+    ph = (ctypes.c_ulonglong * 64)()
     f = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
     w, pt, qt = np.array([20, 3, 80.]), np.array([-0.3, -0.3, 0.5]), np.array([0, 1, 0, 0.])
     for _ in range(2):
-        ph = (ctypes.c_ulonglong * 32)()
+        ph = (ctypes.c_ulonglong * 64)()
         _lib.check(lib.mpcr_rollout_profile(e.handle, xi.ctypes.data, MPCR_LAYOUT_XI, n,
                                             q0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), f(w), f(pt), f(qt), ph))
-    tot = sum(ph[:15]) + sum(ph[i] for i in EXTRA)
-    print(f"{name}: n={n} H={H} cycles/wave-step {tot / n / H:.0f}")
+    waves = [list(ph[:32])] + ([list(ph[32:64])] if any(ph[32:64]) else [])
     names = dict(enumerate(PHASES))
     names[7] = "coll: loop tail"
     names.update(EXTRA)
-    for i, p in names.items():
-        print(f"  {p:26s} {ph[i] / n / H:10.0f} cyc  {100 * ph[i] / tot:5.1f}%")
-    sub = {23: "support vertices", 24: "cone face scan", 25: "SAT support queries", 26: "incident face + polygons",
-           27: "clip", 28: "picks"}
-    if any(ph[i] for i in sub):  # inside the polyhedron manifold (wave level, atomics per stamp)
-        for i, p in sub.items():
-            print(f"    poly: {p:24s} {ph[i] / n / H:10.0f} cyc")
-    for i, p in COUNTS.items():
-        print(f"  {p:34s} {ph[i] / n / H:8.2f} per wave-step")
-    print(f"  Newton iterations per step: {(ph[15] & 0xFFFFFFFF) / n / H:.2f}, line-search passes per step: "
-          f"{(ph[15] >> 32) / n / H:.2f} (steps with constraints only)")
+    res = {"model": name, "n": n, "H": H, "waves_per_candidate": len(waves)}
+    for w_i, pw in enumerate(waves):
+        # two waves per candidate: wave 0 runs kinematics, dynamics, Newton; wave
+        # 1 the collision (and, with coll_rows, the constraint rows); the time a
+        # wave waits at a barrier lands in the stamp after it (wave 0: "geom/com/
+        # eef" waits for the previous step's collision, "constraint rows" / the
+        # rows stamp for this step's; wave 1: "geom/com/eef" for wave 0's
+        # Newton + kinematics)
+        tot = sum(pw[:15]) + sum(pw[i] for i in EXTRA)
+        tag = f" wave {w_i}" if len(waves) > 1 else ""
+        print(f"{name}{tag}: n={n} H={H} cycles/wave-step {tot / n / H:.0f}")
+        for i, p in names.items():
+            if pw[i]:
+                print(f"  {p:26s} {pw[i] / n / H:10.0f} cyc  {100 * pw[i] / tot:5.1f}%")
+        sub = {23: "support vertices", 24: "cone face scan", 25: "SAT support queries", 26: "incident face + polygons",
+               27: "clip", 28: "picks"}
+        if any(pw[i] for i in sub):  # inside the polyhedron manifold (wave level, atomics per stamp)
+            for i, p in sub.items():
+                print(f"    poly: {p:24s} {pw[i] / n / H:10.0f} cyc")
+        for i, p in COUNTS.items():
+            print(f"  {p:34s} {pw[i] / n / H:8.2f} per wave-step")
+        print(f"  Newton iterations per step: {(pw[15] & 0xFFFFFFFF) / n / H:.2f}, line-search passes per step: "
+              f"{(pw[15] >> 32) / n / H:.2f} (steps with constraints only)")
+        rec = {"cycles_per_wave_step": tot / n / H,
+               "phases": {p: {"cycles": pw[i] / n / H, "share": pw[i] / tot} for i, p in names.items()},
+               "counts": {p: pw[i] / n / H for i, p in COUNTS.items()},
+               "newton_iters_per_step": (pw[15] & 0xFFFFFFFF) / n / H,
+               "ls_passes_per_step": (pw[15] >> 32) / n / H}
+        if len(waves) == 1:
+            res.update(rec)
+        else:
+            res[f"wave{w_i}"] = rec
     if out:
         import json
         with open(out, "w") as fh:
-            json.dump({"model": name, "n": n, "H": H, "cycles_per_wave_step": tot / n / H,
-                       "phases": {p: {"cycles": ph[i] / n / H, "share": ph[i] / tot} for i, p in names.items()},
-                       "counts": {p: ph[i] / n / H for i, p in COUNTS.items()},
-                       "newton_iters_per_step": (ph[15] & 0xFFFFFFFF) / n / H,
-                       "ls_passes_per_step": (ph[15] >> 32) / n / H}, fh, indent=1)
-
+            json.dump(res, fh, indent=1)
 
 if __name__ == "__main__":
     main()
