@@ -625,6 +625,9 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
   d.coll_rows = m.npair <= WAVE;  // DevModel::coll_rows: a light collision phase
   for (int p = 0; p < m.npair; p++)
     if (m.pair_func[p] == MPCR_COL_BOX_BOX) d.coll_rows = 0;
+  d.cvx_joint = 1;  // DevModel::cvx_joint: no convex pair carries a cost slot
+  for (int p = d.cvx_base; p < m.npair; p++)
+    if (m.pair_slotadr[p] >= 0) d.cvx_joint = 0;
   if (m.nhullv > 32767) return fail(MPCR_EMODEL, "hull vertex table exceeds 16-bit hints");
   for (int p = 0; p < m.npair; p++) {
     int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];

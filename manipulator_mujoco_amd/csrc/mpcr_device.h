@@ -64,6 +64,10 @@ struct DevModel {
   // pairs, no wave-cooperative box-box pair -- measured: C2 0.955 -> 0.850 ms,
   // scene_mjx at 1024 / 2048 candidates 1.081 / 1.189 -> 1.093 / 1.207 ms)
   int coll_rows;
+  // dual-arm class, two waves per candidate: the convex flush deals its pairs
+  // over both waves (no convex pair has a cost slot, so no per-lane cost_c
+  // order is at stake; the contacts still go to the list in pair order)
+  int cvx_joint;
   float timestep, tolerance, ls_tolerance, meaninertia;
   float gravity[4];
   float tcp_pos[4];  // tcp site position in tcp_body frame

@@ -5,6 +5,7 @@
 // manipulator_mujoco_amd/build.py).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include <type_traits>
@@ -132,7 +133,10 @@ struct __align__(16) SmemT {
   static constexpr int LOG_NVW = NVW_ == 32 ? 5 : 4;
   static constexpr bool WIDE = NVW_ == 32;  // dual-arm class: equalities, actuators, convex hulls
   static constexpr int NQW = WIDE ? DX_NQ : MPCR_N_NQ, NEQP = WIDE ? DX_NEQ : 1, NACT = WIDE ? DX_NU : 1;
-  static constexpr int CVXN = WIDE ? 192 : 1;  // compacted convex-pair list
+  // compacted convex-pair list: room for every convex pair a model may have
+  // (the engine allows 512), so the collision phase flushes it once, at its
+  // end (round 5: the flush runs on both waves of a two-wave candidate)
+  static constexpr int CVXN = WIDE ? 512 : 1;
   static constexpr int NHINT = WIDE ? 512 : 1;  // hull-climb start per convex pair and side
   static constexpr int PMAXW = 2 * MPCR_FACE_MAXV + 2;  // clipped incident face: <= its vertices + one per side plane
   static constexpr int FRAMEW = WIDE ? 3 : 9;  // contact frame entries kept (the wide image recomputes the tangents)
@@ -212,6 +216,18 @@ struct __align__(16) SmemT {
     };
   };
 };
+// The polyhedron manifold's scratch (clip polygon, SAT separations) as its
+// own type: the LDS image's (polyw, satsep: the same layout inside the J
+// rows) or, for the dynamics wave of a two-wave candidate in the joint convex
+// flush, one in the dynamics region (dead from the mass-matrix solve to the
+// next step's kinematics), followed there by the flush's per-item contact
+// counts (jcnt, 2 x 64 items per round)
+template <int PMAXW_>
+struct PolyScratchT {
+  alignas(16) float polyw[2][PMAXW_][4];
+  float satsep[POLY_ALLF];
+};
+
 // The two variants: single-arm scenes (nv <= 16) and the dual-arm class.
 // Single-arm image: 96 constraint rows of which the first 40 keep their J row
 // in LDS (stride 16) and the rest in a per-candidate HBM slab (RolloutArgs::jx;
@@ -264,6 +280,10 @@ using SmemW = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, M
 // dynamics scratch beside the contact / constraint arrays
 using SmemW2 = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT, true>;
 static_assert(sizeof(SmemW2) <= 152448 / 4, "two-wave dual-arm image: 4 blocks per CU");
+static_assert(sizeof(PolyScratchT<SmemW2::PMAXW>) + 2 * WAVE * 4 <= SmemW2::DYN_FLOATS * 4,
+              "the dynamics wave's manifold scratch and the flush counts inside the dynamics region");
+static_assert(offsetof(SmemW, satsep) - offsetof(SmemW, polyw) == offsetof(PolyScratchT<SmemW::PMAXW>, satsep),
+              "the image's manifold scratch has PolyScratchT's layout");
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD + SmemN::NVW, "Hessian + J^T f scratch");
 static_assert(SmemW::NGW * 16 >= SmemW::NVW * SmemW::LD, "Hessian scratch");
 static_assert(SmemW::JL * SmemW::LDJ * 4 >= SmemW::CVXN * 4 + 2 * SmemW::PMAXW * 16 + 16 + POLY_ALLF * 4,

@@ -1214,17 +1214,20 @@ __device__ __forceinline__ void vert_rel(const DevModel* __restrict__ m, const S
 // with one lane per polygon vertex and scan compaction (as box_box_wave), the
 // _manifold_points picks as wave maxima.  Coordinates relative to g2's
 // centre, as MPR's.
-template <class S>
+// PS: the clip polygon / SAT-separation scratch (polyw, satsep): the LDS
+// image's own, or -- the second wave of a two-wave candidate in the joint
+// convex flush -- a PolyScratchT in the dead dynamics region.
+template <class S, class PS>
 #if MPCR_POLY_INLINE
 __device__ __forceinline__
 #else
 __device__ __noinline__
 #endif
-void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hints, int p,
+void poly_manifold_wave(const DevModel* __restrict__ m_, const S& s, PS& ps, const short* hints, int p,
                                                 const float n_[3], float depth, int q, int lane, float dist[4],
                                                 float pos[4][3], float nrm[4][3], int& nsl) {
   const MPCR_GMEM DevModel* __restrict__ m = uniform_model(m_);
-  ASSUME_GLOBAL(hints); ASSUME_LDS(&s); ASSUME_PRIVATE(dist); ASSUME_PRIVATE(pos); ASSUME_PRIVATE(nrm);
+  ASSUME_GLOBAL(hints); ASSUME_LDS(&s); ASSUME_LDS(&ps); ASSUME_PRIVATE(dist); ASSUME_PRIVATE(pos); ASSUME_PRIVATE(nrm);
   ASSUME_PRIVATE(&nsl);
   const float n[3] = {n_[0], n_[1], n_[2]};  // in registers (no alias reloads)
   PSTAMP_DECL
@@ -1269,7 +1272,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
         int h = two ? h0 : h1;
         support_geom(m, s, go, mn, pt, h, c);
         sp = nw[0] * pt[0] + nw[1] * pt[1] + nw[2] * pt[2] - off;
-        s.satsep[k] = sp;
+        ps.satsep[k] = sp;
       }
       mxa = fmaxf(mxa, wmax(sp));
     }
@@ -1281,7 +1284,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
 #pragma unroll 1
     for (int b0 = 0; b0 < nf; b0 += WAVE) {
       const int k = b0 + lane;
-      const bool nb = k < nf && near_max(s.satsep[k], mxa);
+      const bool nb = k < nf && near_max(ps.satsep[k], mxa);
       const int key = k >= nf1 ? 2 * (fa2 + k - nf1) + 1 : 2 * (fa1 + k);
       fmin = fminf(fmin, -wmax(nb ? -(float)key : -3e38f));
     }
@@ -1290,7 +1293,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
       const int key = (int)fmin;
       fr = key >> 1;
       rtwo = (key & 1) != 0;
-      bsep = s.satsep[rtwo ? nf1 + fr - fa2 : fr - fa1];
+      bsep = ps.satsep[rtwo ? nf1 + fr - fa2 : fr - fa1];
     }
     sync();  // satsep shares bytes with the clip buffer below
   }
@@ -1306,7 +1309,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
   // on the dual arm's hulls): the same candidates in the same order.  The
   // support-vertex faces of each side sit one per lane (lane k: entry k) and
   // the duplicate test reads them with readlane.
-  int* const cl = reinterpret_cast<int*>(&s.polyw[1][0][0]);
+  int* const cl = reinterpret_cast<int*>(&ps.polyw[1][0][0]);
   int nc = ns;
   const int vf1 = lane < c1 ? m->vert_face[i1.x + lane] : -1, vf2 = lane < c2 ? m->vert_face[i2.x + lane] : -1;
 #pragma unroll 1
@@ -1427,7 +1430,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
   if (lane < ninc) {
     float w[3];
     vert_rel(m, s, gi, m->face_vert[fii.x + lane], c, w);
-    s.polyw[0][lane][0] = w[0]; s.polyw[0][lane][1] = w[1]; s.polyw[0][lane][2] = w[2];
+    ps.polyw[0][lane][0] = w[0]; ps.polyw[0][lane][1] = w[1]; ps.polyw[0][lane][2] = w[2];
   }
   sync();
   PSTAMP(m, 26);
@@ -1440,7 +1443,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
     if (lane < np) {
       const int k2 = lane + 1 == np ? 0 : lane + 1;
 #pragma unroll
-      for (int k = 0; k < 3; k++) { P[k] = s.polyw[cur][lane][k]; Q[k] = s.polyw[cur][k2][k]; }
+      for (int k = 0; k < 3; k++) { P[k] = ps.polyw[cur][lane][k]; Q[k] = ps.polyw[cur][k2][k]; }
       dp = se[0] * (P[0] - Ae[0]) + se[1] * (P[1] - Ae[1]) + se[2] * (P[2] - Ae[2]);
       dq = se[0] * (Q[0] - Ae[0]) + se[1] * (Q[1] - Ae[1]) + se[2] * (Q[2] - Ae[2]);
       e0 = dp <= 0.f;
@@ -1450,12 +1453,12 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
     const int o = wscan_excl(e0 + e1, tot);
     if (e0 && o < S::PMAXW) {
 #pragma unroll
-      for (int k = 0; k < 3; k++) s.polyw[cur ^ 1][o][k] = P[k];
+      for (int k = 0; k < 3; k++) ps.polyw[cur ^ 1][o][k] = P[k];
     }
     if (e1 && o + e0 < S::PMAXW) {
       const float wgt = dp / (dp - dq);
 #pragma unroll
-      for (int k = 0; k < 3; k++) s.polyw[cur ^ 1][o + e0][k] = P[k] + wgt * (Q[k] - P[k]);
+      for (int k = 0; k < 3; k++) ps.polyw[cur ^ 1][o + e0][k] = P[k] + wgt * (Q[k] - P[k]);
     }
     np = min(tot, S::PMAXW);
     cur ^= 1;
@@ -1466,7 +1469,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, S& s, const short* hint
   bool keep = false;
   if (lane < np) {
 #pragma unroll
-    for (int k = 0; k < 3; k++) P[k] = s.polyw[cur][lane][k];
+    for (int k = 0; k < 3; k++) P[k] = ps.polyw[cur][lane][k];
     dk = nr[0] * P[0] + nr[1] * P[1] + nr[2] * P[2] - offr;
     keep = dk < m->pair_margin[p];
   }
@@ -2178,6 +2181,29 @@ struct SlotHist {
   float v[NC > 0 ? NC : 1][4];
 };
 
+// the active contacts (dist < margin) of pair p into the contact list from
+// position o on (those past MAXACT are dropped; the caller counts them)
+template <class S>
+__device__ __forceinline__ void put_contacts(const DevModel* __restrict__ m, S& s, int o, int p, int nsl,
+                                             const float dist[4], const float pos[4][3], const float nrm[4][3]) {
+  const float mg = m->pair_margin[p];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    if (c < nsl && dist[c] < mg) {
+      if (o < S::MAXACT) {
+        float f[9];
+        make_frame(f, nrm[c]);
+        s.con_pos[o][0] = pos[c][0]; s.con_pos[o][1] = pos[c][1]; s.con_pos[o][2] = pos[c][2];
+#pragma unroll
+        for (int e = 0; e < S::FRAMEW; e++) s.con_frame[o][e] = f[e];
+        s.con_dist[o] = dist[c];
+        s.con_pair[o] = p;
+      }
+      o++;
+    }
+  }
+}
+
 template <class S>
 __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S& s, const RolloutArgs& args, int b,
                                               int t, int H, bool valid, int p, int nsl, const float dist[4],
@@ -2218,25 +2244,7 @@ __device__ __forceinline__ void emit_contacts(const DevModel* __restrict__ m, S&
   int tot;
   const int pre = hscan_excl<S::CPW>(act, tot);
   const int base = s.ncon;
-  if (act) {
-    const float mg = m->pair_margin[p];
-    int o = base + pre;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      if (c < nsl && dist[c] < mg) {
-        if (o < S::MAXACT) {
-          float f[9];
-          make_frame(f, nrm[c]);
-          s.con_pos[o][0] = pos[c][0]; s.con_pos[o][1] = pos[c][1]; s.con_pos[o][2] = pos[c][2];
-#pragma unroll
-          for (int e = 0; e < S::FRAMEW; e++) s.con_frame[o][e] = f[e];
-          s.con_dist[o] = dist[c];
-          s.con_pair[o] = p;
-        }
-        o++;
-      }
-    }
-  }
+  if (act) put_contacts(m, s, base + pre, p, nsl, dist, pos, nrm);
   sync();
   if (hlane<S::CPW>() == 0) s.ncon = base + tot;
   sync();
@@ -3524,54 +3532,97 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
         }
       }
       STAMP(16);
-      if constexpr (S::WIDE) {
-        if (s.ncvx > S::CVXN - WAVE || (k + 1) * S::HL >= m->npair) {  // flush (pair order is kept)
-          const int nc = s.ncvx;
-          for (int i0 = 0; i0 < nc; i0 += S::HL) {
-#ifdef MPCR_WAVETIME
-            wt_cvx++;
-#endif
-            const bool v = i0 + lane < nc;
-            const int pc = v ? s.cvx[i0 + lane] : 0;
-            float cd[4] = {1e30f, 1e30f, 1e30f, 1e30f}, cp[4][3] = {}, cn[4][3] = {};
-            int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn, (args.dbg && b == 0 && t == H - 1) ? args.dbg
-                                                                                               : nullptr)
-                          : 0;
-            STAMP(21);
-            for (unsigned long long pm = __ballot(cn_sl == kPendingManifold); pm; pm &= pm - 1) {
-              const int q = __builtin_ctzll(pm);  // penetrating plane-mesh pairs, one at a time, all lanes
-              const int pq = __shfl(pc, q);
-              const float dq = __shfl(cd[0], q);
-              const int gp = m->pair_g1[pq];
-              const float* Rp = s.gxmat[gp];
-              const float nq[3] = {Rp[2], Rp[5], Rp[8]};
-              plane_mesh_manifold_wave(m, s, m->pair_g2[pq], nq, s.gxpos[gp], -dq, q, lane, cd, cp, cn, cn_sl);
-            }
-            STAMP(22);
-            for (unsigned long long pm = __ballot(cn_sl == kPendingPoly); pm; pm &= pm - 1) {
-              const int q = __builtin_ctzll(pm);  // penetrating polyhedron pairs, one at a time, all lanes
-              const int pq = __shfl(pc, q);
-              const float dq = __shfl(cd[0], q);
-              const float nq[3] = {__shfl(cn[0][0], q), __shfl(cn[0][1], q), __shfl(cn[0][2], q)};
-              poly_manifold_wave(m, s, hx, pq, nq, -dq, q, lane, cd, cp, cn, cn_sl);
-            }
-            STAMP(17);
-            emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c, shist, -1);
-            STAMP(18);
-          }
-          sync();
-          if (lane == 0) s.ncvx = 0;
-          sync();
-        }
+    }
+    if constexpr (!S::WIDE) {
+      if (s.ncon > S::MAXACT) {
+        status |= 1;
+        sync();
+        if (lane == 0) s.ncon = S::MAXACT;
+        sync();
       }
     }
-    if (s.ncon > S::MAXACT) {
-      status |= 1;
-      sync();
-      if (lane == 0) s.ncon = S::MAXACT;
-      sync();
-    }
     }  // run_coll
+    if constexpr (S::WIDE) {
+      // ---- the convex flush: every general-convex pair that survived the
+      //      cull (the list holds all of a model's, so this is the step's only
+      //      flush), MPR per lane, then the pending manifolds wave-cooperatively
+      //      one pair at a time.  Two waves per candidate (round 5): the
+      //      dynamics wave joins after the mass-matrix solve and the pairs are
+      //      dealt over both (item i on wave i & 1, rounds of 128), each wave
+      //      running the manifolds of its own pairs with its own clip scratch;
+      //      the contacts go to the list in pair order (a prefix over both
+      //      waves' counts), so the list -- and every result -- is bitwise the
+      //      one-wave kernel's.  Models with cost slots on convex pairs keep
+      //      the flush on the collision wave (cost_c accumulates per lane).
+      const bool split = WPC == 2 && m->cvx_joint;
+      const bool mine = WPC == 1 || split || wv == 1;
+      if constexpr (WPC == 2) block_sync();  // the list is complete; the dynamics are done
+      PolyScratchT<S::PMAXW>* const psc = reinterpret_cast<PolyScratchT<S::PMAXW>*>(
+          (WPC == 2 && wv == 0) ? &s.xpos[0][0] : &s.polyw[0][0][0]);
+      int* const jcnt = reinterpret_cast<int*>(&s.xpos[0][0]) + sizeof(PolyScratchT<S::PMAXW>) / 4;
+      const int ncv = s.ncvx, rstep = split ? 2 * WAVE : WAVE;
+      int ncon_w = s.ncon;
+      for (int i0 = 0; i0 < ncv; i0 += rstep) {
+#ifdef MPCR_WAVETIME
+        wt_cvx++;
+#endif
+        const int i = split ? i0 + 2 * lane + wv : i0 + lane;
+        const bool v = mine && i < ncv;
+        const int pc = v ? s.cvx[i] : 0;
+        float cd[4] = {1e30f, 1e30f, 1e30f, 1e30f}, cp[4][3] = {}, cn[4][3] = {};
+        int cn_sl = v ? narrow_lane(m, s, hx, pc, cd, cp, cn, (args.dbg && b == 0 && t == H - 1) ? args.dbg
+                                                                                           : nullptr)
+                      : 0;
+        STAMP(21);
+        for (unsigned long long pm = __ballot(cn_sl == kPendingManifold); pm; pm &= pm - 1) {
+          const int q = __builtin_ctzll(pm);  // penetrating plane-mesh pairs, one at a time, all lanes
+          const int pq = __shfl(pc, q);
+          const float dq = __shfl(cd[0], q);
+          const int gp = m->pair_g1[pq];
+          const float* Rp = s.gxmat[gp];
+          const float nq[3] = {Rp[2], Rp[5], Rp[8]};
+          plane_mesh_manifold_wave(m, s, m->pair_g2[pq], nq, s.gxpos[gp], -dq, q, lane, cd, cp, cn, cn_sl);
+        }
+        STAMP(22);
+        for (unsigned long long pm = __ballot(cn_sl == kPendingPoly); pm; pm &= pm - 1) {
+          const int q = __builtin_ctzll(pm);  // penetrating polyhedron pairs, one at a time, all lanes
+          const int pq = __shfl(pc, q);
+          const float dq = __shfl(cd[0], q);
+          const float nq[3] = {__shfl(cn[0][0], q), __shfl(cn[0][1], q), __shfl(cn[0][2], q)};
+          poly_manifold_wave(m, s, *psc, hx, pq, nq, -dq, q, lane, cd, cp, cn, cn_sl);
+        }
+        STAMP(17);
+        if (split) {
+          // this item's active contacts; their list offsets from both waves'
+          // counts in item order (lane l holds items 2l and 2l + 1)
+          int act = 0;
+          if (v && !(m->disableflags & 16)) {
+            const float mg = m->pair_margin[pc];
+#pragma unroll
+            for (int c = 0; c < 4; c++) act += (c < cn_sl && cd[c] < mg) ? 1 : 0;
+          }
+          jcnt[2 * lane + wv] = act;
+          block_sync();
+          const int a0 = jcnt[2 * lane], a1 = jcnt[2 * lane + 1];
+          int tot;
+          const int pre = wscan_excl(a0 + a1, tot) + (wv ? a0 : 0);
+          if (act) put_contacts(m, s, ncon_w + pre, pc, cn_sl, cd, cp, cn);
+          ncon_w += tot;
+          block_sync();  // jcnt is the next round's
+        } else if (mine) {
+          emit_contacts(m, s, args, b, t, H, v, pc, cn_sl, cd, cp, cn, cost_c, shist, -1);
+        }
+        STAMP(18);
+      }
+      if (split && run_coll && lane == 0) s.ncon = ncon_w;
+      sync();
+      if (run_coll && s.ncon > S::MAXACT) {
+        status |= 1;
+        sync();
+        if (lane == 0) s.ncon = S::MAXACT;
+        sync();
+      }
+    }
     // WPC = 2 and DevModel::coll_rows: the collision wave builds the
     // constraint rows too, still beside wave 0's dynamics (they need the
     // contacts, qpos, qvel, cdof and the tree COMs, all ready before the first
