@@ -357,7 +357,7 @@ def strong_subrecord(eng, dev, rank, world, H, steps, warmup, n_global=4096):
             "best": {"index": idx, "cost": best}}
 
 
-def c5_run(rank, world, local, dev, n_global, H, iters, ticks, warmup, capture_exchange):
+def c5_run(rank, world, gpu, dev, n_global, H, iters, ticks, warmup, capture_exchange):
     """C5 (BASELINE configs[4]): closed-loop MPC ticks on the dual-arm scene.
     A tick = compute_cem (SBP/mjx_planner.py:364-406: `iters` CEM iterations
     over the global batch, each rank its n_global / world share, sampling
@@ -371,10 +371,10 @@ def c5_run(rank, world, local, dev, n_global, H, iters, ticks, warmup, capture_e
     from manipulator_mujoco_amd.engine import MPCR_LAYOUT_XI, Plant
     from manipulator_mujoco_amd.planner import cem_planner
     p = cem_planner(num_dof=6, num_batch=n_global, num_steps=H, timestep=0.05, maxiter_cem=iters, num_elite=0.05,
-                    w_pos=W[0], w_rot=W[1], w_col=W[2], maxiter_projection=10, model_path="dual_arm", device=local,
+                    w_pos=W[0], w_rot=W[1], w_col=W[2], maxiter_projection=10, model_path="dual_arm", device=gpu,
                     graph=True, group=dist.group.WORLD if world > 1 else None, return_rollouts=False,
                     capture_exchange=capture_exchange, verbose=False)
-    plant = Plant(p.model, device=local)
+    plant = Plant(p.model, device=gpu)
     qpos = plant.qpos.copy()
     qpos[:6] = Q0
     plant.set_state(qpos=qpos)
@@ -419,14 +419,14 @@ def c5_run(rank, world, local, dev, n_global, H, iters, ticks, warmup, capture_e
                   else "the whole tick (one rank: no exchange)")}
 
 
-def c5_subrecord(rank, world, local, dev, steps, warmup):
+def c5_subrecord(rank, world, gpu, dev, steps, warmup):
     """C5 beside the default line: the global 8192 x 50 x 3
     tick over however many ranks this run has -- the strong-scaling curve the
     north star's ">= 6x further at 8 GPUs" is about.  The exchange runs
     eagerly between graph replays here (the RCCL-captured tick is
     `--config c5 --c5-capture-exchange`)."""
     cfg = CONFIGS["c5"]
-    r = c5_run(rank, world, local, dev, cfg["n"], cfg["H"], cfg["iters"], steps, warmup, capture_exchange=False)
+    r = c5_run(rank, world, gpu, dev, cfg["n"], cfg["H"], cfg["iters"], steps, warmup, capture_exchange=False)
     return {"scaling": "strong", "workload": f"C5 dual_arm closed-loop tick: {cfg['iters']} CEM iterations over "
                                              f"{cfg['n']} candidates x {cfg['H']} steps in total, split over "
                                              f"{world} GPU(s), + the plant step",
@@ -483,7 +483,7 @@ def main_c5(args, cfg):
                    "reps": reps, "host": {"usable_cores": usable, "affinity_cores": aff, "cgroup_cpu_quota": quota,
                                           "nproc": ncpu, "cpu_model": model}}
     gpu, dev, ndev, backend = init_device(args, world, local)
-    r = c5_run(rank, world, local, dev, n_global, H, iters, args.steps, args.warmup, args.c5_capture_exchange)
+    r = c5_run(rank, world, gpu, dev, n_global, H, iters, args.steps, args.warmup, args.c5_capture_exchange)
     if rank == 0:
         coll = {"nccl": "RCCL (xGMI)", "gloo": "gloo (host-staged)"}.get(backend, str(backend))
         fps = flops_per_step(r["model"], r["nefc_mean"], "dual_arm")
@@ -677,7 +677,7 @@ def main():
     subs = {}
     if args.config == "c3" and args.scaling == "weak" and args.n == cfg["n"] and not args.no_sub:
         subs["strong"] = strong_subrecord(eng, dev, rank, world, H, args.steps, args.warmup)
-        subs["c5"] = c5_subrecord(rank, world, local, dev, min(args.steps, 5), 2)
+        subs["c5"] = c5_subrecord(rank, world, gpu, dev, min(args.steps, 5), 2)
 
     if rank == 0:
         coll = {"nccl": "RCCL (xGMI)", "gloo": "gloo (host-staged)"}.get(backend, str(backend))

@@ -179,11 +179,12 @@ __device__ __forceinline__ float wsum(float v) {
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
 }
-// exclusive prefix sum of small per-lane counts (0..7) by bit-plane ballots
+// exclusive prefix sum of small per-lane counts (0 .. 2^BITS - 1) by bit-plane ballots
+template <int BITS = 3>
 __device__ __forceinline__ int wscan_excl(int v, int& total) {
   int pre = 0, tot = 0;
 #pragma unroll
-  for (int bit = 0; bit < 3; bit++) {
+  for (int bit = 0; bit < BITS; bit++) {
     const unsigned long long mk = __ballot((v >> bit) & 1);
     pre += lanes_below(mk) << bit;
     tot += __popcll(mk) << bit;
@@ -3605,7 +3606,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           block_sync();
           const int a0 = jcnt[2 * lane], a1 = jcnt[2 * lane + 1];
           int tot;
-          const int pre = wscan_excl(a0 + a1, tot) + (wv ? a0 : 0);
+          const int pre = wscan_excl<4>(a0 + a1, tot) + (wv ? a0 : 0);  // two items: up to 8
           if (act) put_contacts(m, s, ncon_w + pre, pc, cn_sl, cd, cp, cn);
           ncon_w += tot;
           block_sync();  // jcnt is the next round's
@@ -3629,10 +3630,17 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     // barrier) and hands them over at the second; otherwise wave 0 builds them
     // after the contact list is handed over
     const bool rows_c = WPC == 2 && m->coll_rows;
+    // two waves per candidate, dual-arm class, rows after the hand-over (round
+    // 5): both waves build the constraint rows, the Jacobian entries and the
+    // row parameters dealt over 128 lanes (the bookkeeping -- row counts,
+    // sources, offsets -- computed identically on both), and wave 1 leaves at
+    // the barrier that follows; same values in the same places as one wave
+    const bool rows_j = WPC == 2 && S::WIDE && !rows_c;
+    const int rl0 = rows_j ? wv * S::HL : 0, rls = rows_j ? 2 * S::HL : S::HL;
     if constexpr (WPC == 2) {
       if (!rows_c) {
         block_sync();  // the contact list is ready; wave 1 waits for the next step's geom poses
-        if (!run_main) continue;
+        if (!run_main && !rows_j) continue;
       }
     }
 
@@ -3641,7 +3649,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
     // ---- constraint rows: equality, limits, contacts ------------------------
     bool coupled = true;  // a constraint row spans two kinematic trees (Newton's H not block diagonal)
-    if (WPC == 1 || (rows_c ? run_coll : run_main)) {
+    if (WPC == 1 || rows_j || (rows_c ? run_coll : run_main)) {
       const int ncon = s.ncon;
       const int neq = (m->disableflags & 64) ? 0 : (S::WIDE ? m->neqrow : m->neq);
       int nlim_l = 0, lsides = 0;
@@ -3718,7 +3726,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       sync();
       // Jacobian entries of equality/limit rows: (row, dof)
       const int nsimple = neq + nlim + ntr;
-      for (int idx = lane; idx < nsimple * NVW; idx += S::HL) {
+      for (int idx = lane + rl0; idx < nsimple * NVW; idx += rls) {
         const int r = idx >> S::LOG_NVW, i = idx & (NVW - 1);
         const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
         float v = 0.f;
@@ -3773,7 +3781,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
         jstore(s, gx, r, i, v);
       }
       // contact Jacobians: (contact, dof) -> J_n +- mu J_t rows
-      for (int idx = lane; idx < keep_con * NVW; idx += S::HL) {
+      for (int idx = lane + rl0; idx < keep_con * NVW; idx += rls) {
         const int c = idx >> S::LOG_NVW, i = idx & (NVW - 1);
         const int p = s.con_pair[c];
         const int4 ji = m->pair_jinfo[p];  // one load: both bodies' dof masks and trees
@@ -3818,9 +3826,12 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           jstore(s, gx, off + 3, i, jn - mu * jt2);
         }
       }
-      sync();  // (also orders the J rows past JL written to the HBM slab by other lanes)
+      // (also orders the J rows past JL written to the HBM slab by other lanes,
+      // and with rows_j the other wave's rows)
+      if (rows_j) block_sync();
+      else sync();
       // row parameters: vel, impedance, D, aref
-      for (int r = lane; r < nefc; r += S::HL) {
+      for (int r = lane + rl0; r < nefc; r += rls) {
         const int src = s.efc_src[r], kind = src >> 24, id = (src >> 4) & 0xfffff, side = src & 15;
         float pos, margin, diag;
         const float* sref;
@@ -3903,7 +3914,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           o[0] = s.efc_D[r]; o[1] = s.efc_aref[r]; o[2] = vel;
         }
       }
-      if (args.dbg && b == 0 && t == H - 1) {
+      if (args.dbg && b == 0 && t == H - 1 && run_main) {
         if (lane == 0) { args.dbg[DBG_NCON] = (float)s.ncon; args.dbg[DBG_NEFC] = (float)s.nefc; }
         if (lane < s.ncon && lane < DBG_MAXCON) {
           float* o = args.dbg + DBG_CON + 8 * lane;
@@ -3915,6 +3926,10 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       sync();
     }  // constraint rows
     if constexpr (WPC == 2) {
+      if (rows_j) {
+        block_sync();  // the rows are ready; wave 1 waits for the next step's geom poses
+        if (!run_main) continue;
+      }
       if (rows_c) {
         if (run_coll && lane == 0) s.pad_ = coupled ? 1 : 0;
         block_sync();  // contacts and constraint rows ready; wave 1 waits for the next step's geom poses
