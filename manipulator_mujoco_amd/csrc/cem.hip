@@ -158,8 +158,14 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
 #pragma unroll
     for (int r = 0; r < PJ_NB; r++) lam[r] = sl[r] = 0.f;
     const int LD = nd * PJ_BLK;
-    // this part's rows [t0, t1) of each constraint family
-    const int t0 = (a.H * part) / PJ_NP, t1 = (a.H * (part + 1)) / PJ_NP;
+    // the 3H rows of each constraint family fall into PJ_NR = 4 fixed ranges
+    // whatever the layout, summed in one tree ((r0 + r1) + (r2 + r3)): a
+    // part of PJ_NP = 4 lanes holds one range, of PJ_NP = 2 two (their sum
+    // first), so a candidate's projection is bitwise the same at 16 and at
+    // 32 candidates per workgroup -- i.e. independent of the batch size
+    // (the sharded planner's ranks then reproduce one GPU at C5's 8192)
+    constexpr int PJ_NR = 4, PJ_RPL = PJ_NR / PJ_NP;
+    static_assert(PJ_NR % PJ_NP == 0, "row ranges per part");
     for (int it = 0; it < a.maxiter; it++) {
       // -lincost = lam + rho xi + rho sum_k A_k^T (b - s_k)  (every part holds
       // the same values; part 0 writes them)
@@ -189,35 +195,48 @@ __global__ void __launch_bounds__(64 * PJ_MAXD) sample_project_kernel(ProjArgs a
       float dl[PJ_NB];
 #pragma unroll
       for (int r = 0; r < PJ_NB; r++) dl[r] = sl[r] = 0.f;
-      for (int k = 0; k < 3; k++) {
-        const float b = a.bound[k];
-        const float* Xk = Xs + (size_t)k * a.H * PJ_BLK;
-        auto row_update = [&](const float4 x0, const float4 x1, const float4 x2) {
-          const float x[PJ_BLK] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x, x2.y, x2.z, x2.w};
-          float v = 0.f;
 #pragma unroll
-          for (int c = 0; c < PJ_NB; c++) v = fmaf(x[c], p[c], v);
-          const float e_res = fmaxf(v - b, 0.f) - fmaxf(-v - b, 0.f);  // A^T res per row
-          const float e_sl = fmaxf(b + v, 0.f) - fmaxf(b - v, 0.f);    // A^T (b - s) per row
+      for (int rq = 0; rq < PJ_RPL; rq++) {
+        const int q = part * PJ_RPL + rq;  // this range: rows [t0, t1) of each family
+        const int t0 = (a.H * q) / PJ_NR, t1 = (a.H * (q + 1)) / PJ_NR;
+        float dq[PJ_NB], sq[PJ_NB];
 #pragma unroll
-          for (int c = 0; c < PJ_NB; c++) {
-            dl[c] = fmaf(x[c], e_res, dl[c]);
-            sl[c] = fmaf(x[c], e_sl, sl[c]);
+        for (int r = 0; r < PJ_NB; r++) dq[r] = sq[r] = 0.f;
+        for (int k = 0; k < 3; k++) {
+          const float b = a.bound[k];
+          const float* Xk = Xs + (size_t)k * a.H * PJ_BLK;
+          auto row_update = [&](const float4 x0, const float4 x1, const float4 x2) {
+            const float x[PJ_BLK] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x, x2.y, x2.z, x2.w};
+            float v = 0.f;
+#pragma unroll
+            for (int c = 0; c < PJ_NB; c++) v = fmaf(x[c], p[c], v);
+            const float e_res = fmaxf(v - b, 0.f) - fmaxf(-v - b, 0.f);  // A^T res per row
+            const float e_sl = fmaxf(b + v, 0.f) - fmaxf(b - v, 0.f);    // A^T (b - s) per row
+#pragma unroll
+            for (int c = 0; c < PJ_NB; c++) {
+              dq[c] = fmaf(x[c], e_res, dq[c]);
+              sq[c] = fmaf(x[c], e_sl, sq[c]);
+            }
+          };
+          int t = t0;
+          for (; t + PJ_RG <= t1; t += PJ_RG) {  // a group's LDS loads issue together
+            float4 xg[PJ_RG][3];
+#pragma unroll
+            for (int u = 0; u < PJ_RG; u++)
+#pragma unroll
+              for (int q3 = 0; q3 < 3; q3++) xg[u][q3] = reinterpret_cast<const float4*>(Xk + (t + u) * PJ_BLK)[q3];
+#pragma unroll
+            for (int u = 0; u < PJ_RG; u++) row_update(xg[u][0], xg[u][1], xg[u][2]);
           }
-        };
-        int t = t0;
-        for (; t + PJ_RG <= t1; t += PJ_RG) {  // a group's LDS loads issue together
-          float4 xg[PJ_RG][3];
-#pragma unroll
-          for (int u = 0; u < PJ_RG; u++)
-#pragma unroll
-            for (int q = 0; q < 3; q++) xg[u][q] = reinterpret_cast<const float4*>(Xk + (t + u) * PJ_BLK)[q];
-#pragma unroll
-          for (int u = 0; u < PJ_RG; u++) row_update(xg[u][0], xg[u][1], xg[u][2]);
+          for (; t < t1; t++) {
+            const float4* xr = reinterpret_cast<const float4*>(Xk + t * PJ_BLK);
+            row_update(xr[0], xr[1], xr[2]);
+          }
         }
-        for (; t < t1; t++) {
-          const float4* xr = reinterpret_cast<const float4*>(Xk + t * PJ_BLK);
-          row_update(xr[0], xr[1], xr[2]);
+#pragma unroll
+        for (int c = 0; c < PJ_NB; c++) {  // (r0 + r1) within a two-range part; one range: 0 + r0 = r0
+          dl[c] += dq[c];
+          sl[c] += sq[c];
         }
       }
       // the parts' sums: lanes cl + PJ_CPW q (q = 0..3) swap and add; fp32

@@ -830,12 +830,48 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     e->dev.hull_info = as_gmem(e->d_hull_info);
     e->dev.hull_adjv = as_gmem(e->d_hull_adjv);
     e->dev.hull_head = as_gmem(e->d_hull_head);
+    // the support start table; a cell whose start vertex is the support of
+    // every direction in it is marked exact (bit 15 of the record's index
+    // half: vertex indices are < 32768): the kernel's climb from that vertex
+    // would end where it starts (no neighbour beats it, and no hint vertex
+    // beats the start), so the kernel skips the hint load and the climb --
+    // bitwise the same support point, one dependent load instead of two or
+    // more.  A cube-map cell is the convex cone of its 4 corner rays and the
+    // directions a hull vertex is extreme for are a convex cone, bounded by
+    // its neighbours: the start vertex beats each neighbour by > kExactGap m
+    // (fp32 coordinates) along each corner ray, so along every direction of
+    // the cell (fp32 rounding of a projection or of the cell test moves it
+    // by ~1e-8 m)
+    constexpr double kExactGap = 1e-6;
+    auto cell_exact = [&](int g, int c, int v) {
+      const int R = MPCR_LUT_R, f = c / (R * R), iu = (c / R) % R, iv = c % R, ax = f / 2;
+      const float* x = &hv[v].x;
+      for (int du = 0; du < 2; du++)
+        for (int dv = 0; dv < 2; dv++) {
+          double d[3];
+          d[ax] = (f & 1) ? -1.0 : 1.0;
+          d[(ax + 1) % 3] = -1.0 + 2.0 * (iu + du) / R;
+          d[(ax + 2) % 3] = -1.0 + 2.0 * (iv + dv) / R;
+          const double dn = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+          for (int k = h.hull_adjadr[v]; k < h.hull_adjadr[v] + h.hull_adjnum[v]; k++) {
+            const float* y = &hv[h.hull_adj[k]].x;
+            const double gap = ((double)x[0] - y[0]) * d[0] + ((double)x[1] - y[1]) * d[1] + ((double)x[2] - y[2]) * d[2];
+            if (!(gap > kExactGap * dn)) return false;
+          }
+        }
+      (void)g;
+      return true;
+    };
     std::vector<float4> hl(MPCR_MAX_HULLLUT);
     int nlut = 0;
     for (int g = 0; g < h.ngeom; g++)
       if (h.geom_hulladr[g] >= 0 && h.geom_hullnum[g] > 0) {
         const int la = h.geom_lutadr[g], nc = 6 * MPCR_LUT_R * MPCR_LUT_R;
-        for (int c = 0; c < nc; c++) hl[la + c] = rec(h.hull_lut[la + c]);
+        for (int c = 0; c < nc; c++) {
+          const int v = h.hull_lut[la + c];
+          hl[la + c] = rec(v);
+          if (cell_exact(g, c, v)) hl[la + c].w = bitsf(v | 0x8000 | (h.hull_adjnum[v] << 16));
+        }
         nlut = std::max(nlut, la + nc);
       }
     if (hipMalloc(&e->d_hull_lut, sizeof(float4) * (nlut ? nlut : 1)) != hipSuccess ||

@@ -789,21 +789,24 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
     // both loads issue together (the oracle's rule)
     const int la = m->geom_lutadr[g];
     float4 hv = la >= 0 ? m->hull_lut[la + lut_cell(l)] : m->hull_vert[m->geom_hulladr[g]];
-    int v = la >= 0 ? (__float_as_int(hv.w) & 0xffff) : m->geom_hulladr[g];
-    int deg = la >= 0 ? (__float_as_int(hv.w) >> 16) : __float_as_int(hv.w);
-    float best = hv.x * lu[0] + hv.y * lu[1] + hv.z * lu[2];
-    if (hint >= 0) {
-      const float4 hh = m->hull_vert[hint];
-      const float bh = hh.x * lu[0] + hh.y * lu[1] + hh.z * lu[2];
-      if (bh > best + kSupBand) { v = hint; hv = hh; deg = __float_as_int(hh.w); best = bh; }
-    }
+    const int hw = __float_as_int(hv.w);
+    int v = la >= 0 ? (hw & 0x7fff) : m->geom_hulladr[g];
     PROF_COUNT(m, 20);
-    for (int guard = 0; guard < 4096; guard++) {
-      PROF_COUNT(m, 19);
-      const int nb = climb_round(m, v, deg, lu, best, hv);
-      if (nb < 0) break;
-      v = nb & 0xffff;
-      deg = nb >> 16;
+    if (!(la >= 0 && (hw & 0x8000))) {  // not an exact cell (engine.hip): the hint, then the climb
+      int deg = la >= 0 ? (hw >> 16) : hw;
+      float best = hv.x * lu[0] + hv.y * lu[1] + hv.z * lu[2];
+      if (hint >= 0) {
+        const float4 hh = m->hull_vert[hint];
+        const float bh = hh.x * lu[0] + hh.y * lu[1] + hh.z * lu[2];
+        if (bh > best + kSupBand) { v = hint; hv = hh; deg = __float_as_int(hh.w); best = bh; }
+      }
+      for (int guard = 0; guard < 4096; guard++) {
+        PROF_COUNT(m, 19);
+        const int nb = climb_round(m, v, deg, lu, best, hv);
+        if (nb < 0) break;
+        v = nb & 0xffff;
+        deg = nb >> 16;
+      }
     }
     p[0] = hv.x; p[1] = hv.y; p[2] = hv.z;
     hint = v;

@@ -28,7 +28,9 @@ def _port():
 def _run(cmd):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    # a rank's traceback sits in the middle of torchrun's stderr: keep its lines
+    ranks = "\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[rank"))[-6000:]
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], ranks or r.stderr[-4000:])
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     return json.loads(lines[0])

@@ -125,35 +125,40 @@ def test_headless_closed_loop(torch_cuda, tmp_path):
     assert (np.diff(d) < 1e-3).mean() > 0.9  # steady approach, no divergence
 
 
-def _sharded_worker(rank, world, port, args, out):
+def _sharded_worker(rank, world, port, args, out, kw):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        p = _planner(group=dist.group.WORLD, num_batch=512)
+        p = _planner(group=dist.group.WORLD, **kw)
         res = [p.compute_cem(*a) for a in args]
         out[rank] = [[np.asarray(x).tolist() for x in r[:7]] for r in res]
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_sharded_planner_equals_one_gpu(torch_cuda):
+@pytest.mark.parametrize("kw", [dict(num_batch=512), dict(num_batch=512, model_path="dual_arm", graph=True),
+                                dict(num_batch=8192, num_steps=50, model_path="dual_arm", graph=True)],
+                         ids=["planner_scene", "dual_arm_graph", "dual_arm_c5"])
+def test_two_rank_sharded_planner_equals_one_gpu(torch_cuda, kw):
     """The whole sharded planner with two ranks on the one GPU
     of the box (gloo carries the collectives; RCCL refuses two ranks on one
     device): sampling by global index, local top-E -> all-gather -> global
     top-E, replicated update, best-key MIN all-reduce + owner broadcast.  Both
-    ranks return the single-GPU 9-tuple (first 7 entries) bit for bit."""
+    ranks return the single-GPU 9-tuple (first 7 entries) bit for bit -- the
+    planner scene eagerly, the dual arm from graph replays (the C5 path)."""
     import torch.multiprocessing as mp
     ticks = list(_ticks())
-    single = _planner(num_batch=512)
+    single = _planner(**kw)
     ref = [single.compute_cem(*a) for a in ticks]
     mgr = mp.get_context("spawn").Manager()
     out = mgr.dict()
-    mp.spawn(_sharded_worker, args=(2, _port(), ticks, out), nprocs=2, join=True)
+    mp.spawn(_sharded_worker, args=(2, _port(), ticks, out, kw), nprocs=2, join=True)
     for r in range(2):
-        for got, want in zip(out[r], ref):
-            for x, y in zip(got, want[:7]):
-                np.testing.assert_array_equal(np.asarray(x, dtype=np.asarray(y).dtype), np.asarray(y))
+        for k, (got, want) in enumerate(zip(out[r], ref)):
+            for j, (x, y) in enumerate(zip(got, want[:7])):
+                np.testing.assert_array_equal(np.asarray(x, dtype=np.asarray(y).dtype), np.asarray(y),
+                                              err_msg=f"rank {r} tick {k} entry {j}")
 
 
 def _dual_arm_loop(graph, n, H, ticks):
