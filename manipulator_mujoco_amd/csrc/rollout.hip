@@ -761,15 +761,45 @@ __device__ __forceinline__ int lut_cell(const float l[3]) {
 // org (nullable): the result relative to org, with (geom centre - org)
 // formed first -- MPR works relative to the second geom's centre, so the
 // Minkowski points carry cm-scale rounding instead of world-scale (1 m) rounding
+//
+// A query runs in two parts so a caller can put two of them in flight
+// together (MPR's support pair: round 5): sup_start issues the first loads
+// of a mesh query -- the start table cell of the direction and the hint
+// vertex, independent of each other (the hint's index is clamped to the
+// hull: a query without one loads the hull's first vertex and ignores it) --
+// and sup_finish consumes them: the hint if it beats the table vertex, then
+// the climb (none from an exact cell, engine.hip).  Same values and
+// comparisons as one call, so bitwise the same support point.
+struct SupQ {
+  float l[3], lu[3], ln;
+  float4 hv, hh;
+  int type, la;
+};
 template <class S>
-__device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
-                                             float out[3], int& hint, const float* org = nullptr) {
+__device__ __forceinline__ void sup_start(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
+                                          int hint, SupQ& q) {
+  const float* R = s.gxmat[g];
+  mtv(q.l, R, dir);
+  q.ln = sqrtf(dot3(q.l, q.l));
+  q.type = m->geom_type[g];
+  if (q.type == 7) {
+    const float il = q.ln > 0.f ? 1.f / q.ln : 0.f;
+    q.lu[0] = q.l[0] * il; q.lu[1] = q.l[1] * il; q.lu[2] = q.l[2] * il;
+    q.la = m->geom_lutadr[g];
+    const int h0 = m->geom_hulladr[g];
+    q.hv = q.la >= 0 ? m->hull_lut[q.la + lut_cell(q.l)] : m->hull_vert[h0];
+    q.hh = m->hull_vert[hint >= 0 ? hint : h0];
+  }
+}
+template <class S>
+__device__ __forceinline__ void sup_finish(const DevModel* __restrict__ m, const S& s, int g, SupQ& q, float out[3],
+                                           int& hint, const float* org) {
   const float* R = s.gxmat[g];
   const float* sz = m->geom_size[g];
-  float l[3], p[3] = {0.f, 0.f, 0.f};
-  mtv(l, R, dir);
-  const float ln = sqrtf(dot3(l, l));
-  const int type = m->geom_type[g];
+  const float* l = q.l;
+  const float ln = q.ln;
+  const int type = q.type;
+  float p[3] = {0.f, 0.f, 0.f};
   if (type == 2 || type == 3) {  // sphere, capsule
     if (ln > 0.f) { p[0] = sz[0] * l[0] / ln; p[1] = sz[0] * l[1] / ln; p[2] = sz[0] * l[2] / ln; }
     if (type == 3) p[2] += tie_sign(l[2], ln) * sz[1];
@@ -781,22 +811,19 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
     p[0] = tie_sign(l[0], ln) * sz[0];
     p[1] = tie_sign(l[1], ln) * sz[1];
     p[2] = tie_sign(l[2], ln) * sz[2];
-  } else if (type == 7) {  // mesh hull: steepest ascent on the vertex graph from its first vertex
-    const float il = ln > 0.f ? 1.f / ln : 0.f;
-    const float lu[3] = {l[0] * il, l[1] * il, l[2] * il};
+  } else if (type == 7) {  // mesh hull: steepest ascent on the vertex graph
     // start: the table vertex of l's cube-map cell, or the hint (where the
-    // previous query on this pair ended) when it beats that by the band --
-    // both loads issue together (the oracle's rule)
-    const int la = m->geom_lutadr[g];
-    float4 hv = la >= 0 ? m->hull_lut[la + lut_cell(l)] : m->hull_vert[m->geom_hulladr[g]];
+    // previous query on this pair ended) when it beats that by the band
+    const float* lu = q.lu;
+    float4 hv = q.hv;
     const int hw = __float_as_int(hv.w);
-    int v = la >= 0 ? (hw & 0x7fff) : m->geom_hulladr[g];
+    int v = q.la >= 0 ? (hw & 0x7fff) : m->geom_hulladr[g];
     PROF_COUNT(m, 20);
-    if (!(la >= 0 && (hw & 0x8000))) {  // not an exact cell (engine.hip): the hint, then the climb
-      int deg = la >= 0 ? (hw >> 16) : hw;
+    if (!(q.la >= 0 && (hw & 0x8000))) {  // not an exact cell (engine.hip): the hint, then the climb
+      int deg = q.la >= 0 ? (hw >> 16) : hw;
       float best = hv.x * lu[0] + hv.y * lu[1] + hv.z * lu[2];
       if (hint >= 0) {
-        const float4 hh = m->hull_vert[hint];
+        const float4 hh = q.hh;
         const float bh = hh.x * lu[0] + hh.y * lu[1] + hh.z * lu[2];
         if (bh > best + kSupBand) { v = hint; hv = hh; deg = __float_as_int(hh.w); best = bh; }
       }
@@ -818,6 +845,13 @@ __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, con
     out[0] += s.gxpos[g][0]; out[1] += s.gxpos[g][1]; out[2] += s.gxpos[g][2];
   }
 }
+template <class S>
+__device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
+                                             float out[3], int& hint, const float* org = nullptr) {
+  SupQ q;
+  sup_start(m, s, g, dir, hint, q);
+  sup_finish(m, s, g, q, out, hint, org);
+}
 
 struct MprPt { float v[3], a[3], b[3]; };
 
@@ -825,8 +859,11 @@ template <class S>
 __device__ __forceinline__ void mpr_support(const DevModel* __restrict__ m, const S& s, int g1, int g2,
                                             const float dir[3], MprPt& o, int (&hint)[2], float* trace = nullptr) {
   const float nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support_geom(m, s, g1, dir, o.a, hint[0], s.gxpos[g2]);  // relative to g2's centre
-  support_geom(m, s, g2, nd, o.b, hint[1], s.gxpos[g2]);
+  SupQ q1, q2;  // both queries' first loads in flight together
+  sup_start(m, s, g1, dir, hint[0], q1);
+  sup_start(m, s, g2, nd, hint[1], q2);
+  sup_finish(m, s, g1, q1, o.a, hint[0], s.gxpos[g2]);  // relative to g2's centre
+  sup_finish(m, s, g2, q2, o.b, hint[1], s.gxpos[g2]);
   o.v[0] = o.a[0] - o.b[0]; o.v[1] = o.a[1] - o.b[1]; o.v[2] = o.a[2] - o.b[2];
   if (trace) {
     const int q = (int)trace[47];

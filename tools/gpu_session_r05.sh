@@ -32,7 +32,7 @@ if has tests; then
 fi
 if has c3precise; then  # C3 parity on the fast-math and the precise build, same batch
   MPCR_PARITY_LOG=$OUT/parity_c3_fast.jsonl run c3_fast 400 $PYT -s tests/test_gpu_parity.py -k test_parity_c3_full
-  MPCR_LIB=build_variants/precise.so MPCR_PARITY_LOG=$OUT/parity_c3_precise.jsonl \
+  MPCR_LIB=build_variants/keep/precise.so MPCR_PARITY_LOG=$OUT/parity_c3_precise.jsonl \
     run c3_precise 400 $PYT -s tests/test_gpu_parity.py -k test_parity_c3_full
 fi
 if has mrank; then
@@ -68,13 +68,13 @@ if has ab; then  # interleaved A/B timing of build_variants/*.so (MODEL / N / H 
   grep -h "median" $OUT/ab_*.log | sort > $OUT/ab_summary.txt
 fi
 if has prof; then
-  run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 10 --warmup 2
+  run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-sub --no-cpu-baseline --no-contact-report --steps 10 --warmup 2
 fi
 if has pmc; then
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"; do
     i=$((i+1))
-    run pmc$i 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
+    run pmc$i 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 bench.py --no-sub --no-cpu-baseline --no-contact-report --steps 3 --warmup 1
   done
 fi
 if has pmccfg; then  # the C2 / C4 lines' passes
