@@ -818,7 +818,6 @@ __device__ __forceinline__ void sup_finish(const DevModel* __restrict__ m, const
     float4 hv = q.hv;
     const int hw = __float_as_int(hv.w);
     int v = q.la >= 0 ? (hw & 0x7fff) : m->geom_hulladr[g];
-    PROF_COUNT(m, 20);
     if (!(q.la >= 0 && (hw & 0x8000))) {  // not an exact cell (engine.hip): the hint, then the climb
       int deg = q.la >= 0 ? (hw >> 16) : hw;
       float best = hv.x * lu[0] + hv.y * lu[1] + hv.z * lu[2];
@@ -860,6 +859,7 @@ __device__ __forceinline__ void mpr_support(const DevModel* __restrict__ m, cons
                                             const float dir[3], MprPt& o, int (&hint)[2], float* trace = nullptr) {
   const float nd[3] = {-dir[0], -dir[1], -dir[2]};
   SupQ q1, q2;  // both queries' first loads in flight together
+  PROF_COUNT(m, 20);
   sup_start(m, s, g1, dir, hint[0], q1);
   sup_start(m, s, g2, nd, hint[1], q2);
   sup_finish(m, s, g1, q1, o.a, hint[0], s.gxpos[g2]);  // relative to g2's centre

@@ -16,11 +16,11 @@ PHASES = ["init+basis", "kinematics", "geom/com/eef", "cinert/cdof", "crb/vel/rn
 # slot 7 is the collision loop's tail (box-box moved to 16); 15 packs iteration counts
 EXTRA = {29: "newton: jar/cost", 30: "newton: J^T f + grad", 31: "newton: Hessian", 16: "coll: box-box (wave)", 21: "coll: convex narrow (MPR)", 22: "coll: plane-mesh manifold",
          17: "coll: polyhedron manifold", 18: "coll: convex emit"}
-COUNTS = {19: "hull-climb rounds (wave level)", 20: "mesh support calls (wave level)"}
+COUNTS = {19: "hull-climb rounds (wave level)", 20: "MPR support pairs (wave level)"}
 
 
 def main():
-    so = os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr_prof.so")
+    so = os.environ.get("PROF_LIB") or os.path.join(ROOT, "manipulator_mujoco_amd", "libmpcr_prof.so")
     if "--build" in sys.argv:  # build here (CPU container), run on the GPU box; --counts: wave-level event counters
         build.compile_lib(so, ["-DMPCR_PROFILE"] + (["-DMPCR_PROFILE_COUNTS"] if "--counts" in sys.argv else []))
         print(so)
