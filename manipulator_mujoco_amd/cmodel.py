@@ -7,18 +7,19 @@ Kept field-for-field identical to the C header; ``tests/test_model.py`` checks
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
 MAGIC = 0x4D504352
-VERSION = 7
+VERSION = 8  # v8: the support start table at MPCR_LUT_R = 128
 
 MAX_BODY, MAX_JNT, MAX_DOF, MAX_NQ = 48, 40, 32, 48
 MAX_GEOM, MAX_SITE, MAX_PAIR, MAX_EQ = 128, 24, 768, 8
 MAX_SLOT, MAX_CTRL, MAX_ACT = 512, 8, 16
 MAX_HULLV, MAX_HULLA = 8192, 49152
 MAX_TEN = 4
-LUT_R = 16
+LUT_R = int(os.environ.get("MPCR_LUT_R", 128))  # the support start table resolution (mpcr_model.h MPCR_LUT_R)
 MAX_HULLLUT = 24 * 6 * LUT_R * LUT_R
 MAX_FACE, MAX_FACEV, MAX_VFACE, FACE_MAXV = 12288, 49152, 65536, 16
 
@@ -152,6 +153,28 @@ def lut_cell_dirs(R=LUT_R):
     return out.reshape(-1, 3)
 
 
+_LUT_CACHE = {}
+
+
+def _hull_lut(v, R):
+    """Per cell of the cube map the vertex of v extreme along the cell centre
+    (lowest index on ties), directions in chunks (R = 128: 98 304 cells); the
+    same hull at the same resolution is computed once per process."""
+    key = (R, v.shape, v.tobytes())
+    hit = _LUT_CACHE.get(key)
+    if hit is not None:
+        return hit
+    dirs = lut_cell_dirs(R)
+    out = np.empty(len(dirs), dtype=np.int64)
+    step = max(1, (1 << 22) // max(1, len(v)))
+    for c0 in range(0, len(dirs), step):
+        out[c0:c0 + step] = np.argmax(dirs[c0:c0 + step] @ v.T, axis=1)
+    if len(_LUT_CACHE) > 64:
+        _LUT_CACHE.clear()
+    _LUT_CACHE[key] = out
+    return out
+
+
 def hull_luts(m):
     """geom_lutadr, hull_lut: per hull and cell the vertex extreme along the
     cell centre (lowest index on ties; any vertex is a valid climb start)."""
@@ -163,13 +186,12 @@ def hull_luts(m):
     if int(getattr(m, "nhullv", 0)) == 0:
         return adr, np.zeros(0, dtype=np.int64)
     verts = np.asarray(m.hull_vert, dtype=np.float64).reshape(-1, 3)
-    dirs = lut_cell_dirs()
     for g in range(ng):
         if hadr[g] < 0 or hnum[g] <= 0:
             continue
         v = verts[hadr[g]:hadr[g] + hnum[g]]
         adr[g] = sum(len(x) for x in lut)
-        lut.append(hadr[g] + np.argmax(dirs @ v.T, axis=1))
+        lut.append(hadr[g] + _hull_lut(v, LUT_R))
     return adr, (np.concatenate(lut) if lut else np.zeros(0, dtype=np.int64))
 
 

@@ -862,8 +862,10 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
       (void)g;
       return true;
     };
-    std::vector<float4> hl(MPCR_MAX_HULLLUT);
     int nlut = 0;
+    for (int g = 0; g < h.ngeom; g++)
+      if (h.geom_hulladr[g] >= 0 && h.geom_hullnum[g] > 0) nlut = std::max(nlut, h.geom_lutadr[g] + 6 * MPCR_LUT_R * MPCR_LUT_R);
+    std::vector<float4> hl(nlut > 0 ? nlut : 1);
     for (int g = 0; g < h.ngeom; g++)
       if (h.geom_hulladr[g] >= 0 && h.geom_hullnum[g] > 0) {
         const int la = h.geom_lutadr[g], nc = 6 * MPCR_LUT_R * MPCR_LUT_R;
@@ -872,7 +874,6 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
           hl[la + c] = rec(v);
           if (cell_exact(g, c, v)) hl[la + c].w = bitsf(v | 0x8000 | (h.hull_adjnum[v] << 16));
         }
-        nlut = std::max(nlut, la + nc);
       }
     if (hipMalloc(&e->d_hull_lut, sizeof(float4) * (nlut ? nlut : 1)) != hipSuccess ||
         (nlut && hipMemcpy(e->d_hull_lut, hl.data(), sizeof(float4) * nlut, hipMemcpyHostToDevice) != hipSuccess)) {

@@ -27,7 +27,8 @@ def build(force: bool = False) -> str:
     """liboracle.so (fp64, the checker) and liboracle_f32.so (the same source
     in float: bench.py's cpu_baseline and the parity bar's fp32 probe)."""
     path = os.path.join(_HERE, "liboracle.so")
-    srcs = [os.path.join(_HERE, f) for f in ("mpcr_oracle.c", "oracle_f32.c")]
+    srcs = [os.path.join(_HERE, f) for f in ("mpcr_oracle.c", "oracle_f32.c")] + [
+        os.path.join(os.path.dirname(_HERE), "include", "mpcr_model.h")]
     outs = [path, os.path.join(_HERE, "liboracle_f32.so")]
     newest = max(os.path.getmtime(f) for f in srcs)
     if force or any(not os.path.exists(o) or os.path.getmtime(o) < newest for o in outs):

@@ -58,7 +58,7 @@ def test_table_layout_and_extremes(dual_arm):
 def test_packed_struct_carries_the_table(dual_arm):
     s = dual_arm.to_struct()
     adr, lut = cmodel.hull_luts(dual_arm)
-    assert s.version == cmodel.VERSION == 7
+    assert s.version == cmodel.VERSION == 8  # v8: MPCR_LUT_R = 128
     got_adr = np.ctypeslib.as_array(s.geom_lutadr)[:int(dual_arm.ngeom)]
     assert (got_adr == adr).all()
     assert (np.ctypeslib.as_array(s.hull_lut)[:lut.size] == lut).all()
