@@ -278,8 +278,16 @@ static_assert(sizeof(SmemN2) <= 152448 / 8, "two-wave narrow image: 8 blocks per
 using SmemW = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT>;
 // The two-wave dual-arm image (MPCR_W_WPC2 builds, small batches): the
 // dynamics scratch beside the contact / constraint arrays
-using SmemW2 = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W_JL, 1, MPCR_W_MAXACT, true>;
-static_assert(sizeof(SmemW2) <= 152448 / 4, "two-wave dual-arm image: 4 blocks per CU");
+// and, since it runs at most 4 blocks per CU (<= 1024 candidates on 256
+// CUs: 40 960 B each of the CU's 160 KB), J rows 0..103 in LDS instead of
+// 0..43 (round 5): the rows past 44 -- a dual-arm step has 51 on average,
+// p50 of a candidate's busiest step 60 -- were dependent L2 / HBM-slab loads
+// inside Newton's row loops.  Same values in the same order: bitwise.
+#ifndef MPCR_W2_JL
+#define MPCR_W2_JL 104
+#endif
+using SmemW2 = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W2_JL, 1, MPCR_W_MAXACT, true>;
+static_assert(sizeof(SmemW2) <= 163840 / 4, "two-wave dual-arm image: 4 blocks per CU");
 static_assert(sizeof(PolyScratchT<SmemW2::PMAXW>) + 2 * WAVE * 4 <= SmemW2::DYN_FLOATS * 4,
               "the dynamics wave's manifold scratch and the flush counts inside the dynamics region");
 static_assert(offsetof(SmemW, satsep) - offsetof(SmemW, polyw) == offsetof(PolyScratchT<SmemW::PMAXW>, satsep),
