@@ -2614,6 +2614,11 @@ __device__ __forceinline__ mfx4 mm16(AF&& af, BF&& bf, mfx4 acc, int lane) {
 #ifndef MPCR_MFMA_HESS_W
 #define MPCR_MFMA_HESS_W 1
 #endif
+// two waves per candidate, dual-arm class: wave 1 builds each Newton
+// iteration's Hessian while wave 0 forms J^T f, the gradient and the stop test
+#ifndef MPCR_W2_HESS
+#define MPCR_W2_HESS 1
+#endif
 // The dual-arm variant is compiled for 2 waves/SIMD (<= 256 registers incl.
 // AGPRs; uncapped it took 274 and ran 1 wave/SIMD): with its 21.6 KB image,
 // 7 blocks per CU instead of 4 (dual arm 4096 x 50: 47.5 -> 35.8 ms).
@@ -2790,6 +2795,75 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     } else {
       return dotN<NVW>(s.M[i], vec);
     }
+  };
+  // Newton Hessian H = M + J^T D_active J (+ the cone blocks) into Hs: lane
+  // (row i, column quads q, q + RPW, ...) builds QPL float4s of row i, written
+  // as LDS rows.  Wave 0's Newton step, or -- two waves, dual-arm class --
+  // wave 1's, while wave 0 forms J^T f, the gradient and the stop test.
+  auto newton_hessian = [&](int nefc, float* Hs) {
+    constexpr bool MFMA_HESS_W = NVW == 32 && S::CPW == 1 && MPCR_MFMA_HESS_W;
+    constexpr int RPW = S::HL / NVW;
+    constexpr int QPL = NVW / 4 / RPW;
+    const int gi = lane & (NVW - 1), gq = lane >> S::LOG_NVW;
+    float4 hq[QPL];
+#pragma unroll
+    for (int k = 0; k < QPL; k++) hq[k] = m_quad(gi, gq + RPW * k);
+    if constexpr (MFMA_HESS_W) {
+      // J^T D J on v_mfma_f32_32x32x2_f32: accumulator register 4k + e of
+      // lane (gi, gq) is H[gi][4 (gq + 2k) + e] in the transposed view --
+      // exactly hq[k].e, the VALU build's ownership, and the same products
+      // in the same row order (bitwise the VALU H)
+      mfx16 acc;
+#pragma unroll
+      for (int k = 0; k < QPL; k++) {
+        acc[4 * k] = hq[k].x; acc[4 * k + 1] = hq[k].y; acc[4 * k + 2] = hq[k].z; acc[4 * k + 3] = hq[k].w;
+      }
+      acc = mfma_rows32(s, gx, nefc, gi, gq, [&](int r, float a) { return s.efc_Da[r] * a; }, acc);
+#pragma unroll
+      for (int k = 0; k < QPL; k++) hq[k] = make_float4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
+    } else {
+      jrows(s, gx, 0, 1, nefc, [&](const float* J, int r) {
+        const float c = s.efc_Da[r] * J[gi];
+#pragma unroll
+        for (int k = 0; k < QPL; k++) {
+          const float4 v = reinterpret_cast<const float4*>(J)[gq + RPW * k];
+          hq[k].x = fmaf(c, v.x, hq[k].x); hq[k].y = fmaf(c, v.y, hq[k].y);
+          hq[k].z = fmaf(c, v.z, hq[k].z); hq[k].w = fmaf(c, v.w, hq[k].w);
+        }
+      });
+    }
+    if constexpr (S::WIDE) {  // cone Hessian blocks J_c^T H_c J_c (wave-uniform loop)
+      if (m->cone == 1)
+        for (int r = 0; r < nefc; r++) {
+          const int src = s.efc_src[r];
+          if (!ell_head(src)) continue;
+          const int p = ell_pair(src);
+          const float x[3] = {s.efc_jar[r], s.efc_jar[r + 1], s.efc_jar[r + 2]};
+          const float D[3] = {s.efc_D[r], s.efc_D[r + 1], s.efc_D[r + 2]};
+          float f[3], h[6];
+          cone_update(x, m->pair_cmu[p], m->pair_friction[p], D, f, h);
+          const float* J0 = jrow_ptr(s, gx, r);
+          const float* J1 = jrow_ptr(s, gx, r + 1);
+          const float* J2 = jrow_ptr(s, gx, r + 2);
+          const float j0 = J0[gi], j1 = J1[gi], j2 = J2[gi];
+          const float c0 = h[0] * j0 + h[1] * j1 + h[2] * j2;
+          const float c1 = h[1] * j0 + h[3] * j1 + h[4] * j2;
+          const float c2 = h[2] * j0 + h[4] * j1 + h[5] * j2;
+#pragma unroll
+          for (int k = 0; k < QPL; k++) {
+            const float4 v0 = reinterpret_cast<const float4*>(J0)[gq + RPW * k];
+            const float4 v1 = reinterpret_cast<const float4*>(J1)[gq + RPW * k];
+            const float4 v2 = reinterpret_cast<const float4*>(J2)[gq + RPW * k];
+            hq[k].x += c0 * v0.x + c1 * v1.x + c2 * v2.x;
+            hq[k].y += c0 * v0.y + c1 * v1.y + c2 * v2.y;
+            hq[k].z += c0 * v0.z + c1 * v1.z + c2 * v2.z;
+            hq[k].w += c0 * v0.w + c1 * v1.w + c2 * v2.w;
+          }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < QPL; k++) reinterpret_cast<float4*>(Hs + gi * S::LD)[gq + RPW * k] = hq[k];
+    sync();
   };
 
   // ---- rollout init: template state, qpos[:nctrl] = init_pos ----------------
@@ -3676,6 +3750,8 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     // sources, offsets -- computed identically on both), and wave 1 leaves at
     // the barrier that follows; same values in the same places as one wave
     const bool rows_j = WPC == 2 && S::WIDE && !rows_c;
+    // ... and wave 1 then builds the Newton Hessians (round 5)
+    const bool hess2 = MPCR_W2_HESS && rows_j && NVW == 32 && S::CPW == 1;
     const int rl0 = rows_j ? wv * S::HL : 0, rls = rows_j ? 2 * S::HL : S::HL;
     if constexpr (WPC == 2) {
       if (!rows_c) {
@@ -3967,8 +4043,25 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     }  // constraint rows
     if constexpr (WPC == 2) {
       if (rows_j) {
-        block_sync();  // the rows are ready; wave 1 waits for the next step's geom poses
-        if (!run_main) continue;
+        block_sync();  // the rows are ready
+        if (!run_main) {
+          // wave 1: each Newton iteration's Hessian (two barriers per
+          // iteration, the same count as wave 0's loop), then it waits for
+          // the next step's geom poses
+          STAMP(8);
+          const int nefc = s.nefc;
+          if (hess2 && nefc > 0)
+            for (int it = 0; it < m->iterations; it++) {
+              block_sync();  // wave 0: efc_Da / efc_jar of this iteration
+              STAMP(29);
+              newton_hessian(nefc, &s.gxpos[0][0]);
+              STAMP(31);
+              block_sync();  // wave 0: gradient and stop test
+              STAMP(30);
+              if (s.pad_) break;
+            }
+          continue;
+        }
       }
       if (rows_c) {
         if (run_coll && lane == 0) s.pad_ = coupled ? 1 : 0;
@@ -4078,6 +4171,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           const float gauss = hsum<S::CPW>(lane < nv ? (ma - s.qfs[lane]) * (s.qacc[lane] - s.qas[lane]) : 0.f);
           const float cost = 0.5f * gauss + 0.5f * hsum<S::CPW>(cc);
           sync();
+          if (hess2) block_sync();  // this iteration's active set, to wave 1
           STAMP(29);
           constexpr bool MFMA_HESS = NVW == 16 && S::CPW == 1 && MPCR_MFMA_HESS;
           constexpr bool MFMA_HESS_W = NVW == 32 && S::CPW == 1 && MPCR_MFMA_HESS_W;
@@ -4144,73 +4238,15 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           // of the cost is rounding noise (without it fp32 iterates on noise
           // where the fp64 solve has converged: 3.9 vs 1.9 iterations per
           // dual-arm step)
-          if (scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance ||
-              prev_cost - cost <= 1e-6f * fabsf(cost))
-            break;
+          const bool stop = scale * (prev_cost - cost) < m->tolerance || scale * gn < m->tolerance ||
+                            prev_cost - cost <= 1e-6f * fabsf(cost);
+          if (hess2) {  // hand the decision to wave 1, take its Hessian
+            if (lane == 0) s.pad_ = stop ? 1 : 0;
+            block_sync();
+          }
+          if (stop) break;
           if constexpr (!MFMA_HESS) {
-            // Hessian H = M + J^T D_active J: lane (row i, column quads q, q + RPW,
-            // ...) builds QPL float4s of row i; rows are gathered to lanes
-            // 0..NVW-1 through LDS
-            constexpr int QPL = NVW / 4 / RPW;
-            float4 hq[QPL];
-#pragma unroll
-            for (int k = 0; k < QPL; k++) hq[k] = m_quad(gi, gq + RPW * k);
-            if constexpr (MFMA_HESS_W) {
-              // J^T D J on v_mfma_f32_32x32x2_f32: accumulator register 4k + e of
-              // lane (gi, gq) is H[gi][4 (gq + 2k) + e] in the transposed view --
-              // exactly hq[k].e, the VALU build's ownership, and the same
-              // products in the same row order (bitwise the VALU H)
-              mfx16 acc;
-#pragma unroll
-              for (int k = 0; k < QPL; k++) {
-                acc[4 * k] = hq[k].x; acc[4 * k + 1] = hq[k].y; acc[4 * k + 2] = hq[k].z; acc[4 * k + 3] = hq[k].w;
-              }
-              acc = mfma_rows32(s, gx, nefc, gi, gq, [&](int r, float a) { return s.efc_Da[r] * a; }, acc);
-#pragma unroll
-              for (int k = 0; k < QPL; k++) hq[k] = make_float4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
-            } else {
-              jrows(s, gx, 0, 1, nefc, [&](const float* J, int r) {
-                const float c = s.efc_Da[r] * J[gi];
-#pragma unroll
-                for (int k = 0; k < QPL; k++) {
-                  const float4 v = reinterpret_cast<const float4*>(J)[gq + RPW * k];
-                  hq[k].x = fmaf(c, v.x, hq[k].x); hq[k].y = fmaf(c, v.y, hq[k].y);
-                  hq[k].z = fmaf(c, v.z, hq[k].z); hq[k].w = fmaf(c, v.w, hq[k].w);
-                }
-              });
-            }
-            if constexpr (S::WIDE) {  // cone Hessian blocks J_c^T H_c J_c (wave-uniform loop)
-              if (m->cone == 1)
-                for (int r = 0; r < nefc; r++) {
-                  const int src = s.efc_src[r];
-                  if (!ell_head(src)) continue;
-                  const int p = ell_pair(src);
-                  const float x[3] = {s.efc_jar[r], s.efc_jar[r + 1], s.efc_jar[r + 2]};
-                  const float D[3] = {s.efc_D[r], s.efc_D[r + 1], s.efc_D[r + 2]};
-                  float f[3], h[6];
-                  cone_update(x, m->pair_cmu[p], m->pair_friction[p], D, f, h);
-                  const float* J0 = jrow_ptr(s, gx, r);
-                  const float* J1 = jrow_ptr(s, gx, r + 1);
-                  const float* J2 = jrow_ptr(s, gx, r + 2);
-                  const float j0 = J0[gi], j1 = J1[gi], j2 = J2[gi];
-                  const float c0 = h[0] * j0 + h[1] * j1 + h[2] * j2;
-                  const float c1 = h[1] * j0 + h[3] * j1 + h[4] * j2;
-                  const float c2 = h[2] * j0 + h[4] * j1 + h[5] * j2;
-#pragma unroll
-                  for (int k = 0; k < QPL; k++) {
-                    const float4 v0 = reinterpret_cast<const float4*>(J0)[gq + RPW * k];
-                    const float4 v1 = reinterpret_cast<const float4*>(J1)[gq + RPW * k];
-                    const float4 v2 = reinterpret_cast<const float4*>(J2)[gq + RPW * k];
-                    hq[k].x += c0 * v0.x + c1 * v1.x + c2 * v2.x;
-                    hq[k].y += c0 * v0.y + c1 * v1.y + c2 * v2.y;
-                    hq[k].z += c0 * v0.z + c1 * v1.z + c2 * v2.z;
-                    hq[k].w += c0 * v0.w + c1 * v1.w + c2 * v2.w;
-                  }
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < QPL; k++) reinterpret_cast<float4*>(Hs + gi * S::LD)[gq + RPW * k] = hq[k];
-            sync();
+            if (!hess2) newton_hessian(nefc, Hs);  // (two waves: wave 1 built it meanwhile)
           }
           STAMP(31);
           float mg;
