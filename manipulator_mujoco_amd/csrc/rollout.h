@@ -110,6 +110,10 @@ struct RolloutArgs {
 #ifndef MPCR_W_MC_ROWS
 #define MPCR_W_MC_ROWS 24
 #endif
+// faces per lane per pass of that scan (their loads in flight together)
+#ifndef MPCR_ALLF_U
+#define MPCR_ALLF_U 2
+#endif
 constexpr float POLY_DEEP = 5e-3f;
 constexpr int POLY_ALLF = MPCR_POLY_ALLF > 0 ? MPCR_POLY_ALLF : 1;
 constexpr bool POLY_ALLF_ON = MPCR_POLY_ALLF > 0;

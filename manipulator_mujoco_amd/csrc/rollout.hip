@@ -1225,6 +1225,13 @@ __device__ __forceinline__ int support_vertex(const DevModel* __restrict__ m, co
 // world outward normal of face f of geom g and its plane offset relative to
 // c (nw . (x - c) = off on the face)
 template <class S>
+__device__ __forceinline__ void face_rel_fp(const S& s, int g, const float4 fp, const float* c, float nw[3],
+                                            float& off) {
+  const float nl[3] = {fp.x, fp.y, fp.z};
+  mv(nw, s.gxmat[g], nl);
+  off = fp.w + nw[0] * (s.gxpos[g][0] - c[0]) + nw[1] * (s.gxpos[g][1] - c[1]) + nw[2] * (s.gxpos[g][2] - c[2]);
+}
+template <class S>
 __device__ __forceinline__ void face_rel(const DevModel* __restrict__ m, const S& s, int g, int f, const float* c,
                                          float nw[3], float& off) {
   const float4 fp = m->face_plane[f];
@@ -1298,25 +1305,49 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, const S& s, PS& ps, con
   if (allf) {
     // SAT separation of every face (lane = face, rounds of 64) into LDS,
     // the wave max, then the lowest face index within the max's tie band
+    // (MPCR_ALLF_U faces per lane per pass: their face-plane loads, then
+    // their support queries' first loads, in flight together -- a pass was
+    // two dependent load latencies per 64 faces, up to 8 passes in turn)
     const int fa1 = m->geom_faceadr[g1], fa2 = m->geom_faceadr[g2], nf = nf1 + nf2;
-    float mxa = -3e38f;
+    constexpr int U = MPCR_ALLF_U;
+    float mxl = -3e38f;  // this lane's maximum (the wave max below: max is exact in any order)
 #pragma unroll 1
-    for (int b0 = 0; b0 < nf; b0 += WAVE) {
-      const int k = b0 + lane;
-      float sp = -3e38f;
-      if (k < nf) {
-        const bool two = k >= nf1;
-        const int g = two ? g2 : g1, go = two ? g1 : g2, f = two ? fa2 + k - nf1 : fa1 + k;
-        float nw[3], off, pt[3];
-        face_rel(m, s, g, f, c, nw, off);
-        const float mn[3] = {-nw[0], -nw[1], -nw[2]};
-        int h = two ? h0 : h1;
-        support_geom(m, s, go, mn, pt, h, c);
-        sp = nw[0] * pt[0] + nw[1] * pt[1] + nw[2] * pt[2] - off;
-        ps.satsep[k] = sp;
+    for (int b0 = 0; b0 < nf; b0 += U * WAVE) {
+      float4 fp[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int k = b0 + u * WAVE + lane;
+        fp[u] = make_float4(0.f, 0.f, 1.f, 0.f);
+        if (k < nf) fp[u] = m->face_plane[k >= nf1 ? fa2 + k - nf1 : fa1 + k];
       }
-      mxa = fmaxf(mxa, wmax(sp));
+      SupQ q[U];
+      float nw[U][3], off[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int k = b0 + u * WAVE + lane;
+        if (k < nf) {
+          const bool two = k >= nf1;
+          const int g = two ? g2 : g1, go = two ? g1 : g2;
+          face_rel_fp(s, g, fp[u], c, nw[u], off[u]);
+          const float mn[3] = {-nw[u][0], -nw[u][1], -nw[u][2]};
+          sup_start(m, s, go, mn, two ? h0 : h1, q[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int k = b0 + u * WAVE + lane;
+        if (k < nf) {
+          const bool two = k >= nf1;
+          float pt[3];
+          int h = two ? h0 : h1;
+          sup_finish(m, s, two ? g1 : g2, q[u], pt, h, c);
+          const float sp = nw[u][0] * pt[0] + nw[u][1] * pt[1] + nw[u][2] * pt[2] - off[u];
+          ps.satsep[k] = sp;
+          mxl = fmaxf(mxl, sp);
+        }
+      }
     }
+    const float mxa = wmax(mxl);
     sync();
     // the key 2 f + side keeps the side with the face: two geoms of one mesh
     // share their face range, and on equal faces g1's wins, the
