@@ -294,6 +294,18 @@ using SmemW2 = SmemT<32, 32, 72, 8 + 4 * MPCR_W_MAXACT, 36, true, MPCR_W2_JL, 1,
 static_assert(sizeof(SmemW2) <= 163840 / 4, "two-wave dual-arm image: 4 blocks per CU");
 static_assert(sizeof(PolyScratchT<SmemW2::PMAXW>) + 2 * WAVE * 4 <= SmemW2::DYN_FLOATS * 4,
               "the dynamics wave's manifold scratch and the flush counts inside the dynamics region");
+// the two-wave lead flush (rollout.hip): at most W2_LEAD_MAX convex pairs in
+// the step's list (else the dealt flush), a manifold-queue record of
+// W2_JOB_REC ints per job inside the convex-pair list, and wave 0's results
+// (4 distances, points, normals, the count) W2_JOB_OUT floats per job in the
+// dynamics region after its manifold scratch
+#ifndef MPCR_W2_LEAD
+#define MPCR_W2_LEAD 1
+#endif
+constexpr int W2_LEAD_MAX = 56, W2_JOB_REC = 8, W2_JOB_OUT = 29;
+static_assert(W2_LEAD_MAX <= WAVE && 2 + W2_JOB_REC * W2_LEAD_MAX <= SmemW2::CVXN, "manifold queue inside the list");
+static_assert(sizeof(PolyScratchT<SmemW2::PMAXW>) + 4 * W2_JOB_OUT * W2_LEAD_MAX <= SmemW2::DYN_FLOATS * 4,
+              "wave 0's manifold mailbox inside the dynamics region");
 static_assert(offsetof(SmemW, satsep) - offsetof(SmemW, polyw) == offsetof(PolyScratchT<SmemW::PMAXW>, satsep),
               "the image's manifold scratch has PolyScratchT's layout");
 static_assert(SmemN::NGW * 16 >= SmemN::NVW * SmemN::LD + SmemN::NVW, "Hessian + J^T f scratch");

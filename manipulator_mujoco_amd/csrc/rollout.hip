@@ -3702,13 +3702,101 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       //      the flush on the collision wave (cost_c accumulates per lane).
       const bool split = WPC == 2 && m->cvx_joint;
       const bool mine = WPC == 1 || split || wv == 1;
-      if constexpr (WPC == 2) block_sync();  // the list is complete; the dynamics are done
       PolyScratchT<S::PMAXW>* const psc = reinterpret_cast<PolyScratchT<S::PMAXW>*>(
           (WPC == 2 && wv == 0) ? &s.xpos[0][0] : &s.polyw[0][0][0]);
       int* const jcnt = reinterpret_cast<int*>(&s.xpos[0][0]) + sizeof(PolyScratchT<S::PMAXW>) / 4;
+      // Lead flush (two waves, round 5): with at most W2_LEAD_MAX pairs in the
+      // list, the collision wave runs every pair's MPR (one lane each) as soon
+      // as its list is complete -- while wave 0 still runs the dynamics --
+      // and queues the polyhedron manifolds; after the hand-over both waves
+      // take manifolds from the queue (an LDS counter), wave 0 returning its
+      // results through a mailbox in the dead dynamics region, and the
+      // collision wave emits the contacts in pair order.  Each pair's MPR and
+      // manifold are the same instructions on the same data wherever they
+      // run: bitwise the one-wave kernel.
+      int* const jq = reinterpret_cast<int*>(&s.cvx[0]);  // [0] next job, [1] jobs, records from [2]
+      float* const mbox = reinterpret_cast<float*>(jcnt);  // wave 0's manifold results, W2_JOB_OUT floats per job
+      int lpc = 0, ljob = 0, lsl = 0;
+      float ld[4] = {1e30f, 1e30f, 1e30f, 1e30f}, lp[4][3] = {}, ln[4][3] = {};
+      if (MPCR_W2_LEAD && split && wv == 1 && s.ncvx <= W2_LEAD_MAX) {
+        const bool v = lane < s.ncvx;
+        lpc = v ? s.cvx[lane] : 0;
+        lsl = v ? narrow_lane(m, s, hx, lpc, ld, lp, ln, (args.dbg && b == 0 && t == H - 1) ? args.dbg : nullptr)
+                : 0;
+        STAMP(21);
+        for (unsigned long long pm = __ballot(lsl == kPendingManifold); pm; pm &= pm - 1) {
+          const int q = __builtin_ctzll(pm);
+          const int pq = __shfl(lpc, q);
+          const float dq = __shfl(ld[0], q);
+          const int gp = m->pair_g1[pq];
+          const float* Rp = s.gxmat[gp];
+          const float nq[3] = {Rp[2], Rp[5], Rp[8]};
+          plane_mesh_manifold_wave(m, s, m->pair_g2[pq], nq, s.gxpos[gp], -dq, q, lane, ld, lp, ln, lsl);
+        }
+        STAMP(22);
+        // the manifold queue: (pair | lane << 16, MPR depth, normal, point) per job
+        const unsigned long long pm = __ballot(lsl == kPendingPoly);
+        ljob = lanes_below(pm);
+        if (lsl == kPendingPoly) {
+          int* r = jq + 2 + W2_JOB_REC * ljob;
+          r[0] = lpc | (lane << 16);
+          r[1] = __float_as_int(ld[0]);
+#pragma unroll
+          for (int e = 0; e < 3; e++) { r[2 + e] = __float_as_int(ln[0][e]); r[5 + e] = __float_as_int(lp[0][e]); }
+        }
+        if (lane == 0) { jq[0] = 0; jq[1] = __popcll(pm); }
+      }
+      if constexpr (WPC == 2) block_sync();  // the list is complete; the dynamics are done
       const int ncv = s.ncvx, rstep = split ? 2 * WAVE : WAVE;
+      const bool lead = MPCR_W2_LEAD && split && ncv <= W2_LEAD_MAX;
       int ncon_w = s.ncon;
-      for (int i0 = 0; i0 < ncv; i0 += rstep) {
+      if (lead) {
+        const int njob = jq[1];
+        for (;;) {
+          int j = 0;
+          if (lane == 0) j = __hip_atomic_fetch_add(jq, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          j = __builtin_amdgcn_readfirstlane(j);
+          if (j >= njob) break;
+          const int* r = jq + 2 + W2_JOB_REC * j;
+          const int pq = r[0] & 0xffff, q = r[0] >> 16;
+          const float dq = __int_as_float(r[1]);
+          const float nq[3] = {__int_as_float(r[2]), __int_as_float(r[3]), __int_as_float(r[4])};
+          if (wv == 0) {  // lane q stands in for the collision wave's lane q
+            lsl = lane == q ? kPendingPoly : 0;
+            ld[0] = dq; ld[1] = ld[2] = ld[3] = 1e30f;
+#pragma unroll
+            for (int e = 0; e < 3; e++) { ln[0][e] = nq[e]; lp[0][e] = __int_as_float(r[5 + e]); }
+          }
+          poly_manifold_wave(m, s, *psc, hx, pq, nq, -dq, q, lane, ld, lp, ln, lsl);
+          if (wv == 0 && lane == q) {
+            float* o = mbox + W2_JOB_OUT * j;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+              o[c] = ld[c];
+#pragma unroll
+              for (int e = 0; e < 3; e++) { o[4 + 3 * c + e] = lp[c][e]; o[16 + 3 * c + e] = ln[c][e]; }
+            }
+            o[28] = __int_as_float(lsl);
+          }
+        }
+        STAMP(17);
+        block_sync();  // every manifold done
+        if (wv == 1) {
+          if (lsl == kPendingPoly) {  // run by wave 0
+            const float* o = mbox + W2_JOB_OUT * ljob;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+              ld[c] = o[c];
+#pragma unroll
+              for (int e = 0; e < 3; e++) { lp[c][e] = o[4 + 3 * c + e]; ln[c][e] = o[16 + 3 * c + e]; }
+            }
+            lsl = __float_as_int(o[28]);
+          }
+          emit_contacts(m, s, args, b, t, H, lane < ncv, lpc, lsl, ld, lp, ln, cost_c, shist, -1);
+        }
+        STAMP(18);
+      }
+      for (int i0 = 0; !lead && i0 < ncv; i0 += rstep) {
 #ifdef MPCR_WAVETIME
         wt_cvx++;
 #endif
@@ -3760,7 +3848,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
         }
         STAMP(18);
       }
-      if (split && run_coll && lane == 0) s.ncon = ncon_w;
+      if (split && !lead && run_coll && lane == 0) s.ncon = ncon_w;
       sync();
       if (run_coll && s.ncon > S::MAXACT) {
         status |= 1;
