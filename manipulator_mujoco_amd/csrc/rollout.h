@@ -173,6 +173,7 @@ struct __align__(16) SmemT {
   float tenp[WIDE ? DX_NTEN : 1][2][4];  // spatial-tendon sites in world
   float actf[NACT];       // actuator forces
   int ncon, nefc, ncvx, pad_;
+  int ctok_[SPLIT_ ? 4 : 0];  // two-wave images: [0] the step whose pair cull is done (rollout.hip, swap mode)
   // ---- phase-local: dynamics (kinematics .. mass matrix) overlays the
   //      contact / constraint arrays (collision .. Newton) ----
   union {
@@ -301,6 +302,10 @@ static_assert(sizeof(PolyScratchT<SmemW2::PMAXW>) + 2 * WAVE * 4 <= SmemW2::DYN_
 // dynamics region after its manifold scratch
 #ifndef MPCR_W2_LEAD
 #define MPCR_W2_LEAD 1
+#endif
+// swap mode (rollout.hip): wave 0 runs the non-convex narrow phase
+#ifndef MPCR_W2_SWAP
+#define MPCR_W2_SWAP 1
 #endif
 constexpr int W2_LEAD_MAX = 56, W2_JOB_REC = 8, W2_JOB_OUT = 29;
 static_assert(W2_LEAD_MAX <= WAVE && 2 + W2_JOB_REC * W2_LEAD_MAX <= SmemW2::CVXN, "manifold queue inside the list");

@@ -2902,6 +2902,8 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
   const bool from_state = (args.plant & 1) != 0;
   if (run_main) {  // (WPC = 2: wave 0 sets the image up, wave 1 waits at the barrier below)
   if (lane < PAR_N) s.par[lane] = args.dpar ? args.dpar[lane] : args.par[lane];
+  if constexpr (S::SPLIT)
+    if (lane == 0) s.ctok_[0] = 0;  // no step's pair cull posted yet
   if constexpr (S::WIDE) {
     // a rollout starts its hull climbs afresh; the plant keeps them across
     // steps (reset by mpcr_plant_set_state), so k plant steps = a k-step rollout
@@ -3613,18 +3615,45 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     PACE_SETPRIO();
 #endif
     LAUNDER_PHASE();  // phase boundary: no cross-phase model-load CSE
-    if (run_coll) {  // ---- wave 1 (WPC = 2), concurrently with wave 0's dynamics
+    // Swap mode (two waves, dual-arm class without cost slots, round 5): the
+    // collision wave only culls the pairs and lists the convex ones, posts
+    // the list (an LDS step token, no barrier) and goes on to their MPRs (the
+    // lead flush below); wave 0, after the dynamics, runs the other pairs'
+    // narrow phase, so both waves reach the manifold queue together.  The
+    // contacts keep the one-wave order (these pairs' first, chunk by chunk,
+    // then the convex ones).  With more convex pairs than the lead flush
+    // takes, the collision wave runs that narrow phase itself, as before.
+    const bool swapm = WPC == 2 && S::WIDE && MPCR_W2_SWAP && MPCR_W2_LEAD && m->cvx_joint && m->nslot == 0;
+    for (int pass = 0; pass < 2 && (run_coll || swapm); pass++) {
+    bool do_list = false, do_narrow = false;
+    if (run_coll) {
+      if (pass == 0) { do_list = true; do_narrow = !swapm; }
+      else do_narrow = swapm && s.ncvx > W2_LEAD_MAX;
+    } else if (pass == 1) {  // wave 0 (swap mode): the list is posted for this step
+      if constexpr (S::SPLIT) {  // (bounded: a lost post flags the candidate instead of hanging the launch)
+        int guard = 0;
+        while (__hip_atomic_load(&s.ctok_[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t + 1 &&
+               ++guard < (1 << 22))
+          __builtin_amdgcn_s_sleep(1);
+        if (guard >= (1 << 22)) status |= 2;  // (reported as a failed rollout)
+      }
+      do_narrow = s.ncvx <= W2_LEAD_MAX;
+    }
+    if (do_list || do_narrow) {
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
     //      slots; active contacts compacted into the list; box-box pairs
     //      that pass the bounding-sphere cull are solved wave-cooperatively
-    if (lane == 0) { s.ncon = 0; s.ncvx = 0; }
-    sync();
+    if (do_list) {
+      if (lane == 0) { s.ncon = 0; s.ncvx = 0; }
+      sync();
+    }
     for (int k = 0; k * S::HL < m->npair; k++) {
       const int p = lane + k * S::HL;
       const bool valid = p < m->npair;
       const int func = valid ? m->pair_func[p] : -1;
-      bool run = valid;
-      if (valid && m->pair_slotadr[p] < 0) {
+      const bool defer = S::WIDE && func >= 9;  // general convex: the list
+      bool run = valid && (defer ? do_list : do_narrow);
+      if (run && m->pair_slotadr[p] < 0) {
         const int g1 = m->pair_g1[p], g2 = m->pair_g2[p];
         const float dx = s.gxpos[g2][0] - s.gxpos[g1][0], dy = s.gxpos[g2][1] - s.gxpos[g1][1],
                     dz = s.gxpos[g2][2] - s.gxpos[g1][2];
@@ -3654,14 +3683,13 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       // general convex pairs (sorted last) that survive the cull are compacted
       // into a list and solved 64 at a time below, instead of leaving most
       // lanes of every 64-pair chunk idle behind a few MPR lanes
-      bool defer = false;
-      if constexpr (S::WIDE) {
-        defer = func >= 9;
+      if (S::WIDE && do_list) {
         const unsigned long long dm = __ballot(defer && run);
         if (defer && run) s.cvx[s.ncvx + lanes_below(dm)] = p;
         sync();
         if (lane == 0) s.ncvx += __popcll(dm);
       }
+      if (!do_narrow) continue;
       float dist[4] = {1e30f, 1e30f, 1e30f, 1e30f}, pos[4][3] = {}, nrm[4][3] = {};
       int nsl = 0;
       if (run && func != 4 && !defer && !(MPCR_ABL_FUNC & (1 << func))) nsl = narrow_lane(m, s, hx, p, dist, pos, nrm);
@@ -3687,7 +3715,14 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
         sync();
       }
     }
-    }  // run_coll
+    }  // do_list || do_narrow
+    if constexpr (S::SPLIT) {
+      if (swapm && run_coll && pass == 0) {  // post the list (every lane's entries first)
+        sync();
+        if (lane == 0) __hip_atomic_store(&s.ctok_[0], t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    }  // pass
     if constexpr (S::WIDE) {
       // ---- the convex flush: every general-convex pair that survived the
       //      cull (the list holds all of a model's, so this is the step's only
@@ -3751,6 +3786,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       const bool lead = MPCR_W2_LEAD && split && ncv <= W2_LEAD_MAX;
       int ncon_w = s.ncon;
       if (lead) {
+        STAMP(16);  // (profile build: wave 0's wait for the queue)
         const int njob = jq[1];
         for (;;) {
           int j = 0;
