@@ -3647,7 +3647,10 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       if (lane == 0) { s.ncon = 0; s.ncvx = 0; }
       sync();
     }
-    for (int k = 0; k * S::HL < m->npair; k++) {
+    // (the general-convex pairs are sorted last, from DevModel::cvx_base: a
+    // list-only pass starts at their chunk, a narrow-only pass ends there)
+    const int k_lo = do_narrow ? 0 : m->cvx_base / S::HL, p_hi = do_list ? m->npair : min(m->npair, m->cvx_base);
+    for (int k = k_lo; k * S::HL < p_hi; k++) {
       const int p = lane + k * S::HL;
       const bool valid = p < m->npair;
       const int func = valid ? m->pair_func[p] : -1;
