@@ -775,18 +775,29 @@ struct SupQ {
   float4 hv, hh;
   int type, la;
 };
+// a geom's per-query constants (type, table, first hull vertex), loaded once
+// per MPR run instead of in front of every support query (MPCR_SUP_GEOMQ)
+#ifndef MPCR_SUP_GEOMQ
+#define MPCR_SUP_GEOMQ 1
+#endif
+struct GeomQ { int type, la, h0; };
+__device__ __forceinline__ GeomQ geom_q(const DevModel* __restrict__ m, int g) {
+  GeomQ q{m->geom_type[g], m->geom_lutadr[g], m->geom_hulladr[g]};
+  asm volatile("" : "+v"(q.type), "+v"(q.la), "+v"(q.h0));  // kept in registers, not re-loaded per query
+  return q;
+}
 template <class S>
 __device__ __forceinline__ void sup_start(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
-                                          int hint, SupQ& q) {
+                                          int hint, SupQ& q, const GeomQ* gq = nullptr) {
   const float* R = s.gxmat[g];
   mtv(q.l, R, dir);
   q.ln = sqrtf(dot3(q.l, q.l));
-  q.type = m->geom_type[g];
+  q.type = gq ? gq->type : m->geom_type[g];
   if (q.type == 7) {
     const float il = q.ln > 0.f ? 1.f / q.ln : 0.f;
     q.lu[0] = q.l[0] * il; q.lu[1] = q.l[1] * il; q.lu[2] = q.l[2] * il;
-    q.la = m->geom_lutadr[g];
-    const int h0 = m->geom_hulladr[g];
+    q.la = gq ? gq->la : m->geom_lutadr[g];
+    const int h0 = gq ? gq->h0 : m->geom_hulladr[g];
     q.hv = q.la >= 0 ? m->hull_lut[q.la + lut_cell(q.l)] : m->hull_vert[h0];
     q.hh = m->hull_vert[hint >= 0 ? hint : h0];
   }
@@ -856,12 +867,13 @@ struct MprPt { float v[3], a[3], b[3]; };
 
 template <class S>
 __device__ __forceinline__ void mpr_support(const DevModel* __restrict__ m, const S& s, int g1, int g2,
-                                            const float dir[3], MprPt& o, int (&hint)[2], float* trace = nullptr) {
+                                            const float dir[3], MprPt& o, int (&hint)[2], float* trace = nullptr,
+                                            const GeomQ* gq = nullptr) {
   const float nd[3] = {-dir[0], -dir[1], -dir[2]};
   SupQ q1, q2;  // both queries' first loads in flight together
   PROF_COUNT(m, 20);
-  sup_start(m, s, g1, dir, hint[0], q1);
-  sup_start(m, s, g2, nd, hint[1], q2);
+  sup_start(m, s, g1, dir, hint[0], q1, gq);
+  sup_start(m, s, g2, nd, hint[1], q2, gq ? gq + 1 : nullptr);
   sup_finish(m, s, g1, q1, o.a, hint[0], s.gxpos[g2]);  // relative to g2's centre
   sup_finish(m, s, g2, q2, o.b, hint[1], s.gxpos[g2]);
   o.v[0] = o.a[0] - o.b[0]; o.v[1] = o.a[1] - o.b[1]; o.v[2] = o.a[2] - o.b[2];
@@ -947,6 +959,12 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   MprPt p[4], v4;
   float va[3], vb[3], dd;
   const float tol = kMprTol;
+#if MPCR_SUP_GEOMQ
+  const GeomQ gqa[2] = {geom_q(m, g1), geom_q(m, g2)};
+  const GeomQ* const gq = gqa;
+#else
+  const GeomQ* const gq = nullptr;
+#endif
   // point x off the plane through the origin with (unnormalised) normal c by more than kMprEps
   auto off_plane = [](float x, const float c[3]) { return fabsf(x) >= kMprEps * sqrtf(dot3(c, c)); };
 #pragma unroll
@@ -958,7 +976,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   if (mpr_zero(p[0].v[0]) && mpr_zero(p[0].v[1]) && mpr_zero(p[0].v[2])) p[0].v[0] += 10.f * kMprEps;
   dir[0] = -p[0].v[0]; dir[1] = -p[0].v[1]; dir[2] = -p[0].v[2];
   nrm3(dir);
-  mpr_support(m, s, g1, g2, dir, p[1], hint, trace);
+  mpr_support(m, s, g1, g2, dir, p[1], hint, trace, gq);
   dd = dot3(p[1].v, dir);
   if (mpr_zero(dd) || dd < 0.f) return false;
   cross(dir, p[0].v, p[1].v);
@@ -979,7 +997,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     }
   }
   nrm3(dir);
-  mpr_support(m, s, g1, g2, dir, p[2], hint, trace);
+  mpr_support(m, s, g1, g2, dir, p[2], hint, trace, gq);
   dd = dot3(p[2].v, dir);
   if (mpr_zero(dd) || dd < 0.f) return false;
 #pragma unroll
@@ -992,7 +1010,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   }
   for (int guard = 0;; guard++) {
     if (guard > kMprIter) return false;
-    mpr_support(m, s, g1, g2, dir, p[3], hint, trace);
+    mpr_support(m, s, g1, g2, dir, p[3], hint, trace, gq);
     dd = dot3(p[3].v, dir);
     if (mpr_zero(dd) || dd < 0.f) return false;
     bool cont = false;
@@ -1016,7 +1034,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
     mpr_dir(p, dir);
     dd = dot3(dir, p[1].v);
     if (mpr_zero(dd) || dd > 0.f) break;
-    mpr_support(m, s, g1, g2, dir, v4, hint, trace);
+    mpr_support(m, s, g1, g2, dir, v4, hint, trace, gq);
     dd = dot3(v4.v, dir);
     if (!(mpr_zero(dd) || dd > 0.f) || mpr_reach(p, v4, dir, tol) || it > kMprIter) return false;
     mpr_expand(p, v4);
@@ -1024,7 +1042,7 @@ __device__ bool mpr_lane(const DevModel* __restrict__ m, const S& s, int g1, int
   for (int it = 0;; it++) {
     if (trace) trace[11] = (float)it;
     mpr_dir(p, dir);
-    mpr_support(m, s, g1, g2, dir, v4, hint, trace);
+    mpr_support(m, s, g1, g2, dir, v4, hint, trace, gq);
     if (mpr_reach(p, v4, dir, tol) || it > kMprIter) break;
     mpr_expand(p, v4);
   }
