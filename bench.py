@@ -204,10 +204,20 @@ def cpu_baseline(m, xi, H, Pd, threads, reps=5, precision="fp32"):
 
 
 def _free_port():
+    """A free port below the ephemeral range (32768..), where no client
+    socket of the ranks can take it before rank 0's rendezvous binds it."""
+    import random
     import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        return p
+    raise RuntimeError("no free port in 20000..32000")
 
 
 def launch_ranks(nproc, argv, grace_s=30.0):

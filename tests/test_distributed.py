@@ -10,11 +10,19 @@ import torch.multiprocessing as mp
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free port below the ephemeral range (a client socket of the spawned
+    ranks can take an ephemeral pick before the rendezvous binds it)."""
+    import random
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        return p
+    raise RuntimeError("no free port in 20000..32000")
 
 
 def _worker(rank, world, port, costs, out):

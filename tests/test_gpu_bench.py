@@ -20,9 +20,20 @@ COMMON = ["--config", "c3", "--scaling", "strong", "--candidates", "512", "--ste
 
 
 def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A free port below the ephemeral range (32768..): an ephemeral pick can
+    be taken, before the rendezvous binds it, by a client socket of the
+    spawned ranks (the Manager connection) -- EADDRINUSE on the box, r05."""
+    import random
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        return p
+    raise RuntimeError("no free port in 20000..32000")
 
 
 def _run(cmd):

@@ -80,11 +80,20 @@ def test_sharded_sampling_equals_full_batch(torch_cuda):
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free port below the ephemeral range (32768..): an ephemeral pick can
+    be taken, before the rendezvous binds it, by a client socket of the
+    spawned ranks (the Manager connection) -- EADDRINUSE on the box, r05."""
+    import random
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        return p
+    raise RuntimeError("no free port in 20000..32000")
 
 
 @pytest.mark.parametrize("graph", [False, True])
