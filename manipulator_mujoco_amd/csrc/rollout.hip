@@ -535,21 +535,29 @@ struct SweepN<N, -1, STEP> {
 // dof-indexed LDS vectors (x may alias b).  Lt: 4 N^2-float LDS scratch (it
 // may alias A's storage: every element is read before the first write).  Must
 // be called by all lanes (two barriers).
+// (split in two for a factor computed ahead of its solve, possibly on
+// another wave: blocked_factor, then blocked_sweep -- the same operations)
 template <int N, class F>
-__device__ __forceinline__ void blocked_solve(const DevModel* __restrict__ m, F&& elem, const float* bv, float* xv,
-                                              int lane, float* Lt) {
+__device__ __forceinline__ void blocked_factor(const DevModel* __restrict__ m, F&& elem, int lane, float (&a)[N],
+                                               float& dinv) {
   static_assert(N == 8 || N == 16, "blocked Cholesky width");
   if (MPCR_CHOL_LANE_LAUNDER) asm volatile("" : "+v"(lane));
-  const int lr = lane & 15, t = lane >> 4, lb = lane & ~15;
+  const int lr = lane & 15, lb = lane & ~15;
   const int d = m->blane_dof[lane];
-  float a[N];
 #pragma unroll
   for (int j = 0; j < N; j++) {
     const int dj = m->blane_dof[lb + j];
     a[j] = (d >= 0 && dj >= 0) ? elem(d, dj) : (j == lr ? 1.f : 0.f);
   }
-  float dinv = 0.f;
+  dinv = 0.f;
   CholN<N, 0>::run(a, dinv, lr);
+}
+template <int N>
+__device__ __forceinline__ void blocked_sweep(const DevModel* __restrict__ m, const float (&a)[N], float dinv,
+                                              const float* bv, float* xv, int lane, float* Lt) {
+  if (MPCR_CHOL_LANE_LAUNDER) asm volatile("" : "+v"(lane));
+  const int lr = lane & 15, t = lane >> 4;
+  const int d = m->blane_dof[lane];
   float acc = d >= 0 ? bv[d] : 0.f;
   SweepN<N, 0, 1>::run(a, acc, dinv);
   const float y = acc * dinv;
@@ -572,6 +580,13 @@ __device__ __forceinline__ void blocked_solve(const DevModel* __restrict__ m, F&
   const float x = acc * dinv;
   sync();
   if (d >= 0) xv[d] = x;
+}
+template <int N, class F>
+__device__ __forceinline__ void blocked_solve(const DevModel* __restrict__ m, F&& elem, const float* bv, float* xv,
+                                              int lane, float* Lt) {
+  float a[N], dinv;
+  blocked_factor<N>(m, elem, lane, a, dinv);
+  blocked_sweep<N>(m, a, dinv, bv, xv, lane, Lt);
 }
 // the blocked path for a kernel variant of NVW dofs: 8-wide chains in the
 // narrow kernel (trees <= 8 dofs), 16-wide in the dual-arm one (trees <= 16)
@@ -2668,6 +2683,10 @@ __device__ __forceinline__ mfx4 mm16(AF&& af, BF&& bf, mfx4 acc, int lane) {
 #ifndef MPCR_W2_HESS
 #define MPCR_W2_HESS 1
 #endif
+// ... and the implicit solve's blocked factor of M + dt D on wave 1 during Newton
+#ifndef MPCR_W2_IMPL
+#define MPCR_W2_IMPL 1
+#endif
 // The dual-arm variant is compiled for 2 waves/SIMD (<= 256 registers incl.
 // AGPRs; uncapped it took 274 and ran 1 wave/SIMD): with its 21.6 KB image,
 // 7 blocks per CU instead of 4 (dual arm 4096 x 50: 47.5 -> 35.8 ms).
@@ -3928,6 +3947,13 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     const bool rows_j = WPC == 2 && S::WIDE && !rows_c;
     // ... and wave 1 then builds the Newton Hessians (round 5)
     const bool hess2 = MPCR_W2_HESS && rows_j && NVW == 32 && S::CPW == 1;
+    // ... and factors the implicit solve's M + dt D (blocked path) for wave 0
+    // to sweep after Newton: the factor needs only M, wave 1 is otherwise
+    // idle then, and its element gather was most of the solve's time
+    const bool impl2 = MPCR_W2_IMPL && hess2 && S::WIDE && m->integrator == 3 && !m->impl_cross && blk_usable<NVW>(m);
+    constexpr int BLK_N = NVW == 16 ? 8 : 16;
+    static_assert(!S::SPLIT || (BLK_N + 1) * WAVE <= S::DYN_FLOATS, "the implicit factor inside the dynamics region");
+    float* const implf = &s.xpos[0][0];  // the factor: BLK_N + 1 floats per lane (dynamics region, dead until Euler)
     const int rl0 = rows_j ? wv * S::HL : 0, rls = rows_j ? 2 * S::HL : S::HL;
     if constexpr (WPC == 2) {
       if (!rows_c) {
@@ -4226,6 +4252,15 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           // the next step's geom poses
           STAMP(8);
           const int nefc = s.nefc;
+          if (impl2) {
+            const float dt = m->timestep;
+            float fa[BLK_N], fdinv;
+            blocked_factor<BLK_N>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], m_get(i, j)); }, lane, fa,
+                                  fdinv);
+#pragma unroll
+            for (int j = 0; j < BLK_N; j++) implf[j * WAVE + lane] = fa[j];
+            implf[BLK_N * WAVE + lane] = fdinv;
+          }
           if (hess2 && nefc > 0)
             for (int it = 0; it < m->iterations; it++) {
               block_sync();  // wave 0: efc_Da / efc_jar of this iteration
@@ -4236,6 +4271,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
               STAMP(30);
               if (s.pad_) break;
             }
+          if (impl2) block_sync();  // the implicit factor, to wave 0's solve
           continue;
         }
       }
@@ -4593,8 +4629,16 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
         if (S::CPW == 1 && !m->impl_cross && blk_usable<NVW>(m)) {  // M + dt D block diagonal by tree
           if (lane < NVW) s.srch[lane] = lane < nv ? s.qfs[lane] + qc : 0.f;
           sync();
-          blk_solve<NVW>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], m_get(i, j)); }, s.srch, s.srch,
-                         lane, &s.gxpos[0][0]);
+          if (impl2) {  // wave 1's factor
+            block_sync();
+            float fa[BLK_N];
+#pragma unroll
+            for (int j = 0; j < BLK_N; j++) fa[j] = implf[j * WAVE + lane];
+            blocked_sweep<BLK_N>(m, fa, implf[BLK_N * WAVE + lane], s.srch, s.srch, lane, &s.gxpos[0][0]);
+          } else {
+            blk_solve<NVW>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], m_get(i, j)); }, s.srch, s.srch,
+                           lane, &s.gxpos[0][0]);
+          }
           sync();
         } else {
           float Lm[NVW];
