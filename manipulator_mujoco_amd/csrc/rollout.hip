@@ -4252,7 +4252,10 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           // the next step's geom poses
           STAMP(8);
           const int nefc = s.nefc;
-          if (impl2) {
+          // the implicit factor: in the first iteration's wait (wave 0's
+          // solve, line search and next active set), else after the loop
+          bool fdone = !impl2;
+          auto impl_factor = [&]() {
             const float dt = m->timestep;
             float fa[BLK_N], fdinv;
             blocked_factor<BLK_N>(m, [&](int i, int j) { return fmaf(dt, m->impl_D[i][j], m_get(i, j)); }, lane, fa,
@@ -4260,7 +4263,8 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
 #pragma unroll
             for (int j = 0; j < BLK_N; j++) implf[j * WAVE + lane] = fa[j];
             implf[BLK_N * WAVE + lane] = fdinv;
-          }
+            fdone = true;
+          };
           if (hess2 && nefc > 0)
             for (int it = 0; it < m->iterations; it++) {
               block_sync();  // wave 0: efc_Da / efc_jar of this iteration
@@ -4270,7 +4274,9 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
               block_sync();  // wave 0: gradient and stop test
               STAMP(30);
               if (s.pad_) break;
+              if (!fdone) impl_factor();
             }
+          if (!fdone) impl_factor();
           if (impl2) block_sync();  // the implicit factor, to wave 0's solve
           continue;
         }
