@@ -575,6 +575,8 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     }
     d.mc_n = ok && m.nv * SmemW::MCW <= SmemW::MC ? m.nv : 0;
     if (env_int_or("MPCR_M_SLAB", 0)) d.mc_n = 0;  // tests: the HBM-slab path on a model that fits
+    // the two-wave lead flush's pair limit; a lower one (tests) sends more steps to the dealt flush
+    d.w2_lead_max = std::max(-1, std::min(W2_LEAD_MAX, env_int_or("MPCR_W2_LEAD_MAX", W2_LEAD_MAX)));
   }
   for (int i = 0; i < m.nq; i++) d.qpos_init[i] = (float)m.qpos_init[i];
   for (int i = 0; i < m.nv; i++) d.qvel_init[i] = (float)m.qvel_init[i];

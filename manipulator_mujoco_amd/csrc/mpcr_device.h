@@ -68,6 +68,7 @@ struct DevModel {
   // over both waves (no convex pair has a cost slot, so no per-lane cost_c
   // order is at stake; the contacts still go to the list in pair order)
   int cvx_joint;
+  int w2_lead_max;  // the two-wave lead flush's pair limit (rollout.h W2_LEAD_MAX; MPCR_W2_LEAD_MAX lowers it: tests)
   float timestep, tolerance, ls_tolerance, meaninertia;
   float gravity[4];
   float tcp_pos[4];  // tcp site position in tcp_body frame

@@ -3665,7 +3665,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     bool do_list = false, do_narrow = false;
     if (run_coll) {
       if (pass == 0) { do_list = true; do_narrow = !swapm; }
-      else do_narrow = swapm && s.ncvx > W2_LEAD_MAX;
+      else do_narrow = swapm && s.ncvx > m->w2_lead_max;
     } else if (pass == 1) {  // wave 0 (swap mode): the list is posted for this step
       if constexpr (S::SPLIT) {  // (bounded: a lost post flags the candidate instead of hanging the launch)
         int guard = 0;
@@ -3674,7 +3674,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
           __builtin_amdgcn_s_sleep(1);
         if (guard >= (1 << 22)) status |= 2;  // (reported as a failed rollout)
       }
-      do_narrow = s.ncvx <= W2_LEAD_MAX;
+      do_narrow = s.ncvx <= m->w2_lead_max;
     }
     if (do_list || do_narrow) {
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
@@ -3793,7 +3793,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       float* const mbox = reinterpret_cast<float*>(jcnt);  // wave 0's manifold results, W2_JOB_OUT floats per job
       int lpc = 0, ljob = 0, lsl = 0;
       float ld[4] = {1e30f, 1e30f, 1e30f, 1e30f}, lp[4][3] = {}, ln[4][3] = {};
-      if (MPCR_W2_LEAD && split && wv == 1 && s.ncvx <= W2_LEAD_MAX) {
+      if (MPCR_W2_LEAD && split && wv == 1 && s.ncvx <= m->w2_lead_max) {
         const bool v = lane < s.ncvx;
         lpc = v ? s.cvx[lane] : 0;
         lsl = v ? narrow_lane(m, s, hx, lpc, ld, lp, ln, (args.dbg && b == 0 && t == H - 1) ? args.dbg : nullptr)
@@ -3823,7 +3823,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       }
       if constexpr (WPC == 2) block_sync();  // the list is complete; the dynamics are done
       const int ncv = s.ncvx, rstep = split ? 2 * WAVE : WAVE;
-      const bool lead = MPCR_W2_LEAD && split && ncv <= W2_LEAD_MAX;
+      const bool lead = MPCR_W2_LEAD && split && ncv <= m->w2_lead_max;
       int ncon_w = s.ncon;
       if (lead) {
         STAMP(16);  // (profile build: wave 0's wait for the queue)

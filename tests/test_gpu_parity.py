@@ -429,6 +429,43 @@ def test_two_wave_variant_is_bitwise_one_wave(torch_cuda, name, n):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("lead_max", [-1, 0, 6])
+def test_two_wave_dual_arm_flush_paths_bitwise(torch_cuda, monkeypatch, lead_max):
+    """The two-wave dual-arm kernel's convex flush has two paths: the lead
+    flush (swap mode: the collision wave runs every pair's MPR beside wave 0's
+    dynamics, a manifold queue over both waves) for steps with at most
+    DevModel::w2_lead_max listed pairs, else the dealt flush (item i on wave
+    i & 1).  MPCR_W2_LEAD_MAX lowers the limit: -1 sends every step to the
+    dealt flush (no pair list is ever that short), 0 only the pair-free steps
+    to the lead path, 6 mixes them within each rollout.  Every mix is bitwise
+    the one-wave kernel."""
+    torch = torch_cuda
+    from manipulator_mujoco_amd import _lib
+    lib = _lib.load()
+    n, H = 512, 50
+    m = models.load("dual_arm", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 6, torch.device("cuda:0"))
+    monkeypatch.setenv("MPCR_W2_LEAD_MAX", str(lead_max))
+    e = Engine(m, H, n, Pd)
+    outs = []
+    prev = lib.mpcr_set_two_wave_max_n(-1)
+    try:
+        for thr in (0, n):
+            lib.mpcr_set_two_wave_max_n(thr)
+            c4 = torch.empty((n, 4), device="cuda:0")
+            th = torch.empty((n, 6 * H), device="cuda:0")
+            td = torch.empty((n, 6 * H), device="cuda:0")
+            st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+            e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, cost4=c4, theta=th, thetadot=td, status=st)
+            torch.cuda.synchronize()
+            outs.append((c4, th, td, st))
+    finally:
+        lib.mpcr_set_two_wave_max_n(prev)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("seg,groups", [(25, 1), (50, 2), (20, 4)])
 def test_dual_arm_horizon_segments_bitwise(torch_cuda, monkeypatch, seg, groups):
     """Dual-arm rollouts as horizon segments (rollout_launch: each segment
