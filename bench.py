@@ -401,7 +401,7 @@ def c5_run(rank, world, gpu, dev, n_global, H, iters, ticks, warmup, capture_exc
             ev[1].record()
         state["out"] = out
 
-    elapsed, tick_ms, _ = _timed(tick, ticks, warmup, world, dev)
+    elapsed, tick_ms, tick_each = _timed(tick, ticks, warmup, world, dev)
     # the dominant kernel: the rank's rollout call on the last iteration's
     # samples, eagerly, HIP events on its stream (graph replays cannot be split)
     n = p.n_local
@@ -417,8 +417,9 @@ def c5_run(rank, world, gpu, dev, n_global, H, iters, ticks, warmup, capture_exc
         if k:
             kms.append(a.elapsed_time(b))
     out = state["out"]
-    nefc_mean = float((st >> 10).double().mean().item()) / H
-    return {"elapsed": elapsed, "tick_ms": tick_ms, "kernel_ms": float(np.median(kms)), "n_local": n,
+    nefc_mean = float((st >> 11).double().mean().item()) / H
+    return {"elapsed": elapsed, "tick_ms": tick_ms, "tick_ms_each": [round(x, 3) for x in tick_each],
+            "kernel_ms": float(np.median(kms)), "n_local": n,
             "nefc_mean": nefc_mean, "model": p.model, "engine": p.engine,
             "best_cost": [float(x) for x in np.asarray(out[0])],
             "best_cost_grc": [float(out[1]), float(out[2]), float(out[3])],
@@ -523,6 +524,8 @@ def main_c5(args, cfg):
                          "flops_per_step": fps, "hbm_algorithmic_bytes": hbm_launch},
             "best": {"cost_per_iteration": r["best_cost"], "cost_grc": r["best_cost_grc"]},
             "eef_dist_after": r["eef_dist"], "mean_constraint_rows": round(r["nefc_mean"], 2),
+            "ticks": {"timed": args.steps, "warmup": args.warmup, "ms_each": r["tick_ms_each"],
+                      "note": "consecutive closed-loop ticks: each starts from the plant state the previous left"},
         }
         if cpu_rec is not None:
             rec["cpu_baseline"] = cpu_rec
@@ -536,6 +539,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--ticks", type=int, default=None,
+                    help="--config c5: closed-loop ticks timed (BASELINE configs[4] runs 30); overrides --steps")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
                     help="BASELINE.json config preset (c3 = the metric's workload, the default)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
@@ -572,6 +577,8 @@ def main():
         return launch_selftest()
     cfg = CONFIGS[args.config]
     if args.config == "c5":
+        if args.ticks:
+            args.steps = args.ticks
         return main_c5(args, cfg)
     args.model = args.model or cfg["model"]
     args.n = args.n or cfg["n"]
@@ -670,7 +677,7 @@ def main():
     elapsed, kern_ms, kms = _timed(step, args.steps, 0, world, dev)
     idx, best = md.decode_key(int(key.item()))
     trunc = int((status & 1).sum().item())
-    nefc_mean = float((status >> 10).double().mean().item()) / H
+    nefc_mean = float((status >> 11).double().mean().item()) / H
 
     contact = None
     if rank == 0 and not args.no_contact_report and m.nslot:

@@ -52,16 +52,20 @@
 extern "C" {
 #endif
 
-/* ABI version.  2 (round 4): the status word's max-rows field widened to 8
-   bits, so rows-summed moved from bit 8 to bit 10 (version 1: 6 bits << 2,
-   sum << 8).  Decode with the accessors below, not raw shifts. */
-#define MPCR_ABI_VERSION 2
+/* ABI version.  3 (round 6): bit 10 reports a lost two-wave handshake
+   (MPCR_STATUS_SYNC), so rows-summed moved to bit 11.  2 (round 4): the
+   max-rows field widened to 8 bits (version 1: 6 bits << 2, sum << 8).
+   Decode with the accessors below, not raw shifts. */
+#define MPCR_ABI_VERSION 3
 
 /* the per-candidate status word of mpcr_rollout_cost / _dp */
 #define MPCR_STATUS_TRUNCATED(s) ((s) & 1)                  /* constraint rows truncated  */
 #define MPCR_STATUS_NONFINITE(s) (((s) >> 1) & 1)           /* non-finite state           */
 #define MPCR_STATUS_MAX_ROWS(s) (((s) >> 2) & 255)          /* busiest step's rows (<= 255) */
-#define MPCR_STATUS_ROWS_SUM(s) ((unsigned)(s) >> 10)       /* rows summed over the horizon */
+#define MPCR_STATUS_SYNC(s) (((s) >> 10) & 1)               /* two-wave handshake timed out:
+                                                                the candidate's outputs are void */
+#define MPCR_STATUS_ROWS_SUM(s) ((unsigned)(s) >> 11)       /* rows summed over the horizon */
+#define MPCR_STATUS_FAILED(s) (((s) & 2) | ((s) & (1 << 10)))  /* no usable result */
 
 enum {
   MPCR_OK = 0,
@@ -123,9 +127,10 @@ void mpcr_engine_free(mpcr_engine* e);
    best_key             device uint64: atomic-min of
                         (ordered(cost) << 32 | (index_base + i)), NaN first (nullable)
    status [n]           per-candidate flags (bit0: constraint rows truncated,
-                        bit1: non-finite state) | (max constraint rows in
-                        one step, 8 bits capped at 255, << 2) | (constraint
-                        rows summed over the horizon << 10)      (nullable)
+                        bit1: non-finite state, bit10: two-wave handshake
+                        lost) | (max constraint rows in one step, 8 bits
+                        capped at 255, << 2) | (constraint rows summed over
+                        the horizon << 11)                       (nullable)
    stream               hipStream_t or NULL (default stream)
    n = 0 is a no-op returning MPCR_OK (input and cost4 may then be NULL). */
 int mpcr_rollout_cost(mpcr_engine* e, const float* input, int layout, int n, const double* q0,

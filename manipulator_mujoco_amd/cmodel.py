@@ -19,7 +19,11 @@ MAX_GEOM, MAX_SITE, MAX_PAIR, MAX_EQ = 128, 24, 768, 8
 MAX_SLOT, MAX_CTRL, MAX_ACT = 512, 8, 16
 MAX_HULLV, MAX_HULLA = 8192, 49152
 MAX_TEN = 4
-LUT_R = int(os.environ.get("MPCR_LUT_R", 128))  # the support start table resolution (mpcr_model.h MPCR_LUT_R)
+# the support start table resolution: mpcr_model.h MPCR_LUT_R, which the
+# engine and the oracle fix at build time.  A constant here; the A/B tool
+# (tools/lut_ab.sh) packs other resolutions through MPCR_AB_LUT_R together
+# with a library built for them.
+LUT_R = int(os.environ.get("MPCR_AB_LUT_R", 128))
 MAX_HULLLUT = 24 * 6 * LUT_R * LUT_R
 MAX_FACE, MAX_FACEV, MAX_VFACE, FACE_MAXV = 12288, 49152, 65536, 16
 

@@ -4,6 +4,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -842,11 +843,20 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     // directions a hull vertex is extreme for are a convex cone, bounded by
     // its neighbours: the start vertex beats each neighbour by > kExactGap m
     // (fp32 coordinates) along each corner ray, so along every direction of
-    // the cell (fp32 rounding of a projection or of the cell test moves it
-    // by ~1e-8 m)
+    // the cell.  The margin scales with the hull's extent: the kernel's fp32
+    // projections err by a few ulp of the largest coordinate (~1e-8 m on the
+    // gripper's cm-sized hulls, whose margin stays 1e-6 m)
     constexpr double kExactGap = 1e-6;
+    std::vector<double> hull_gap(h.ngeom, kExactGap);
+    for (int g = 0; g < h.ngeom; g++)
+      if (h.geom_hulladr[g] >= 0)
+        for (int v = h.geom_hulladr[g]; v < h.geom_hulladr[g] + h.geom_hullnum[g]; v++) {
+          const double r = std::sqrt((double)hv[v].x * hv[v].x + (double)hv[v].y * hv[v].y + (double)hv[v].z * hv[v].z);
+          hull_gap[g] = std::max(hull_gap[g], 32.0 * FLT_EPSILON * r);
+        }
     auto cell_exact = [&](int g, int c, int v) {
       const int R = MPCR_LUT_R, f = c / (R * R), iu = (c / R) % R, iv = c % R, ax = f / 2;
+      const double gap_min = hull_gap[g];
       const float* x = &hv[v].x;
       for (int du = 0; du < 2; du++)
         for (int dv = 0; dv < 2; dv++) {
@@ -858,10 +868,9 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
           for (int k = h.hull_adjadr[v]; k < h.hull_adjadr[v] + h.hull_adjnum[v]; k++) {
             const float* y = &hv[h.hull_adj[k]].x;
             const double gap = ((double)x[0] - y[0]) * d[0] + ((double)x[1] - y[1]) * d[1] + ((double)x[2] - y[2]) * d[2];
-            if (!(gap > kExactGap * dn)) return false;
+            if (!(gap > gap_min * dn)) return false;
           }
         }
-      (void)g;
       return true;
     };
     int nlut = 0;

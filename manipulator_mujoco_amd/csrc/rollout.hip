@@ -715,6 +715,12 @@ __device__ __forceinline__ bool mpr_zero(float x) { return fabsf(x) < kMprEps; }
 #define MPCR_SUP_TIE 1e-6f  // < 0: MuJoCo's mju_sign (only an exact zero is a tie)
 #endif
 constexpr float kSupTie = MPCR_SUP_TIE;
+// hull support ties (round 6, oracle HULL_TIE): vertices within this many
+// metres of the climb's end are tied with it (hull_tie); 0 = the plain climb
+#ifndef MPCR_HULL_TIE
+#define MPCR_HULL_TIE 1e-7f
+#endif
+constexpr float kHullTie = MPCR_HULL_TIE;
 constexpr float kSupBand = MPCR_SUP_BAND;
 __device__ __forceinline__ float tie_sign(float lk, float ln) {
   if (kSupTie < 0.f) return lk > 0.f ? 1.f : (lk < 0.f ? -1.f : 0.f);
@@ -727,31 +733,65 @@ __device__ __forceinline__ float tie_sign(float lk, float ln) {
 // need no lookup: the first 8 neighbours (90 % of hull vertices have <= 8)
 // sit in v's NaN-padded head block (addressed by v alone, 8 independent
 // loads), the rest of a longer list in hull_adjv after one hull_info load.
-__device__ __forceinline__ void climb_scan(const float4 (&w)[8], const float l[3], float& bn, float4& hv, int& nb) {
+// Hull support ties (round 6, the oracle's hull_tie): a round also keeps
+// the lowest-index neighbour within kHullTie of the current vertex (tkey:
+// index << 16 | degree, the record's w bits rotated; ~0u: none).  The round
+// that ends the climb thus names the climb end's lowest tied neighbour, and
+// sup_finish walks on to it while one is lower (tie_round).
+__device__ __forceinline__ void climb_scan(const float4 (&w)[8], const float l[3], float& bn, float4& hv, int& nb,
+                                           float lo, uint32_t& tkey) {
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     const float du = w[j].x * l[0] + w[j].y * l[1] + w[j].z * l[2];  // NaN pads never win
+    const uint32_t wb = __float_as_uint(w[j].w);
+    if (du >= lo) tkey = min(tkey, __builtin_amdgcn_alignbit(wb, wb, 16));
     if (du > bn) { bn = du + kSupBand; nb = __float_as_int(w[j].w); hv = w[j]; }
   }
 }
 __device__ __forceinline__ int climb_round(const DevModel* __restrict__ m, int v, int deg, const float l[3],
-                                           float& best, float4& hv) {
+                                           float& best, float4& hv, uint32_t& tkey) {
   int nb = -1;
   float bn = best + kSupBand;
+  const float lo = best - kHullTie;
+  tkey = ~0u;
   float4 w[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) w[j] = m->hull_head[(size_t)v * 8 + j];
-  climb_scan(w, l, bn, hv, nb);
+  climb_scan(w, l, bn, hv, nb, lo, tkey);
   if (deg > 8) {
     const int a = m->hull_info[v].x, last = a + deg - 1;
     for (int k0 = a + 8; k0 <= last; k0 += 8) {
 #pragma unroll
       for (int j = 0; j < 8; j++) w[j] = m->hull_adjv[min(k0 + j, last)];  // repeats of the last never win twice
-      climb_scan(w, l, bn, hv, nb);
+      climb_scan(w, l, bn, hv, nb, lo, tkey);
     }
   }
   if (nb >= 0) best = bn - kSupBand;
   return nb;
+}
+
+// The support of a hull on a tie.  When the direction is normal (to
+// ~kHullTie) to an edge or a face of the hull, every vertex of it is a
+// maximum, and which one the climb reaches depends on where it started (the
+// start table's cell, the pair's hint) and on the last bits of the dot
+// products (fp32 and fp64 pick differently).  From the climb's end v the
+// support walks to the lowest-index neighbour within kHullTie of v's value
+// while that neighbour's index is lower: on a tied edge or triangle that is
+// the tie's lowest index from whichever vertex the climb reached, so a start
+// table's resolution stays a performance choice, not a parity change.  One
+// walk round, out of line with scalar arguments (its call's spills stay on
+// this path): the lowest tied neighbour key of vertex v.
+__device__ __noinline__ uint32_t tie_round(const DevModel* __restrict__ m, int v, int deg, float lo, float l0,
+                                           float l1, float l2) {
+  uint32_t tkey = ~0u;
+  const int a = m->hull_info[v].x;
+#pragma unroll 1
+  for (int k = 0; k < deg; k++) {
+    const float4 w = k < 8 ? m->hull_head[(size_t)v * 8 + k] : m->hull_adjv[a + k];
+    const uint32_t wb = __float_as_uint(w.w);
+    if (w.x * l0 + w.y * l1 + w.z * l2 >= lo) tkey = min(tkey, __builtin_amdgcn_alignbit(wb, wb, 16));
+  }
+  return tkey;
 }
 
 // cube-map cell of a local direction (the model's hull_lut order, oracle
@@ -818,8 +858,10 @@ __device__ __forceinline__ void sup_start(const DevModel* __restrict__ m, const 
   }
 }
 template <class S>
+// ties = false: the caller uses the support value only (the SAT's
+// separations), which any tied vertex gives to within kHullTie
 __device__ __forceinline__ void sup_finish(const DevModel* __restrict__ m, const S& s, int g, SupQ& q, float out[3],
-                                           int& hint, const float* org) {
+                                           int& hint, const float* org, bool ties = true) {
   const float* R = s.gxmat[g];
   const float* sz = m->geom_size[g];
   const float* l = q.l;
@@ -852,12 +894,25 @@ __device__ __forceinline__ void sup_finish(const DevModel* __restrict__ m, const
         const float bh = hh.x * lu[0] + hh.y * lu[1] + hh.z * lu[2];
         if (bh > best + kSupBand) { v = hint; hv = hh; deg = __float_as_int(hh.w); best = bh; }
       }
+      uint32_t tkey = ~0u;
       for (int guard = 0; guard < 4096; guard++) {
         PROF_COUNT(m, 19);
-        const int nb = climb_round(m, v, deg, lu, best, hv);
+        const int nb = climb_round(m, v, deg, lu, best, hv, tkey);
         if (nb < 0) break;
         v = nb & 0xffff;
         deg = nb >> 16;
+      }
+#ifndef MPCR_TIE_WALK
+#define MPCR_TIE_WALK 1
+#endif
+      if (MPCR_TIE_WALK == 0 && ties) asm volatile("" ::"v"(tkey));  // (A/B: the tracking without the walk)
+      if (MPCR_TIE_WALK && kHullTie > 0.f && ties && (int)(tkey >> 16) < v) {  // a lower-index tied neighbour: walk (hull_tie)
+        const float lo = best - kHullTie;
+        for (int guard = 0; guard < 64 && (int)(tkey >> 16) < v; guard++) {
+          v = tkey >> 16;
+          tkey = tie_round(m, v, tkey & 0xffff, lo, lu[0], lu[1], lu[2]);
+        }
+        hv = m->hull_vert[v];
       }
     }
     p[0] = hv.x; p[1] = hv.y; p[2] = hv.z;
@@ -872,10 +927,10 @@ __device__ __forceinline__ void sup_finish(const DevModel* __restrict__ m, const
 }
 template <class S>
 __device__ __forceinline__ void support_geom(const DevModel* __restrict__ m, const S& s, int g, const float dir[3],
-                                             float out[3], int& hint, const float* org = nullptr) {
+                                             float out[3], int& hint, const float* org = nullptr, bool ties = true) {
   SupQ q;
   sup_start(m, s, g, dir, hint, q);
-  sup_finish(m, s, g, q, out, hint, org);
+  sup_finish(m, s, g, q, out, hint, org, ties);
 }
 
 struct MprPt { float v[3], a[3], b[3]; };
@@ -1373,7 +1428,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, const S& s, PS& ps, con
           const bool two = k >= nf1;
           float pt[3];
           int h = two ? h0 : h1;
-          sup_finish(m, s, two ? g1 : g2, q[u], pt, h, c);
+          sup_finish(m, s, two ? g1 : g2, q[u], pt, h, c, false);
           const float sp = nw[u][0] * pt[0] + nw[u][1] * pt[1] + nw[u][2] * pt[2] - off[u];
           ps.satsep[k] = sp;
           mxl = fmaxf(mxl, sp);
@@ -1467,7 +1522,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, const S& s, PS& ps, con
     face_rel(m, s, g, fid, c, nw, off);
     const float mn[3] = {-nw[0], -nw[1], -nw[2]};
     int h = two ? h0 : h1;
-    support_geom(m, s, go, mn, pt, h, c);
+    support_geom(m, s, go, mn, pt, h, c, false);
     sep = nw[0] * pt[0] + nw[1] * pt[1] + nw[2] * pt[2] - off;
   }
   // the maximum's tie band: the lowest face index (a flush face pair has the
@@ -3667,14 +3722,17 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
       if (pass == 0) { do_list = true; do_narrow = !swapm; }
       else do_narrow = swapm && s.ncvx > m->w2_lead_max;
     } else if (pass == 1) {  // wave 0 (swap mode): the list is posted for this step
+      bool posted = true;
       if constexpr (S::SPLIT) {  // (bounded: a lost post flags the candidate instead of hanging the launch)
         int guard = 0;
         while (__hip_atomic_load(&s.ctok_[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t + 1 &&
                ++guard < (1 << 22))
           __builtin_amdgcn_s_sleep(1);
-        if (guard >= (1 << 22)) status |= 2;  // (reported as a failed rollout)
+        // a lost post: its own status bit (MPCR_STATUS_SYNC, the outputs are
+        // void), and the list is not read -- wave 1 may still be writing it
+        if (guard >= (1 << 22)) { status |= 1 << 10; posted = false; }
       }
-      do_narrow = s.ncvx <= m->w2_lead_max;
+      do_narrow = posted && s.ncvx <= m->w2_lead_max;
     }
     if (do_list || do_narrow) {
     // ---- collision: lanes over pairs (typed segments); cost_c on the masked
@@ -4741,7 +4799,7 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
     args.cost4[4 * (size_t)b + 1] = cost_g;
     args.cost4[4 * (size_t)b + 2] = cost_r;
     args.cost4[4 * (size_t)b + 3] = cost_c;
-    if (args.status) args.status[b] = status | (min(nefc_max, 255) << 2) | (nefc_sum << 10);
+    if (args.status) args.status[b] = status | (min(nefc_max, 255) << 2) | (nefc_sum << 11);
     if (args.best_key) {
       const uint32_t u = __float_as_uint(cost);
       uint32_t key = isnan(cost) ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
@@ -4831,7 +4889,13 @@ static int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 static std::atomic<int> g_wpc2_max_n{env_int("MPCR_WPC2_MAX_N", MPCR_WPC2_MAX_N_DEFAULT)};
+#ifdef MPCR_STOP_AFTER
+// attribution builds stop a wave mid-step; the two-wave kernels would leave
+// its partner at an unmatched barrier, so these builds run one wave only
+static int wpc2_max_n() { return 0; }
+#else
 static int wpc2_max_n() { return g_wpc2_max_n.load(std::memory_order_relaxed); }
+#endif
 int rollout_set_wpc2_max_n(int n) {
   return n >= 0 ? g_wpc2_max_n.exchange(n) : wpc2_max_n();
 }

@@ -1020,6 +1020,58 @@ static int lut_cell(const double l[3]) {
    incident-polygon vertices, 14 climb rounds, 15 support-vertex faces,
    16.. histogram of support pairs per call (capped at 47) */
 static __thread long g_mpr_stats[64]; /* per thread: the checker's pool threads never share it */
+/* Hull support ties (round 6).  The climb ends at a vertex no neighbour
+   beats; when the direction is (within HULL_TIE metres) normal to an edge or
+   a face of the hull, every vertex of it is a maximum and which one the
+   climb reaches depends on where it started (the start table's cell, the
+   pair's hint) and on the last bits of the dot products (fp32 and fp64 pick
+   differently).  So the climb's last round also names the end v's
+   lowest-index neighbour within HULL_TIE of v's value, and the support walks
+   on to it while it is lower than the current vertex (the threshold fixed at
+   the climb end's value): on a tied edge or triangle that is the tie's
+   lowest index from whichever of its vertices the climb reached, as an
+   argmax over all vertices that takes the first of equal values (MJX's
+   jnp.argmax support of a mesh) -- a support start table's resolution is a
+   performance choice, not a parity change (VERDICT r5 item 1;
+   tools/tie_start_independence.py).  HULL_TIE = 1e-7 m is ~1e-6 of the
+   gripper hulls' extent (the box / capsule / cylinder axis tie's relative
+   scale, tie_sign) and ~10x the fp32 rounding of a vertex projection; the
+   kernel's sup_finish / tie_round do the same in fp32.  Queries whose caller
+   uses the support value only (the SAT's separations, support_value) skip
+   the walk: every tied vertex gives that value to within HULL_TIE.  Exact
+   mode (EXACT_SUP): no tie rule. */
+static double g_hull_tie = 1e-7;
+void oracle_set_hull_tie(double v) { g_hull_tie = v; } /* experiments: 0 = the plain climb's end */
+#define HULL_TIE ((g_exact & EXACT_SUP) ? 0.0 : g_hull_tie)
+static __thread int g_value_only; /* support_value's queries: no tie walk */
+static __thread int g_sup_kind; /* diagnostic: 0 MPR, 1 support vertex, 2 support value (SAT), 3 plane */
+static __thread long g_tie_kind[4][2];
+void oracle_tie_kind(long* out, int reset) {
+  if (out) memcpy(out, g_tie_kind, sizeof(g_tie_kind));
+  if (reset) memset(g_tie_kind, 0, sizeof(g_tie_kind));
+}
+/* the lowest-index neighbour of v whose value reaches lo (-1: none) */
+static int tied_neighbour(const mpcr_model_t* m, int v, double lo, const double lu[3]) {
+  int t = -1;
+  for (int k = m->hull_adjadr[v]; k < m->hull_adjadr[v] + m->hull_adjnum[v]; k++) {
+    const int u = m->hull_adj[k];
+    if ((t < 0 || u < t) && dot3(m->hull_vert[u], lu) >= lo) t = u;
+  }
+  return t;
+}
+static int hull_tie(const mpcr_model_t* m, int v, int t, double lo, const double lu[3]) {
+  const int v0 = v;
+  g_mpr_stats[6]++;
+  for (int guard = 0; guard < 64 && t >= 0 && t < v; guard++) {
+    v = t;
+    t = tied_neighbour(m, v, lo, lu);
+  }
+  g_mpr_stats[7] += v != v0;
+  g_tie_kind[g_sup_kind & 3][0]++;
+  g_tie_kind[g_sup_kind & 3][1] += v != v0;
+  return v;
+}
+
 static void support_rel(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint,
                         const double* org);
 static void support(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint) {
@@ -1064,20 +1116,24 @@ static void support_rel(const mpcr_model_t* m, const odata* d, int g, const doub
         const double bh = dot3(m->hull_vert[*hint], lu);
         if (bh > best + SUP_BAND) { v = *hint; best = bh; }
       }
+      int tmin = -1; /* the last round's lowest-index neighbour within HULL_TIE of v */
       for (;;) {
         int nb = v;
         g_mpr_stats[2]++;
         g_mpr_stats[3] += m->hull_adjnum[v];
         double bn = best + SUP_BAND; /* a neighbour must beat this; ties within the band go to the first */
+        tmin = -1;
         for (int k = m->hull_adjadr[v]; k < m->hull_adjadr[v] + m->hull_adjnum[v]; k++) {
           int u = m->hull_adj[k];
           double du = dot3(m->hull_vert[u], lu);
+          if (du >= best - HULL_TIE && (tmin < 0 || u < tmin)) tmin = u;
           if (du > bn) { bn = du + SUP_BAND; nb = u; }
         }
         if (nb == v) break;
         best = bn - SUP_BAND;
         v = nb;
       }
+      if (HULL_TIE > 0 && !g_value_only && tmin >= 0 && tmin < v) v = hull_tie(m, v, tmin, best - HULL_TIE, lu);
       memcpy(p, m->hull_vert[v], sizeof(p));
       *hint = v;
       break;
@@ -1353,7 +1409,9 @@ static void col_plane_mesh(const mpcr_model_t* m, odata* d, int pair, int gp, in
   const double* R = d->geom_xmat[g];
   const double* Rp = d->geom_xmat[gp];
   double n[3] = {Rp[2], Rp[5], Rp[8]}, nn[3] = {-Rp[2], -Rp[5], -Rp[8]}, q[3], pos[3];
+  g_sup_kind = 3;
   support(m, d, g, nn, q, &d->hint[pair][1]);
+  g_sup_kind = 0;
   double dist0 = (q[0] - d->geom_xpos[gp][0]) * n[0] + (q[1] - d->geom_xpos[gp][1]) * n[1] +
                  (q[2] - d->geom_xpos[gp][2]) * n[2];
   if (dist0 >= 0) {
@@ -1499,7 +1557,9 @@ static void vert_world(const mpcr_model_t* m, const odata* d, int g, int v, doub
 static double support_value(const mpcr_model_t* m, const odata* d, int g, const double dir[3], int* hint,
                             const double* c) {
   double p[3];
+  g_value_only = 1; /* the value only: no tie walk (hull_tie) */
   support_rel(m, d, g, dir, p, hint, c);
+  g_value_only = 0;
   return dot3(p, dir);
 }
 
@@ -1533,6 +1593,7 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   const long climb0 = g_mpr_stats[2];
   g_mpr_stats[8]++;
   h = h0;
+  g_sup_kind = 1;
   const int s1 = support_vertex(m, d, g1, n, &h);
   h = h1;
   const int s2 = support_vertex(m, d, g2, nn, &h);
@@ -1578,7 +1639,9 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
     face_world(m, d, g, fid[k], nf, &off, cg);
     for (int c = 0; c < 3; c++) mnf[c] = -nf[c];
     h = two ? h0 : h1;
+    g_sup_kind = 2;
     sep[k] = -support_value(m, d, go, mnf, &h, cg) - off; /* min over go of nf . x, minus the plane */
+    g_sup_kind = 0;
     if (sep[k] > mx) mx = sep[k];
   }
   /* the maximum's tie band: the lowest face index (a flush face pair has the
@@ -1594,7 +1657,9 @@ static int poly_manifold(const mpcr_model_t* m, odata* d, int pair, int g1, int 
   /* incident face: the most anti-parallel face on gi's support vertex along -nr */
   const double mnr[3] = {-nr[0], -nr[1], -nr[2]};
   h = gi == g1 ? h0 : h1;
+  g_sup_kind = 1;
   const int si = support_vertex(m, d, gi, mnr, &h);
+  g_sup_kind = 0;
   const int ci = m->vert_facenum[si] < 64 ? m->vert_facenum[si] : 64;
   double al[64];
   mx = -1e300;
@@ -1776,7 +1841,9 @@ static void col_plane_convex(const mpcr_model_t* m, odata* d, int pair, int gp, 
   }
   const double* R = d->geom_xmat[gp];
   double n[3] = {R[2], R[5], R[8]}, nn[3] = {-R[2], -R[5], -R[8]}, p[3], pos[3];
+  g_sup_kind = 3;
   support(m, d, g, nn, p, &d->hint[pair][1]);
+  g_sup_kind = 0;
   double dist = (p[0] - d->geom_xpos[gp][0]) * n[0] + (p[1] - d->geom_xpos[gp][1]) * n[1] +
                 (p[2] - d->geom_xpos[gp][2]) * n[2];
   for (int k = 0; k < 3; k++) pos[k] = p[k] - 0.5 * dist * n[k];

@@ -25,6 +25,13 @@ def torch_cuda():
     return torch
 
 
+def assert_no_sync_loss(st):
+    """No candidate lost a two-wave handshake (status bit 10,
+    MPCR_STATUS_SYNC in include/mpcr.h: its outputs would be void)."""
+    s = st.cpu().numpy() if hasattr(st, "cpu") else np.asarray(st)
+    assert int(((s >> 10) & 1).sum()) == 0, "two-wave handshake lost"
+
+
 def projected_xi(n, H, seed, device):
     """BASELINE.md synthetic inputs: xi ~ N(0, 10.003 I) projected with 10 ADMM iterations."""
     import torch
@@ -334,7 +341,9 @@ def test_dual_arm_parity_to_conditioning(torch_cuda, H):
     xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
     xi_h = xi.cpu().numpy()
     e = Engine(m, H, n, Pd)
-    g = e.rollout_cost(xi_h, MPCR_LAYOUT_XI, Q0, W, PT, QT).astype(np.float64)
+    st = np.zeros(n, dtype=np.int32)
+    g = e.rollout_cost(xi_h, MPCR_LAYOUT_XI, Q0, W, PT, QT, status=st).astype(np.float64)
+    assert_no_sync_loss(st)
     o, sens = pu.conditioning(m, _td(Pd, xi_h, H), seed=H)
     st = pu.check(m, g[:, 0], o, sens, f"dual arm H={H}")
     comp = pu.check_components(m, g, o, f"dual arm H={H}")
@@ -362,7 +371,8 @@ def test_dual_arm_c4_properties(torch_cuda):
     assert torch.equal(a, b) and torch.isfinite(a).all() and torch.equal(c2, a[half:])
     s_ = st.cpu().numpy()
     assert int((s_ & 1).sum()) == 0
-    rows_per_step = (s_ >> 10) / H
+    assert_no_sync_loss(s_)
+    rows_per_step = (s_ >> 11) / H
     assert rows_per_step.min() >= 8  # 8 equality rows + the linkage contacts
     # the busiest step's rows (status bits 2-9, no longer saturating at 63):
     # below the wide image's 8 + 4 x 48 = 200-row cap (measured p50 / p99 /
@@ -427,6 +437,7 @@ def test_two_wave_variant_is_bitwise_one_wave(torch_cuda, name, n):
         lib.mpcr_set_two_wave_max_n(prev)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+    assert_no_sync_loss(outs[1][3])
 
 
 @pytest.mark.parametrize("lead_max", [-1, 0, 6])
@@ -464,6 +475,7 @@ def test_two_wave_dual_arm_flush_paths_bitwise(torch_cuda, monkeypatch, lead_max
         lib.mpcr_set_two_wave_max_n(prev)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+    assert_no_sync_loss(outs[1][3])
 
 
 @pytest.mark.parametrize("seg,groups", [(25, 1), (50, 2), (20, 4)])
@@ -497,6 +509,7 @@ def test_dual_arm_horizon_segments_bitwise(torch_cuda, monkeypatch, seg, groups)
         del e
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
+    assert_no_sync_loss(out[1][3])
 
 
 def test_dual_arm_compact_mass_matrix_bitwise_slab(torch_cuda, monkeypatch):
@@ -522,3 +535,4 @@ def test_dual_arm_compact_mass_matrix_bitwise_slab(torch_cuda, monkeypatch):
         del e
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
+    assert_no_sync_loss(out[1][3])

@@ -246,3 +246,48 @@ def test_dual_arm_closed_loop_c5(torch_cuda):
     assert pg._graphs is not None and dg == de
     _check_selected_costs(pg, og, sg, H)
     print(f"C5 loop eef_dist per tick: {[round(x, 4) for x in dg]}")
+
+
+def test_dual_arm_c5_thirty_ticks(torch_cuda):
+    """BASELINE.json configs[4] over its whole configured loop: 30 receding-
+    horizon ticks of 8192 x 50 x 3 CEM iterations on the dual arm,
+    graph-captured (SBP/mpc_planner.py:151-233, run_mpc_planner.py:7-44).
+    Every tick's selected cost matches the fp64 oracle's rollout of that
+    tick's best_vels from the tick's start (to 1e-4 or its conditioning), and
+    the plant -- the rollout kernel with n = 1 stepping the closed loop --
+    stays on the fp64 oracle's replay of the 30 applied joint velocities from
+    the initial state (joint positions within 1e-4 rad or twice the spread of
+    8 fp32-sized noise draws)."""
+    import parity_util as pu
+    n, H, ticks = 8192, 50, 30
+    from manipulator_mujoco_amd.engine import Plant
+    p = _planner(model_path="dual_arm", num_batch=n, num_steps=H, maxiter_cem=3, graph=True)
+    plant = Plant(p.model)
+    qpos = plant.qpos.copy()
+    qa, da = np.asarray(p.model.ctrl_qposadr[:6]), np.asarray(p.model.ctrl_dofadr[:6])
+    qpos[qa] = Q0
+    plant.set_state(qpos=qpos)
+    plant.forward()
+    xi_mean, outs, starts, applied, traj = np.zeros(p.nvar), [], [], [], []
+    for _ in range(ticks):
+        starts.append(plant.qpos[qa].copy())
+        out = p.compute_cem(xi_mean, plant.qpos[qa], plant.qvel[da], plant.qacc[da], PT, QT)
+        xi_mean = out[6]
+        outs.append(out[:7])
+        v = np.mean(out[4][1:H - 2], axis=0)
+        applied.append(v)
+        plant.step(v)
+        traj.append(plant.qpos[qa].copy())
+    assert p._graphs is not None
+    rels = _check_selected_costs(p, outs, starts, H)
+    # the plant's 30 steps replayed by the oracle (one rollout, H = 30)
+    td = np.asarray(applied, dtype=np.float64).T.reshape(1, 6 * ticks)
+    want = pu.oracle.rollout(p.model, td, Q0, pu.W, PT, QT)["theta"].reshape(6, ticks).T
+    spread = np.zeros_like(want)
+    for sd in range(1, 9):
+        b = pu.oracle.rollout(p.model, td, Q0, pu.W, PT, QT, noise=1e-6, seed=sd)["theta"].reshape(6, ticks).T
+        spread = np.maximum(spread, np.abs(b - want))
+    err = np.abs(np.asarray(traj) - want)
+    assert (err <= np.maximum(1e-4, 2 * spread)).all(), (err.max(), spread.max())
+    print(f"C5 30 ticks: selected cost vs oracle worst {max(rels):.1e} median {np.median(rels):.1e}; "
+          f"plant vs oracle replay worst {err.max():.1e} rad (spread {spread.max():.1e})")

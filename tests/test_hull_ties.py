@@ -1,0 +1,76 @@
+"""Hull support ties: the support of a convex hull must
+not depend on where its hill climb starts.  A direction normal to a hull
+edge or face makes every vertex of it a maximum; the climb's end then
+depends on its start (the support start table's cell, the pair's hint) and
+on the last bits of the dot products.  The tie rule (oracle hull_tie, the
+kernel's sup_finish / tie_round) walks from the climb's end to the tie's
+lowest vertex index, so a start table whose every cell points at a random
+vertex of its hull gives bitwise the same rollouts -- a table resolution is
+a performance choice, not a parity change.  Without the rule (tie band 0)
+the same batch changes (the test's teeth).  CPU only: the fp64 oracle and
+its fp32 build over a dual-arm batch (URD/dual_arm_gripper_scene.xml)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from manipulator_mujoco_amd import cmodel, models
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+
+Q0 = np.array([1.5, -1.8, 1.75, -1.25, -1.6, 0.0])
+ARGS = (Q0, [20.0, 3.0, 80.0], [-0.3, -0.3, 0.5], [0.0, 1.0, 0.0, 0.0])
+
+
+@pytest.fixture(scope="module")
+def batch():
+    from diag_f32 import batch as make
+    m = models.load("dual_arm", 0.05)
+    return m, make(m, 256, 100, 4)
+
+
+def _scrambled(orig):
+    def f(mm):
+        adr, lut = orig(mm)
+        lut = np.array(lut, copy=True)
+        rng = np.random.default_rng(1)
+        R = cmodel.LUT_R
+        for g in range(len(mm.geom_type)):
+            if mm.geom_hulladr[g] >= 0 and mm.geom_hullnum[g] > 0 and adr[g] >= 0:
+                lut[adr[g]:adr[g] + 6 * R * R] = mm.geom_hulladr[g] + rng.integers(0, mm.geom_hullnum[g], 6 * R * R)
+        return adr, lut
+    return f
+
+
+def _costs(m, td, prec, scramble, monkeypatch):
+    with monkeypatch.context() as mp:
+        if scramble:
+            mp.setattr(cmodel, "hull_luts", _scrambled(cmodel.hull_luts))
+        if prec == "fp64":
+            return oracle.rollout(m, td, *ARGS, want_theta=False, workers=8)["cost4"]
+        r = oracle.Runner(m, 8, *ARGS, precision="fp32", exact_mask=4)
+        try:
+            return r.rollout(td).astype(np.float64)
+        finally:
+            r.close()
+
+
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_support_is_start_independent(batch, monkeypatch, prec):
+    m, td = batch
+    L = oracle.lib_f32() if prec == "fp32" else oracle.lib()
+    L.oracle_set_hull_tie.argtypes = [ctypes.c_float if prec == "fp32" else ctypes.c_double]
+    try:
+        for tie, same in ((1e-7, True), (0.0, False)):
+            L.oracle_set_hull_tie(tie)
+            a = _costs(m, td, prec, False, monkeypatch)
+            b = _costs(m, td, prec, True, monkeypatch)
+            if same:
+                np.testing.assert_array_equal(a, b, err_msg=f"{prec}: the start table moved a rollout")
+            else:  # teeth: without the rule the random starts end on other tied vertices
+                assert (a[:, 0] != b[:, 0]).any(), prec
+    finally:
+        L.oracle_set_hull_tie(1e-7)

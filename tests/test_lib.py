@@ -24,7 +24,7 @@ def test_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(_lib.EXPORTS) <= set(names)
-    assert lib.mpcr_abi_version() == 2  # status word layout of round 4 (include/mpcr.h)
+    assert lib.mpcr_abi_version() == 3  # status word layout of round 6 (include/mpcr.h)
 
 
 def test_model_blob_roundtrip_and_rejects_garbage():

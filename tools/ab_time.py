@@ -55,7 +55,7 @@ if hasattr(lib, "mpcr_rollout_occupancy"):
                f" wide {info[3]} blocks/CU, {info[4]} B LDS, {info[5]} VGPR]")
 e.rollout_cost(*args, cost4=c4, theta=th, thetadot=td, best_key=key, status=st)
 sv = st.cpu().numpy()
-rows = f" rows/step {float((sv >> 10).mean()) / H:.1f} max-rows p50/p90/p99 " + "/".join(
+rows = f" rows/step {float((sv >> 11).mean()) / H:.1f} max-rows p50/p90/p99 " + "/".join(
     str(int(np.percentile((sv >> 2) & 255, q))) for q in (50, 90, 99))
 print(f"{os.path.basename(sys.argv[1])}{occ}{rows} {name} median {np.median(ts):.3f} ms min {np.min(ts):.3f} "
       f"-> {n / np.median(ts) * 1e3:.0f} rollouts/s  cost0 {float(c4[:, 0].sum()):.6e}")

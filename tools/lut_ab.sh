@@ -1,5 +1,5 @@
 #!/bin/bash
-# Support start table resolution A/B (MPCR_LUT_R: the Python packer and the
+# Support start table resolution A/B (MPCR_AB_LUT_R: the Python packer and the
 # library must agree, so each variant runs with its own env).
 #   LUTS="16:cur16 64:lut64" bash tools/lut_ab.sh   (build_variants/lut/<name>.so)
 set -u
@@ -10,7 +10,7 @@ for round in 1 2; do
     r=${v%%:*}; name=${v#*:}
     for cfg in "dual_arm 1024 50" "dual_arm 4096 100"; do
       set -- $cfg
-      MPCR_LUT_R=$r MODEL=$1 N=$2 H=$3 R=3 timeout -k 10 200 python tools/ab_time.py build_variants/lut/$name.so > $OUT/${round}_${name}_$2.log 2>&1 || exit $?
+      MPCR_AB_LUT_R=$r MODEL=$1 N=$2 H=$3 R=3 timeout -k 10 200 python tools/ab_time.py build_variants/lut/$name.so > $OUT/${round}_${name}_$2.log 2>&1 || exit $?
       echo "$name $(grep median $OUT/${round}_${name}_$2.log | sed 's/\[.*\]//')"
     done
   done

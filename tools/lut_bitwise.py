@@ -1,4 +1,4 @@
-"""The C4 shard's cost4 from the library in argv[1] (packer at MPCR_LUT_R from
+"""The C4 shard's cost4 from the library in argv[1] (packer at MPCR_AB_LUT_R from
 the environment), saved to argv[2]: a bitwise comparison between support
 start-table resolutions (diagnostic)."""
 import os

@@ -25,6 +25,6 @@ for name in ("scene_mjx", "planner_scene", "ur5e_hande_mjx", "dual_arm"):
         e.rollout_cost(xi, MPCR_LAYOUT_XI, q0, (20., 3., 80.), (-0.3, -0.3, 0.5), (0., 1., 0., 0.), status=st)
         s = st.cpu().numpy()
         mx = (s >> 2) & 255
-        print(f"{name} seed {seed}: mean rows {np.mean(s >> 10) / H:.1f}  max-rows pct50/99/99.9/max "
+        print(f"{name} seed {seed}: mean rows {np.mean(s >> 11) / H:.1f}  max-rows pct50/99/99.9/max "
               f"{np.percentile(mx, 50):.0f}/{np.percentile(mx, 99):.0f}/{np.percentile(mx, 99.9):.0f}/{mx.max()}  "
               f"trunc {int((s & 1).sum())}")

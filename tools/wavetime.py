@@ -63,7 +63,7 @@ def main():
     st = torch.zeros(n, dtype=torch.int32, device="cuda")  # per-candidate rows: max (bits 2-9), sum (10-)
     e.rollout_cost(torch.tensor(xi, device="cuda"), MPCR_LAYOUT_XI, q0, w, pt, qt, status=st)
     sv = st.cpu().numpy()
-    rows_mean, rows_max = (sv >> 10) / H, (sv >> 2) & 255
+    rows_mean, rows_max = (sv >> 11) / H, (sv >> 2) & 255
     work = buf.reshape(-1)[4 * n:].reshape(n, 2)
     buf = buf.reshape(-1)[:4 * n].reshape(n, 4)
     newton, lsp, cvx = (work[:, 0] & 0xffffffff).astype(float), (work[:, 0] >> 32).astype(float), work[:, 1].astype(float)
