@@ -776,22 +776,35 @@ __device__ __forceinline__ int climb_round(const DevModel* __restrict__ m, int v
 // start table's cell, the pair's hint) and on the last bits of the dot
 // products (fp32 and fp64 pick differently).  From the climb's end v the
 // support walks to the lowest-index neighbour within kHullTie of v's value
-// while that neighbour's index is lower: on a tied edge or triangle that is
-// the tie's lowest index from whichever vertex the climb reached, so a start
-// table's resolution stays a performance choice, not a parity change.  One
-// walk round, out of line with scalar arguments (its call's spills stay on
-// this path): the lowest tied neighbour key of vertex v.
-__device__ __noinline__ uint32_t tie_round(const DevModel* __restrict__ m, int v, int deg, float lo, float l0,
-                                           float l1, float l2) {
+// while that neighbour's index is lower: the tie's lowest index from
+// whichever of its vertices the climb reached (the oracle's hull_tie), so a
+// start table's resolution stays a performance choice, not a parity change
+// (tests/test_hull_ties.py).  One walk round, out of line with scalar
+// arguments (its call's spills stay on this path; inlined, or folded into
+// the climb loop, the walk cost the hot climb registers or time): v's
+// coordinates and the key of its lowest tied neighbour.
+struct TieStep { float x, y, z; uint32_t tkey; };  // v's coordinates, its lowest tied neighbour's key
+__device__ __noinline__ TieStep tie_round(const DevModel* __restrict__ m, int v, int deg, float lo, float l0,
+                                          float l1, float l2) {
   uint32_t tkey = ~0u;
-  const int a = m->hull_info[v].x;
-#pragma unroll 1
-  for (int k = 0; k < deg; k++) {
-    const float4 w = k < 8 ? m->hull_head[(size_t)v * 8 + k] : m->hull_adjv[a + k];
-    const uint32_t wb = __float_as_uint(w.w);
-    if (w.x * l0 + w.y * l1 + w.z * l2 >= lo) tkey = min(tkey, __builtin_amdgcn_alignbit(wb, wb, 16));
+  const float l[3] = {l0, l1, l2};
+  float4 w[8];
+  const float4 x = m->hull_vert[v];
+#pragma unroll
+  for (int j = 0; j < 8; j++) w[j] = m->hull_head[(size_t)v * 8 + j];  // the head block's loads in flight together
+  float bn = 3e38f;  // (no neighbour is climbed to)
+  float4 hv;
+  int nb;
+  climb_scan(w, l, bn, hv, nb, lo, tkey);
+  if (deg > 8) {
+    const int a = m->hull_info[v].x, last = a + deg - 1;
+    for (int k0 = a + 8; k0 <= last; k0 += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) w[j] = m->hull_adjv[min(k0 + j, last)];
+      climb_scan(w, l, bn, hv, nb, lo, tkey);
+    }
   }
-  return tkey;
+  return TieStep{x.x, x.y, x.z, tkey};
 }
 
 // cube-map cell of a local direction (the model's hull_lut order, oracle
@@ -902,17 +915,14 @@ __device__ __forceinline__ void sup_finish(const DevModel* __restrict__ m, const
         v = nb & 0xffff;
         deg = nb >> 16;
       }
-#ifndef MPCR_TIE_WALK
-#define MPCR_TIE_WALK 1
-#endif
-      if (MPCR_TIE_WALK == 0 && ties) asm volatile("" ::"v"(tkey));  // (A/B: the tracking without the walk)
-      if (MPCR_TIE_WALK && kHullTie > 0.f && ties && (int)(tkey >> 16) < v) {  // a lower-index tied neighbour: walk (hull_tie)
+      if (kHullTie > 0.f && ties && (int)(tkey >> 16) < v) {  // a lower-index tied neighbour: walk (hull_tie)
         const float lo = best - kHullTie;
         for (int guard = 0; guard < 64 && (int)(tkey >> 16) < v; guard++) {
           v = tkey >> 16;
-          tkey = tie_round(m, v, tkey & 0xffff, lo, lu[0], lu[1], lu[2]);
+          const TieStep ts = tie_round(m, v, tkey & 0xffff, lo, lu[0], lu[1], lu[2]);
+          hv.x = ts.x; hv.y = ts.y; hv.z = ts.z;
+          tkey = ts.tkey;
         }
-        hv = m->hull_vert[v];
       }
     }
     p[0] = hv.x; p[1] = hv.y; p[2] = hv.z;

@@ -1059,12 +1059,25 @@ static int tied_neighbour(const mpcr_model_t* m, int v, double lo, const double 
   }
   return t;
 }
+static __thread long g_walk_stats[4]; /* diagnostic: walks, jumps, walks past the first jump */
+void oracle_walk_stats(long* out, int reset) {
+  if (out) memcpy(out, g_walk_stats, sizeof(g_walk_stats));
+  if (reset) memset(g_walk_stats, 0, sizeof(g_walk_stats));
+}
 static int hull_tie(const mpcr_model_t* m, int v, int t, double lo, const double lu[3]) {
   const int v0 = v;
   g_mpr_stats[6]++;
+  g_walk_stats[0]++;
   for (int guard = 0; guard < 64 && t >= 0 && t < v; guard++) {
     v = t;
     t = tied_neighbour(m, v, lo, lu);
+    g_walk_stats[1]++;
+    if (guard == 0 && t >= 0 && t < v) g_walk_stats[2]++;
+    if (guard == 0) {
+      int pl = 0;
+      for (int k = m->vert_faceadr[v]; k < m->vert_faceadr[v] + m->vert_facenum[v]; k++) pl |= m->face_vnum[m->vert_face[k]] >= 4;
+      g_walk_stats[3] += pl;
+    }
   }
   g_mpr_stats[7] += v != v0;
   g_tie_kind[g_sup_kind & 3][0]++;
