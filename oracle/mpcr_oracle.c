@@ -1028,8 +1028,10 @@ static __thread long g_mpr_stats[64]; /* per thread: the checker's pool threads 
    differently).  So the climb's last round also names the end v's
    lowest-index neighbour within HULL_TIE of v's value, and the support walks
    on to it while it is lower than the current vertex (the threshold fixed at
-   the climb end's value): on a tied edge or triangle that is the tie's
-   lowest index from whichever of its vertices the climb reached, as an
+   the climb end's value): an edge's lower end, a triangle's lowest vertex,
+   a polygon's lowest vertex unless the descent along its tied neighbours
+   stops at a local minimum -- from whichever tied vertex the climb reached
+   (tests/test_hull_ties.py), as an
    argmax over all vertices that takes the first of equal values (MJX's
    jnp.argmax support of a mesh) -- a support start table's resolution is a
    performance choice, not a parity change (VERDICT r5 item 1;
@@ -1041,6 +1043,14 @@ static __thread long g_mpr_stats[64]; /* per thread: the checker's pool threads 
    the walk: every tied vertex gives that value to within HULL_TIE.  Exact
    mode (EXACT_SUP): no tie rule. */
 static double g_hull_tie = 1e-7;
+static int g_hint_ge = 0;
+static __thread int g_from_hint;
+static __thread long g_walk_kind[4]; /* walks by (start: table 0 / hint 1) + (climb moved 0 / stayed 2) */
+void oracle_walk_kind(long* out, int reset) {
+  if (out) memcpy(out, g_walk_kind, sizeof(g_walk_kind));
+  if (reset) memset(g_walk_kind, 0, sizeof(g_walk_kind));
+}
+void oracle_set_hint_ge(int v) { g_hint_ge = v; }
 void oracle_set_hull_tie(double v) { g_hull_tie = v; } /* experiments: 0 = the plain climb's end */
 #define HULL_TIE ((g_exact & EXACT_SUP) ? 0.0 : g_hull_tie)
 static __thread int g_value_only; /* support_value's queries: no tie walk */
@@ -1073,11 +1083,7 @@ static int hull_tie(const mpcr_model_t* m, int v, int t, double lo, const double
     t = tied_neighbour(m, v, lo, lu);
     g_walk_stats[1]++;
     if (guard == 0 && t >= 0 && t < v) g_walk_stats[2]++;
-    if (guard == 0) {
-      int pl = 0;
-      for (int k = m->vert_faceadr[v]; k < m->vert_faceadr[v] + m->vert_facenum[v]; k++) pl |= m->face_vnum[m->vert_face[k]] >= 4;
-      g_walk_stats[3] += pl;
-    }
+
   }
   g_mpr_stats[7] += v != v0;
   g_tie_kind[g_sup_kind & 3][0]++;
@@ -1127,18 +1133,21 @@ static void support_rel(const mpcr_model_t* m, const odata* d, int g, const doub
       double best = dot3(m->hull_vert[v], lu);
       if (*hint >= 0) {
         const double bh = dot3(m->hull_vert[*hint], lu);
-        if (bh > best + SUP_BAND) { v = *hint; best = bh; }
+        if (g_hint_ge ? bh >= best + SUP_BAND : bh > best + SUP_BAND) { v = *hint; best = bh; g_from_hint = 1; }
       }
-      int tmin = -1; /* the last round's lowest-index neighbour within HULL_TIE of v */
+      const int v_start = v;
+      int tmin = -1, tcnt = 0; /* the last round's lowest-index neighbour within HULL_TIE of v, their count */
       for (;;) {
         int nb = v;
         g_mpr_stats[2]++;
         g_mpr_stats[3] += m->hull_adjnum[v];
         double bn = best + SUP_BAND; /* a neighbour must beat this; ties within the band go to the first */
         tmin = -1;
+        tcnt = 0;
         for (int k = m->hull_adjadr[v]; k < m->hull_adjadr[v] + m->hull_adjnum[v]; k++) {
           int u = m->hull_adj[k];
           double du = dot3(m->hull_vert[u], lu);
+          if (du >= best - HULL_TIE) tcnt++;
           if (du >= best - HULL_TIE && (tmin < 0 || u < tmin)) tmin = u;
           if (du > bn) { bn = du + SUP_BAND; nb = u; }
         }
@@ -1146,7 +1155,12 @@ static void support_rel(const mpcr_model_t* m, const odata* d, int g, const doub
         best = bn - SUP_BAND;
         v = nb;
       }
-      if (HULL_TIE > 0 && !g_value_only && tmin >= 0 && tmin < v) v = hull_tie(m, v, tmin, best - HULL_TIE, lu);
+      if (HULL_TIE > 0 && !g_value_only && tmin >= 0 && tmin < v) {
+        g_walk_kind[(g_from_hint ? 1 : 0) + (v == v_start ? 2 : 0)]++;
+        g_walk_stats[3] += tcnt == 1;
+        v = hull_tie(m, v, tmin, best - HULL_TIE, lu);
+      }
+      g_from_hint = 0;
       memcpy(p, m->hull_vert[v], sizeof(p));
       *hint = v;
       break;
