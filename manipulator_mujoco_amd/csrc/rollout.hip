@@ -905,7 +905,9 @@ __device__ __forceinline__ void sup_finish(const DevModel* __restrict__ m, const
       if (hint >= 0) {
         const float4 hh = q.hh;
         const float bh = hh.x * lu[0] + hh.y * lu[1] + hh.z * lu[2];
-        if (bh > best + kSupBand) { v = hint; hv = hh; deg = __float_as_int(hh.w); best = bh; }
+        // (on equal values the hint: after a tie walk it is the tie's lowest
+        // index, so the climb then ends where it starts, with no walk)
+        if (bh >= best + kSupBand) { v = hint; hv = hh; deg = __float_as_int(hh.w); best = bh; }
       }
       uint32_t tkey = ~0u;
       for (int guard = 0; guard < 4096; guard++) {

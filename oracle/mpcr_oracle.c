@@ -1043,7 +1043,7 @@ static __thread long g_mpr_stats[64]; /* per thread: the checker's pool threads 
    the walk: every tied vertex gives that value to within HULL_TIE.  Exact
    mode (EXACT_SUP): no tie rule. */
 static double g_hull_tie = 1e-7;
-static int g_hint_ge = 0;
+static int g_hint_ge = 1; /* the hint on equal values (the kernel's start rule; 0: the table's) */
 static __thread int g_from_hint;
 static __thread long g_walk_kind[4]; /* walks by (start: table 0 / hint 1) + (climb moved 0 / stayed 2) */
 void oracle_walk_kind(long* out, int reset) {
@@ -1128,12 +1128,16 @@ static void support_rel(const mpcr_model_t* m, const odata* d, int g, const doub
       double lu[3] = {0, 0, 0};
       if (ln > 0) for (int k = 0; k < 3; k++) lu[k] = l[k] / ln;
       /* start: the table vertex of l's cube-map cell, or the hint (where the
-         previous query on this pair ended) when it beats that by the band */
+         previous query on this pair ended) when it reaches that by the band
+         -- on equal values the hint, as the kernel (after a tie walk the hint
+         is the tie's lowest index) */
       int v = m->geom_lutadr[g] >= 0 ? m->hull_lut[m->geom_lutadr[g] + lut_cell(l)] : m->geom_hulladr[g];
       double best = dot3(m->hull_vert[v], lu);
       if (*hint >= 0) {
         const double bh = dot3(m->hull_vert[*hint], lu);
-        if (g_hint_ge ? bh >= best + SUP_BAND : bh > best + SUP_BAND) { v = *hint; best = bh; g_from_hint = 1; }
+        if (g_hint_ge == 2 ? bh >= best - HULL_TIE : (g_hint_ge ? bh >= best + SUP_BAND : bh > best + SUP_BAND)) {
+          v = *hint; best = bh; g_from_hint = 1;
+        }
       }
       const int v_start = v;
       int tmin = -1, tcnt = 0; /* the last round's lowest-index neighbour within HULL_TIE of v, their count */

@@ -152,6 +152,10 @@ def main():
           f"probe F (fp32 oracle) well-misses {int((well & (pf >= pu.TOL)).sum())}; {label} well-misses {len(miss)}, "
           f"worst {rel[well].max():.2e}")
     order = miss[np.argsort(-rel[miss])]
+    cs_ = [x for x in sys.argv if x.startswith("--cand=")]
+    if cs_:  # triage these candidates whatever their conditioning
+        order = np.array([int(x) for x in cs_[0][7:].split(",")])
+        print("chosen candidates:", " ".join(f"{i}: rel {rel[i]:.1e} probe-A {sens[i]:.1e}" for i in order))
     # the fp32 oracle's components on the same inputs (is the GPU nearer the
     # fp32 restatement than the fp64 one?)
     with oracle.exact(mask):
