@@ -66,6 +66,7 @@ def test_support_is_start_independent(batch, monkeypatch, prec):
     try:
         for tie, same in ((1e-7, True), (0.0, False)):
             L.oracle_set_hull_tie(tie)
+            L.oracle_set_hint_ge(1 if same else 0)  # the teeth: the plain climb (the table's start on equal values)
             a = _costs(m, td, prec, False, monkeypatch)
             b = _costs(m, td, prec, True, monkeypatch)
             if same:
@@ -74,3 +75,4 @@ def test_support_is_start_independent(batch, monkeypatch, prec):
                 assert (a[:, 0] != b[:, 0]).any(), prec
     finally:
         L.oracle_set_hull_tie(1e-7)
+        L.oracle_set_hint_ge(1)
