@@ -36,6 +36,9 @@ fi
 if has c5ticks; then  # BASELINE configs[4]: 30 closed-loop ticks
   run bench_c5_30 400 python bench.py --config c5 --no-cpu-baseline --ticks 30 --warmup 1
 fi
+if has c5share; then  # the C5 tick's stages at one rank's share on 8 GPUs
+  run c5_share_stages 300 python tools/c5_share_stages.py
+fi
 if has c3precise; then  # C3 parity on the fast-math and the precise build, same batch
   MPCR_PARITY_LOG=$OUT/parity_c3_fast.jsonl run c3_fast 400 $PYT -s tests/test_gpu_parity.py -k test_parity_c3_full
   MPCR_LIB=build_variants/keep/precise.so MPCR_PARITY_LOG=$OUT/parity_c3_precise.jsonl \
