@@ -100,6 +100,9 @@ namespace mpcr {
 #ifndef MPCR_ABL_DEEP
 #define MPCR_ABL_DEEP 0
 #endif
+#ifndef MPCR_CB_SKIP
+#define MPCR_CB_SKIP 1  // capsule-box: skip the interior knots when no lane's minimum is inside (narrow_lane)
+#endif
 #ifndef MPCR_ABL_FUNC
 #define MPCR_ABL_FUNC 0
 #endif
@@ -1841,9 +1844,14 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
     mtv(a, R2, A);
     mtv(dd, R2, B);
     float tlo = -1.f, thi = 2.f, flo = 0.f, fhi = 0.f;
-    // knots: 0, 1, (+-h_k - a_k)/dd_k inside (0,1)
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
+    // knots: 0, 1, (+-h_k - a_k)/dd_k inside (0,1), where the squared
+    // distance's derivative fp (piecewise linear, non-decreasing: the
+    // distance is convex along the segment) is evaluated.  The interior knots
+    // only matter when fp changes sign inside (fp(0) < 0 <= fp(1)); when no
+    // lane's does, the minimum is an end on every lane (ts 0 or 1 below, as
+    // the full scan gives) and the six interior knots are skipped (C3: most
+    // steps of the 20 robot capsule / box pairs, MPCR_CB_SKIP)
+    auto knot = [&](int i) {
       float t;
       bool ok = true;
       if (i == 0) t = 0.f;
@@ -1856,15 +1864,24 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
         ok = ok && t > 0.f && t < 1.f;
       }
       if (ok) {
+        // x - clamp(x, -h, h) is +-(|x| - h) outside the slab, 0 inside --
+        // the same value as the sign-selected excess, one v_med3 instead
+        // of the compares and selects
         float fp = 0.f;
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-          float x = a[k] + t * dd[k], e = fabsf(x) - h[k];
-          if (e > 0) fp += 2.f * dd[k] * (x > 0 ? e : -e);
+          const float x = a[k] + t * dd[k];
+          fp += 2.f * dd[k] * (x - __builtin_amdgcn_fmed3f(x, -h[k], h[k]));
         }
         if (fp < 0) { if (t > tlo) { tlo = t; flo = fp; } }
         else { if (t < thi) { thi = t; fhi = fp; } }
       }
+    };
+    knot(0);
+    knot(1);
+    if (!MPCR_CB_SKIP || hballot<S::CPW>(tlo == 0.f && thi == 1.f) != 0ull) {
+#pragma unroll
+      for (int i = 2; i < 8; i++) knot(i);
     }
     float ts;
     if (tlo < 0) ts = 0.f;
