@@ -63,7 +63,8 @@ extern "C" {
 #define MPCR_STATUS_NONFINITE(s) (((s) >> 1) & 1)           /* non-finite state           */
 #define MPCR_STATUS_MAX_ROWS(s) (((s) >> 2) & 255)          /* busiest step's rows (<= 255) */
 #define MPCR_STATUS_SYNC(s) (((s) >> 10) & 1)               /* two-wave handshake timed out:
-                                                                the candidate's outputs are void */
+                                                                the candidate's outputs are void
+                                                                and its cost is +inf */
 #define MPCR_STATUS_ROWS_SUM(s) ((unsigned)(s) >> 11)       /* rows summed over the horizon */
 #define MPCR_STATUS_FAILED(s) (((s) & 2) | ((s) & (1 << 10)))  /* no usable result */
 

@@ -4823,7 +4823,10 @@ __global__ void __launch_bounds__(WAVE * WPC, WIDE ? MPCR_W_WAVES : MPCR_N_WAVES
   finite = hballot<S::CPW>(!finite) == 0;
   if (!finite) status |= 2;
   if (lane == 0 && live) {
-    const float cost = s.par[PAR_W] * cost_g + s.par[PAR_W + 1] * cost_r + s.par[PAR_W + 2] * cost_c;
+    // a lost two-wave handshake (MPCR_STATUS_SYNC) voids the rollout: +inf
+    // keeps it out of the argmin and the elites (a NaN would win the argmin)
+    const float cost = (status & (1 << 10)) ? __builtin_inff()
+                                            : s.par[PAR_W] * cost_g + s.par[PAR_W + 1] * cost_r + s.par[PAR_W + 2] * cost_c;
     args.cost4[4 * (size_t)b + 0] = cost;
     args.cost4[4 * (size_t)b + 1] = cost_g;
     args.cost4[4 * (size_t)b + 2] = cost_r;
