@@ -54,6 +54,7 @@ L32.oracle_set_hull_tie.argtypes = [ctypes.c_float]
 for prec in ("fp64", "fp32"):
     for t in (0.0, tie):
         (L32 if prec == "fp32" else L).oracle_set_hull_tie(t)
+        (L32 if prec == "fp32" else L).oracle_set_hint_ge(1 if t > 0 else 0)  # no rule: the plain climb's start
         res = []
         for scr in (False, True):
             cmodel.hull_luts = scrambled if scr else orig
@@ -65,6 +66,7 @@ for prec in ("fp64", "fp32"):
                 res.append(r.rollout(td).astype(np.float64))
                 r.close() if hasattr(r, "close") else None
         cmodel.hull_luts = orig
+        (L32 if prec == "fp32" else L).oracle_set_hint_ge(1)
         a, b = res
         rel = np.abs(a[:, 0] - b[:, 0]) / np.abs(a[:, 0])
         print(f"{prec} hull tie {t:g}: candidates differing {(a[:, 0] != b[:, 0]).sum()}/{n}, >1e-6 "
