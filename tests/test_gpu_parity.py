@@ -536,3 +536,48 @@ def test_dual_arm_compact_mass_matrix_bitwise_slab(torch_cuda, monkeypatch):
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
     assert_no_sync_loss(out[1][3])
+
+
+def test_kernel_support_is_start_independent(torch_cuda, monkeypatch):
+    """The kernel's hull supports do not depend on where a climb starts
+    (the tie walk of sup_finish / tie_round): the dual arm
+    rolled out with a support start table whose every cell points at a random
+    vertex of its hull (the engine then marks no cell exact, so every query
+    climbs from there) gives bitwise the same costs, theta and status as with
+    the model's own table -- a table resolution is a performance choice, not
+    a parity change."""
+    torch = torch_cuda
+    from manipulator_mujoco_amd import cmodel
+    n, H = 1024, 50
+    m = models.load("dual_arm", 0.05)
+    _, P, Pd, _ = basis.planner_basis(H, 0.05)
+    xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
+    orig = cmodel.hull_luts
+
+    def scrambled(mm):
+        adr, lut = orig(mm)
+        lut = np.array(lut, copy=True)
+        rng = np.random.default_rng(1)
+        R = cmodel.LUT_R
+        for g in range(len(mm.geom_type)):
+            if mm.geom_hulladr[g] >= 0 and mm.geom_hullnum[g] > 0 and adr[g] >= 0:
+                lut[adr[g]:adr[g] + 6 * R * R] = mm.geom_hulladr[g] + rng.integers(0, mm.geom_hullnum[g], 6 * R * R)
+        return adr, lut
+
+    out = []
+    for scr in (False, True):
+        with monkeypatch.context() as mp:
+            if scr:
+                mp.setattr(cmodel, "hull_luts", scrambled)
+            e = Engine(m, H, n, Pd)
+        st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+        th = torch.empty((n, 6 * H), device="cuda:0")
+        c = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, theta=th, status=st).clone()
+        torch.cuda.synchronize()
+        out.append((c.cpu().numpy(), th.cpu().numpy(), st.cpu().numpy()))
+        del e
+    (ca, ta, sa), (cb, tb, sb) = out
+    diff = (ca != cb).any(axis=1) | (ta != tb).any(axis=1)
+    rel = np.abs(ca[:, 0].astype(np.float64) - cb[:, 0]) / np.abs(ca[:, 0])
+    print(f"start table scrambled: {int(diff.sum())}/{n} candidates differ, worst cost rel {rel.max():.1e}")
+    assert not diff.any() and np.array_equal(sa, sb)
