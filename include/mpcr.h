@@ -52,11 +52,12 @@
 extern "C" {
 #endif
 
-/* ABI version.  3 (round 6): bit 10 reports a lost two-wave handshake
+/* ABI version.  4 (round 6): model format v9 without the support start
+   table, which the engine builds (mpcr_model_hull_starts).  3: bit 10 reports a lost two-wave handshake
    (MPCR_STATUS_SYNC), so rows-summed moved to bit 11.  2 (round 4): the
    max-rows field widened to 8 bits (version 1: 6 bits << 2, sum << 8).
    Decode with the accessors below, not raw shifts. */
-#define MPCR_ABI_VERSION 3
+#define MPCR_ABI_VERSION 4
 
 /* the per-candidate status word of mpcr_rollout_cost / _dp */
 #define MPCR_STATUS_TRUNCATED(s) ((s) & 1)                  /* constraint rows truncated  */
@@ -111,6 +112,20 @@ int mpcr_model_load(const char* path, double timestep, mpcr_model** out);
 int mpcr_model_set_timestep(mpcr_model* m, double timestep);
 int mpcr_model_info(const mpcr_model* m, int* nq, int* nv, int* nslot, int* nctrl, int* npair);
 void mpcr_model_free(mpcr_model* m);
+/* The support start table an engine builds for m's convex hulls (model
+   format v9 dropped it from the blob; engine.hip hull_start_table): R x R
+   cells on each of the 6 cube faces (R = 0: the library's MPCR_LUT_R), cell
+   (2 axis + negative) R^2 + iu R + iv (rollout.hip lut_cell), each naming
+   the global hull vertex extreme along the cell centre (fp64; the lowest
+   index among exact ties).  geom_adr[ngeom] (nullable) receives each geom's
+   first cell (-1: no hull), cells (nullable) all of them when cap holds the
+   count.  Returns the cell count (< 0: error).  Host only, no device
+   (tests/test_hull_lut.py). */
+int64_t mpcr_model_hull_starts(const mpcr_model* m, int R, int32_t* geom_adr, int32_t* cells, int64_t cap);
+/* Test knob (the start-independence tests): engines created while seed != 0
+   start every hull climb at a vertex of its hull hashed from (seed, geom,
+   cell) instead of the extreme one.  Process-wide; returns the previous seed. */
+uint64_t mpcr_set_hull_start_scramble(uint64_t seed);
 
 /* engines: device copy of the model + the Pdot basis (horizon x nbasis,
    row-major fp32, bernstein_coeff_ordern_new(..)[1]) + scratch for max_n. */

@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 #define MPCR_MODEL_MAGIC   0x4d504352u /* 'MPCR' */
-#define MPCR_MODEL_VERSION 8
+#define MPCR_MODEL_VERSION 9 /* v9: no support start table (the engine builds it) */
 
 #define MPCR_MAX_BODY   48
 #define MPCR_MAX_JNT    40
@@ -38,13 +38,13 @@ extern "C" {
 #define MPCR_MAX_ACT    16   /* actuators */
 #define MPCR_MAX_HULLV  8192 /* convex-hull vertices of all collision meshes */
 #define MPCR_MAX_HULLA  49152 /* hull-graph adjacency entries */
-/* support start table: 6 cube faces x R x R cells per hull (round 5: 16 -> 128;
-   finer cells start the hull climbs nearer the answer and more of them are
-   exact, DESIGN.md: C4 shard 47.1 -> 44.1 ms, bitwise the same supports) */
+/* support start table resolution: 6 cube faces x R x R cells per hull.  Not
+   part of the blob since v9 -- the engine builds the table from hull_vert
+   (engine.hip hull_start_table), so R is the library's build-time choice
+   (round 5: 16 -> 128, round 6: 256; DESIGN.md perf log) */
 #ifndef MPCR_LUT_R
-#define MPCR_LUT_R      128
+#define MPCR_LUT_R      256
 #endif
-#define MPCR_MAX_HULLLUT (24 * 6 * MPCR_LUT_R * MPCR_LUT_R) /* 24 hulls */
 #define MPCR_MAX_FACE   12288 /* polygon faces of the polyhedron-pair hulls and boxes */
 #define MPCR_MAX_FACEV  49152 /* face polygon vertex entries (<= MPCR_FACE_MAXV each) */
 #define MPCR_MAX_VFACE  65536 /* vertex -> incident face entries */
@@ -260,13 +260,6 @@ typedef struct mpcr_model_t {
   double ten_solimp[MPCR_MAX_TEN][5];
   double ten_margin[MPCR_MAX_TEN];
   double ten_invweight0[MPCR_MAX_TEN]; /* J_ten M^-1 J_ten^T at qpos0 */
-  /* support start table of every hull (derived from hull_vert when packed):
-     the local direction's cube-map cell (mpcr_lut_cell) names the vertex
-     extreme along the cell centre; hull climbs start there (or at the
-     query's hint if that beats it by the tie band) */
-  int32_t geom_lutadr[MPCR_MAX_GEOM]; /* first cell, -1: no hull          */
-  int32_t hull_lut[MPCR_MAX_HULLLUT];  /* global vertex index per cell     */
-
   /* v7: polygon faces of the hulls and boxes of polyhedron pairs (mesh-mesh,
      box-mesh): the face-clipping contact manifold
      (mujoco-mjx 3.3.1 convex_convex: a reference face, the incident face

@@ -28,7 +28,7 @@ EXPORTS = (
     "mpcr_cem_factor", "mpcr_cem_sample_project", "mpcr_project", "mpcr_cem_update", "mpcr_rollout_cost_dp",
     "mpcr_plant_create", "mpcr_plant_free", "mpcr_plant_set_state", "mpcr_plant_get_state", "mpcr_plant_step",
     "mpcr_rollout_occupancy", "mpcr_set_two_wave_max_n", "mpcr_engine_dispatches", "mpcr_comm_unique_id", "mpcr_comm_init", "mpcr_comm_free", "mpcr_comm_allreduce_key",
-    "mpcr_comm_allgather", "mpcr_comm_gather_elites",
+    "mpcr_comm_allgather", "mpcr_comm_gather_elites", "mpcr_model_hull_starts", "mpcr_set_hull_start_scramble",
 )
 _VOID = ("mpcr_last_error", "mpcr_model_free", "mpcr_engine_free", "mpcr_best_key_decode", "mpcr_cem_free",
          "mpcr_plant_free", "mpcr_comm_free")
@@ -94,9 +94,13 @@ def load():
     lib.mpcr_comm_allreduce_key.argtypes = [vp, vp, i, vp]
     lib.mpcr_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
     lib.mpcr_comm_gather_elites.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
+    lib.mpcr_model_hull_starts.argtypes = [vp, i, P(ctypes.c_int32), P(ctypes.c_int32), ctypes.c_int64]
+    lib.mpcr_set_hull_start_scramble.argtypes = [u64]
     for name in EXPORTS + ("mpcr_rollout_trace", "mpcr_plant_step_debug", "mpcr_plant_dbg_size"):
         if name not in _VOID:
             getattr(lib, name).restype = i
+    lib.mpcr_model_hull_starts.restype = ctypes.c_int64
+    lib.mpcr_set_hull_start_scramble.restype = u64
     _lib = lib
     return lib
 

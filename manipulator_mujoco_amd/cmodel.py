@@ -7,24 +7,17 @@ Kept field-for-field identical to the C header; ``tests/test_model.py`` checks
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 
 MAGIC = 0x4D504352
-VERSION = 8  # v8: the support start table at MPCR_LUT_R = 128
+VERSION = 9  # v9: no support start table (the engine builds it from hull_vert)
 
 MAX_BODY, MAX_JNT, MAX_DOF, MAX_NQ = 48, 40, 32, 48
 MAX_GEOM, MAX_SITE, MAX_PAIR, MAX_EQ = 128, 24, 768, 8
 MAX_SLOT, MAX_CTRL, MAX_ACT = 512, 8, 16
 MAX_HULLV, MAX_HULLA = 8192, 49152
 MAX_TEN = 4
-# the support start table resolution: mpcr_model.h MPCR_LUT_R, which the
-# engine and the oracle fix at build time.  A constant here; the A/B tool
-# (tools/lut_ab.sh) packs other resolutions through MPCR_AB_LUT_R together
-# with a library built for them.
-LUT_R = int(os.environ.get("MPCR_AB_LUT_R", 128))
-MAX_HULLLUT = 24 * 6 * LUT_R * LUT_R
 MAX_FACE, MAX_FACEV, MAX_VFACE, FACE_MAXV = 12288, 49152, 65536, 16
 
 COL_PLANE_CAPSULE, COL_PLANE_BOX, COL_CAPSULE_CAPSULE, COL_CAPSULE_BOX, COL_BOX_BOX = 0, 1, 2, 3, 4
@@ -111,7 +104,6 @@ class mpcr_model_t(ctypes.Structure):
         ("ten_range", _a(_d, MAX_TEN, 2)), ("ten_solref", _a(_d, MAX_TEN, 2)),
         ("ten_solimp", _a(_d, MAX_TEN, 5)), ("ten_margin", _a(_d, MAX_TEN)),
         ("ten_invweight0", _a(_d, MAX_TEN)),
-        ("geom_lutadr", _a(_i, MAX_GEOM)), ("hull_lut", _a(_i, MAX_HULLLUT)),
         ("nface", _i), ("nfacev", _i), ("nvface", _i), ("pad6", _i),
         ("geom_faceadr", _a(_i, MAX_GEOM)), ("geom_facenum", _a(_i, MAX_GEOM)), ("geom_cornadr", _a(_i, MAX_GEOM)),
         ("face_vadr", _a(_i, MAX_FACE)), ("face_vnum", _a(_i, MAX_FACE)), ("face_vert", _a(_i, MAX_FACEV)),
@@ -141,62 +133,6 @@ def _fill(dst, src):
         rows[:, :src.shape[1]] = src
         flat = rows.ravel()
     view.reshape(-1)[:flat.size] = flat.astype(view.dtype)
-
-
-def lut_cell_dirs(R=LUT_R):
-    """Cell-centre directions of the support start table, cell order
-    (2 axis + negative) * R * R + iu * R + iv with u, v the components
-    (axis + 1) % 3, (axis + 2) % 3 (see mpcr_lut_cell in the kernel/oracle)."""
-    c = -1.0 + (2.0 * np.arange(R) + 1.0) / R
-    out = np.zeros((6, R, R, 3))
-    for f in range(6):
-        ax, neg = f // 2, f % 2
-        out[f, :, :, ax] = -1.0 if neg else 1.0
-        out[f, :, :, (ax + 1) % 3] = c[:, None]
-        out[f, :, :, (ax + 2) % 3] = c[None, :]
-    return out.reshape(-1, 3)
-
-
-_LUT_CACHE = {}
-
-
-def _hull_lut(v, R):
-    """Per cell of the cube map the vertex of v extreme along the cell centre
-    (lowest index on ties), directions in chunks (R = 128: 98 304 cells); the
-    same hull at the same resolution is computed once per process."""
-    key = (R, v.shape, v.tobytes())
-    hit = _LUT_CACHE.get(key)
-    if hit is not None:
-        return hit
-    dirs = lut_cell_dirs(R)
-    out = np.empty(len(dirs), dtype=np.int64)
-    step = max(1, (1 << 22) // max(1, len(v)))
-    for c0 in range(0, len(dirs), step):
-        out[c0:c0 + step] = np.argmax(dirs[c0:c0 + step] @ v.T, axis=1)
-    if len(_LUT_CACHE) > 64:
-        _LUT_CACHE.clear()
-    _LUT_CACHE[key] = out
-    return out
-
-
-def hull_luts(m):
-    """geom_lutadr, hull_lut: per hull and cell the vertex extreme along the
-    cell centre (lowest index on ties; any vertex is a valid climb start)."""
-    ng = int(getattr(m, "ngeom", 0))
-    adr = -np.ones(ng, dtype=np.int64)
-    lut = []
-    hadr = np.asarray(getattr(m, "geom_hulladr", -np.ones(ng)), dtype=np.int64)
-    hnum = np.asarray(getattr(m, "geom_hullnum", np.zeros(ng)), dtype=np.int64)
-    if int(getattr(m, "nhullv", 0)) == 0:
-        return adr, np.zeros(0, dtype=np.int64)
-    verts = np.asarray(m.hull_vert, dtype=np.float64).reshape(-1, 3)
-    for g in range(ng):
-        if hadr[g] < 0 or hnum[g] <= 0:
-            continue
-        v = verts[hadr[g]:hadr[g] + hnum[g]]
-        adr[g] = sum(len(x) for x in lut)
-        lut.append(hadr[g] + _hull_lut(v, LUT_R))
-    return adr, (np.concatenate(lut) if lut else np.zeros(0, dtype=np.int64))
 
 
 def pack(m) -> mpcr_model_t:
@@ -229,10 +165,4 @@ def pack(m) -> mpcr_model_t:
         attr = _ALIASES.get(name, name)
         if hasattr(m, attr):
             _fill(getattr(s, name), getattr(m, attr))
-    adr, lut = hull_luts(m)
-    if lut.size > MAX_HULLLUT:
-        raise ValueError(f"model hull start tables {lut.size} exceed capacity {MAX_HULLLUT}")
-    np.ctypeslib.as_array(s.geom_lutadr)[:] = -1
-    _fill(s.geom_lutadr, adr)
-    _fill(s.hull_lut, lut)
     return s

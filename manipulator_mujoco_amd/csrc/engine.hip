@@ -4,6 +4,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
@@ -11,6 +12,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mpcr.h"
@@ -180,15 +182,6 @@ static int check_model(const mpcr_model_t& m) {
   for (int g = 0; g < m.ngeom; g++) {
     if (m.geom_hulladr[g] >= 0 && m.geom_hulladr[g] + m.geom_hullnum[g] > m.nhullv)
       return fail(MPCR_EMODEL, "geom %d hull outside the vertex table", g);
-    if (m.geom_hulladr[g] >= 0 && m.geom_hullnum[g] > 0) {  // the support start table (cmodel.hull_luts)
-      const int la = m.geom_lutadr[g], nc = 6 * MPCR_LUT_R * MPCR_LUT_R;
-      if (la < 0 || la + nc > MPCR_MAX_HULLLUT) return fail(MPCR_EMODEL, "geom %d has no hull start table", g);
-      for (int c = 0; c < nc; c++) {
-        const int v = m.hull_lut[la + c];
-        if (v < m.geom_hulladr[g] || v >= m.geom_hulladr[g] + m.geom_hullnum[g])
-          return fail(MPCR_EMODEL, "geom %d start table names vertex %d outside its hull", g, v);
-      }
-    }
   }
   for (int v = 0; v < m.nhullv; v++)
     if (m.hull_adjadr[v] < 0 || m.hull_adjadr[v] + m.hull_adjnum[v] > m.nhulla)
@@ -314,6 +307,116 @@ extern "C" int mpcr_model_info(const mpcr_model* m, int* nq, int* nv, int* nslot
 
 extern "C" void mpcr_model_free(mpcr_model* m) { delete m; }
 
+// ---- support start table (model v9: built here from hull_vert, not packed) ----
+// Per hull and cube-map cell (6 faces x R x R, rollout.hip lut_cell order) the
+// vertex extreme along the cell centre, in fp64.  The cells of a hull run in
+// scan order, each climbing the hull graph (strict ascent) from the previous
+// cell's vertex -- neighbouring cells mostly share one, so a cell costs a
+// round or two -- and then taking the lowest index among the exactly tied
+// maxima reachable along tied edges.  Any vertex of the hull would do as a
+// start: the kernel's tie walk makes its supports start-independent
+// (tests/test_gpu_parity.py), so R is a speed choice, and the extreme vertex
+// keeps the climbs short and lets the engine mark cells exact.
+static std::atomic<uint64_t> g_start_scramble{0};
+
+static uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+template <class F>
+static void for_each_hull_parallel(const std::vector<int>& hulls, F&& f) {
+  const int nt = (int)std::min<size_t>(hulls.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+  if (nt <= 1) {
+    for (int g : hulls) f(g);
+    return;
+  }
+  std::atomic<int> next{0};
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nt; t++)
+    pool.emplace_back([&] {
+      for (int i; (i = next.fetch_add(1)) < (int)hulls.size();) f(hulls[i]);
+    });
+  for (auto& t : pool) t.join();
+}
+
+// geom_adr[ngeom]: each geom's first cell (-1: no hull); returns the cell
+// count.  cells (nullable): the global vertex of every cell; scramble != 0
+// names a hashed vertex of the hull instead (the start-independence tests).
+static int64_t hull_start_table(const mpcr_model_t& m, int R, uint64_t scramble, int32_t* geom_adr,
+                                int32_t* cells) {
+  const int64_t nc = 6LL * R * R;
+  int64_t n = 0;
+  std::vector<int> hulls;
+  std::vector<int64_t> first(m.ngeom, -1);
+  for (int g = 0; g < m.ngeom; g++)
+    if (m.geom_hulladr[g] >= 0 && m.geom_hullnum[g] > 0) {
+      first[g] = n;
+      n += nc;
+      hulls.push_back(g);
+    }
+  if (geom_adr)
+    for (int g = 0; g < m.ngeom; g++) geom_adr[g] = (int32_t)first[g];
+  if (!cells) return n;
+  std::vector<double> cen(R);
+  for (int i = 0; i < R; i++) cen[i] = -1.0 + (2.0 * i + 1.0) / R;
+  for_each_hull_parallel(hulls, [&](int g) {
+    const int a = m.geom_hulladr[g], na = m.geom_hullnum[g];
+    int32_t* out = cells + first[g];
+    if (scramble) {
+      for (int64_t c = 0; c < nc; c++) out[c] = a + (int)(mix64(scramble ^ ((uint64_t)g << 40) ^ (uint64_t)c) % na);
+      return;
+    }
+    std::vector<int> tied;
+    int v = a;
+    for (int64_t c = 0; c < nc; c++) {
+      const int f = (int)(c / ((int64_t)R * R)), iu = (int)((c / R) % R), iv = (int)(c % R), ax = f / 2;
+      double d[3];
+      d[ax] = (f & 1) ? -1.0 : 1.0;
+      d[(ax + 1) % 3] = cen[iu];
+      d[(ax + 2) % 3] = cen[iv];
+      auto val = [&](int u) { return m.hull_vert[u][0] * d[0] + m.hull_vert[u][1] * d[1] + m.hull_vert[u][2] * d[2]; };
+      double best = val(v);
+      for (;;) {
+        int nb = v;
+        for (int k = m.hull_adjadr[v]; k < m.hull_adjadr[v] + m.hull_adjnum[v]; k++) {
+          const int u = m.hull_adj[k];
+          const double du = val(u);
+          if (du > best) { best = du; nb = u; }
+        }
+        if (nb == v) break;
+        v = nb;
+      }
+      tied.assign(1, v);
+      int lo = v;
+      for (size_t i = 0; i < tied.size() && tied.size() < 256; i++)
+        for (int k = m.hull_adjadr[tied[i]]; k < m.hull_adjadr[tied[i]] + m.hull_adjnum[tied[i]]; k++) {
+          const int u = m.hull_adj[k];
+          if (val(u) == best && std::find(tied.begin(), tied.end(), u) == tied.end()) {
+            tied.push_back(u);
+            lo = std::min(lo, u);
+          }
+        }
+      out[c] = lo;
+    }
+  });
+  return n;
+}
+
+extern "C" int64_t mpcr_model_hull_starts(const mpcr_model* m, int R, int32_t* geom_adr, int32_t* cells, int64_t cap) {
+  if (!m) return fail(MPCR_EINVAL, "null model");
+  if (R == 0) R = MPCR_LUT_R;
+  if (R < 1 || R > 1024) return fail(MPCR_EINVAL, "table resolution %d outside 1..1024", R);
+  const int64_t n = hull_start_table(m->m, R, 0, geom_adr, nullptr);
+  if (cells && cap >= n) hull_start_table(m->m, R, 0, nullptr, cells);
+  return n;
+}
+
+extern "C" uint64_t mpcr_set_hull_start_scramble(uint64_t seed) { return g_start_scramble.exchange(seed); }
+
 // ---------------------------------------------------------------------------
 // device model
 
@@ -336,7 +439,7 @@ static void h_rot(double r[3], const double q[4], const double v[3]) {
   for (int i = 0; i < 3; i++) r[i] = m[3 * i] * v[0] + m[3 * i + 1] * v[1] + m[3 * i + 2] * v[2];
 }
 
-static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
+static int build_dev_model(const mpcr_model_t& m, const int32_t* lutadr, DevModel& d) {
   std::memset(&d, 0, sizeof(d));
   // dynamic bodies (not welded to the world), in topological order
   std::vector<int> dmap(m.nbody, -1);
@@ -597,7 +700,7 @@ static int build_dev_model(const mpcr_model_t& m, DevModel& d) {
     d.geom_rbound[i] = (float)m.geom_rbound[g];
     d.geom_hulladr[i] = m.geom_hulladr[g];
     d.geom_hullnum[i] = m.geom_hullnum[g];
-    d.geom_lutadr[i] = m.geom_lutadr[g];
+    d.geom_lutadr[i] = lutadr[g];
     d.geom_faceadr[i] = m.geom_faceadr[g];
     d.geom_facenum[i] = m.geom_faceadr[g] >= 0 ? m.geom_facenum[g] : 0;
     d.geom_cornadr[i] = m.geom_cornadr[g];
@@ -785,7 +888,9 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
   e->H = horizon;
   e->nbasis = nbasis;
   e->host = m->m;
-  int rc = build_dev_model(e->host, e->dev);
+  std::vector<int32_t> lutadr(std::max(1, e->host.ngeom));
+  const int64_t nlut = hull_start_table(e->host, MPCR_LUT_R, 0, lutadr.data(), nullptr);
+  int rc = build_dev_model(e->host, lutadr.data(), e->dev);
   if (rc) { delete e; return rc; }
   e->wide = needs_wide(e->host, e->dev);
   if (e->host.nhullv > 0) {  // hull vertices (float4) + graph, pointed to by the device model
@@ -873,19 +978,19 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
         }
       return true;
     };
-    int nlut = 0;
-    for (int g = 0; g < h.ngeom; g++)
-      if (h.geom_hulladr[g] >= 0 && h.geom_hullnum[g] > 0) nlut = std::max(nlut, h.geom_lutadr[g] + 6 * MPCR_LUT_R * MPCR_LUT_R);
+    std::vector<int32_t> cells(nlut);
+    hull_start_table(h, MPCR_LUT_R, g_start_scramble.load(), nullptr, cells.data());
     std::vector<float4> hl(nlut > 0 ? nlut : 1);
+    std::vector<int> hulls;
     for (int g = 0; g < h.ngeom; g++)
-      if (h.geom_hulladr[g] >= 0 && h.geom_hullnum[g] > 0) {
-        const int la = h.geom_lutadr[g], nc = 6 * MPCR_LUT_R * MPCR_LUT_R;
-        for (int c = 0; c < nc; c++) {
-          const int v = h.hull_lut[la + c];
-          hl[la + c] = rec(v);
-          if (cell_exact(g, c, v)) hl[la + c].w = bitsf(v | 0x8000 | (h.hull_adjnum[v] << 16));
-        }
+      if (lutadr[g] >= 0) hulls.push_back(g);
+    for_each_hull_parallel(hulls, [&](int g) {
+      for (int64_t c = lutadr[g], c1 = c + 6LL * MPCR_LUT_R * MPCR_LUT_R; c < c1; c++) {
+        const int v = cells[c];
+        hl[c] = rec(v);
+        if (cell_exact(g, (int)(c - lutadr[g]), v)) hl[c].w = bitsf(v | 0x8000 | (h.hull_adjnum[v] << 16));
       }
+    });
     if (hipMalloc(&e->d_hull_lut, sizeof(float4) * (nlut ? nlut : 1)) != hipSuccess ||
         (nlut && hipMemcpy(e->d_hull_lut, hl.data(), sizeof(float4) * nlut, hipMemcpyHostToDevice) != hipSuccess)) {
       mpcr_engine_free(e);

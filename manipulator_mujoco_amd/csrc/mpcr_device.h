@@ -156,7 +156,7 @@ struct DevModel {
   // convex hulls of mesh geoms (geom frame), hill-climbing graph -----------------
   int geom_hulladr[DX_NG];
   int geom_hullnum[DX_NG];
-  int geom_lutadr[DX_NG];  // first hull_lut cell, -1: no table
+  int geom_lutadr[DX_NG];  // first hull_lut cell (engine.hip hull_start_table), -1: no table
   const MPCR_GMEM float4* hull_vert;  // xyz | degree (int bits in w)
   const MPCR_GMEM int2* hull_info;    // (adjacency start, count) per vertex
   const MPCR_GMEM float4* hull_adjv;  // neighbour xyz | (index | degree << 16) (bits in w): one load per neighbour

@@ -18,7 +18,7 @@
 #include <atomic>
 
 #include "rollout.h"
-#include "../../include/mpcr_model.h"  // MPCR_LUT_R (the hull start table layout)
+#include "../../include/mpcr_model.h"  // MPCR_LUT_R (the engine's hull start table)
 
 namespace mpcr {
 
@@ -810,8 +810,8 @@ __device__ __noinline__ TieStep tie_round(const DevModel* __restrict__ m, int v,
   return TieStep{x.x, x.y, x.z, tkey};
 }
 
-// cube-map cell of a local direction (the model's hull_lut order, oracle
-// lut_cell): major axis (lowest on ties), its sign, the other two components
+// cube-map cell of a local direction (the engine's start table order,
+// engine.hip hull_start_table; oracle lut_cell): major axis (lowest on ties), its sign, the other two components
 // (cyclic order) over |l_axis| in MPCR_LUT_R bins
 template <int R = MPCR_LUT_R>
 __device__ __forceinline__ int lut_cell(const float l[3]) {
@@ -873,6 +873,11 @@ __device__ __forceinline__ void sup_start(const DevModel* __restrict__ m, const 
     q.hh = m->hull_vert[hint >= 0 ? hint : h0];
   }
 }
+// MPCR_SAT_TIES 1: the SAT's value-only queries walk the ties too (A/B of
+// the start independence, tools/scramble_check.py)
+#ifndef MPCR_SAT_TIES
+#define MPCR_SAT_TIES 0
+#endif
 template <class S>
 // ties = false: the caller uses the support value only (the SAT's
 // separations), which any tied vertex gives to within kHullTie
@@ -1443,7 +1448,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, const S& s, PS& ps, con
           const bool two = k >= nf1;
           float pt[3];
           int h = two ? h0 : h1;
-          sup_finish(m, s, two ? g1 : g2, q[u], pt, h, c, false);
+          sup_finish(m, s, two ? g1 : g2, q[u], pt, h, c, MPCR_SAT_TIES != 0);
           const float sp = nw[u][0] * pt[0] + nw[u][1] * pt[1] + nw[u][2] * pt[2] - off[u];
           ps.satsep[k] = sp;
           mxl = fmaxf(mxl, sp);
@@ -1537,7 +1542,7 @@ void poly_manifold_wave(const DevModel* __restrict__ m_, const S& s, PS& ps, con
     face_rel(m, s, g, fid, c, nw, off);
     const float mn[3] = {-nw[0], -nw[1], -nw[2]};
     int h = two ? h0 : h1;
-    support_geom(m, s, go, mn, pt, h, c, false);
+    support_geom(m, s, go, mn, pt, h, c, MPCR_SAT_TIES != 0);
     sep = nw[0] * pt[0] + nw[1] * pt[1] + nw[2] * pt[2] - off;
   }
   // the maximum's tie band: the lowest face index (a flush face pair has the

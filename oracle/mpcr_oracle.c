@@ -37,6 +37,7 @@
  */
 #include <math.h>
 #include <execinfo.h>
+#include <pthread.h>
 #include <signal.h>
 #include <unistd.h>
 #include <stdlib.h>
@@ -996,21 +997,127 @@ static double tie_sign(double lk, double ln) {
   return fabs(lk) < g_floor[2] * ln ? 0.0 : (lk >= 0 ? 1.0 : -1.0);
 }
 
-/* world support point of geom g along dir (any length); *hint: hull vertex the
-   previous query on this geom ended at (-1: none), where the climb starts */
-/* cube-map cell of a local direction l (the model's hull_lut order): major
+/* cube-map cell of a local direction l (the start table's order): major
    axis (lowest on ties), its sign, then the other two components (cyclic
    order) over |l_axis| in R bins; the kernel's lut_cell in fp32 */
+#define ORACLE_LUT_R 128 /* any resolution gives the same supports (the tie walk); the kernel's is MPCR_LUT_R */
 static int lut_cell(const double l[3]) {
   const double a0 = fabs(l[0]), a1 = fabs(l[1]), a2 = fabs(l[2]);
   const int ax = (a0 >= a1 && a0 >= a2) ? 0 : (a1 >= a2 ? 1 : 2);
   const double la = fabs(l[ax]);
   if (!(la > 0)) return 0;
-  const int R = MPCR_LUT_R;
+  const int R = ORACLE_LUT_R;
   int iu = (int)floor((l[(ax + 1) % 3] / la + 1.0) * 0.5 * R), iv = (int)floor((l[(ax + 2) % 3] / la + 1.0) * 0.5 * R);
   iu = iu < 0 ? 0 : (iu > R - 1 ? R - 1 : iu);
   iv = iv < 0 ? 0 : (iv > R - 1 ? R - 1 : iv);
   return (2 * ax + (l[ax] < 0)) * R * R + iu * R + iv;
+}
+
+/* Support start tables.  The model blob carries none since v9 (the engine
+   builds its own, engine.hip hull_start_table); the oracle builds one per
+   model on first use, by the same definition -- per hull and cube-map cell
+   the vertex extreme along the cell centre, cells in scan order, each
+   climbing (strict ascent) from the previous cell's vertex, then the lowest
+   index among the exactly tied maxima along tied edges -- and keeps it for
+   the process (at most ORACLE_LUT_CACHE models; past that, climbs start at
+   the hull's first vertex: slower, the same supports).  Every entry point
+   names its model once (use_model), so the queries read the table through
+   thread-locals.  oracle_set_start_scramble(seed != 0): hashed vertices
+   instead (tests/test_hull_ties.py). */
+#define ORACLE_LUT_CACHE 32
+typedef struct { uint64_t key; int32_t adr[MPCR_MAX_GEOM]; int32_t* cells; } lut_entry;
+static lut_entry g_lut[ORACLE_LUT_CACHE];
+static int g_nlut;
+static pthread_mutex_t g_lut_mu = PTHREAD_MUTEX_INITIALIZER;
+static uint64_t g_scramble;
+static __thread const int32_t* t_lutadr;
+static __thread const int32_t* t_cells;
+void oracle_set_start_scramble(unsigned long long seed) { g_scramble = seed; }
+
+static uint64_t mix64(uint64_t x) {
+  x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull; x ^= x >> 27; x *= 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+static uint64_t hash_words(uint64_t h, const void* p, size_t nbytes) {
+  const unsigned char* b = (const unsigned char*)p;
+  for (size_t i = 0; i + 8 <= nbytes; i += 8) {
+    uint64_t w;
+    memcpy(&w, b + i, 8);
+    h = mix64(h ^ w);
+  }
+  for (size_t i = nbytes & ~(size_t)7; i < nbytes; i++) h = mix64(h ^ b[i]);
+  return h;
+}
+
+static void build_starts(const mpcr_model_t* m, lut_entry* e, uint64_t scramble) {
+  const int R = ORACLE_LUT_R, nc = 6 * R * R;
+  int n = 0;
+  for (int g = 0; g < m->ngeom; g++) {
+    e->adr[g] = (m->geom_hulladr[g] >= 0 && m->geom_hullnum[g] > 0) ? n : -1;
+    if (e->adr[g] >= 0) n += nc;
+  }
+  e->cells = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+  if (!e->cells) return;
+  int tied[256];
+  for (int g = 0; g < m->ngeom; g++) {
+    if (e->adr[g] < 0) continue;
+    const int a = m->geom_hulladr[g], na = m->geom_hullnum[g];
+    int32_t* out = e->cells + e->adr[g];
+    int v = a;
+    for (int c = 0; c < nc; c++) {
+      if (scramble) { out[c] = a + (int)(mix64(scramble ^ ((uint64_t)g << 40) ^ (uint64_t)c) % (uint64_t)na); continue; }
+      const int f = c / (R * R), iu = (c / R) % R, iv = c % R, ax = f / 2;
+      double dd[3];
+      dd[ax] = (f & 1) ? -1.0 : 1.0;
+      dd[(ax + 1) % 3] = -1.0 + (2.0 * iu + 1.0) / R;
+      dd[(ax + 2) % 3] = -1.0 + (2.0 * iv + 1.0) / R;
+      double best = dot3(m->hull_vert[v], dd);
+      for (;;) {
+        int nb = v;
+        for (int k = m->hull_adjadr[v]; k < m->hull_adjadr[v] + m->hull_adjnum[v]; k++) {
+          const int u = m->hull_adj[k];
+          const double du = dot3(m->hull_vert[u], dd);
+          if (du > best) { best = du; nb = u; }
+        }
+        if (nb == v) break;
+        v = nb;
+      }
+      int nt = 1, lo = v;
+      tied[0] = v;
+      for (int i = 0; i < nt && nt < 256; i++)
+        for (int k = m->hull_adjadr[tied[i]]; k < m->hull_adjadr[tied[i]] + m->hull_adjnum[tied[i]] && nt < 256; k++) {
+          const int u = m->hull_adj[k];
+          if (!(dot3(m->hull_vert[u], dd) == best)) continue;
+          int seen = 0;
+          for (int j = 0; j < nt; j++) seen |= tied[j] == u;
+          if (!seen) { tied[nt++] = u; if (u < lo) lo = u; }
+        }
+      out[c] = lo;
+    }
+  }
+}
+
+static void use_model(const mpcr_model_t* m) {
+  t_lutadr = t_cells = NULL;
+  if (m->nhullv <= 0) return;
+  const uint64_t scramble = g_scramble;
+  uint64_t h = mix64(0x6d70637273746172ull ^ scramble ^ ((uint64_t)m->ngeom << 32) ^ (uint64_t)m->nhullv);
+  h = hash_words(h, m->geom_hulladr, sizeof(int32_t) * m->ngeom);
+  h = hash_words(h, m->geom_hullnum, sizeof(int32_t) * m->ngeom);
+  h = hash_words(h, m->hull_vert, sizeof(m->hull_vert[0]) * m->nhullv);
+  h = hash_words(h, m->hull_adjadr, sizeof(int32_t) * m->nhullv);
+  h = hash_words(h, m->hull_adj, sizeof(int32_t) * m->nhulla);
+  pthread_mutex_lock(&g_lut_mu);
+  lut_entry* e = NULL;
+  for (int i = 0; i < g_nlut && !e; i++)
+    if (g_lut[i].key == h) e = &g_lut[i];
+  if (!e && g_nlut < ORACLE_LUT_CACHE) {
+    e = &g_lut[g_nlut];
+    build_starts(m, e, scramble);
+    if (e->cells) { e->key = h; g_nlut++; } else e = NULL;
+  }
+  pthread_mutex_unlock(&g_lut_mu);
+  if (e) { t_lutadr = e->adr; t_cells = e->cells; }
 }
 
 /* MPR work counters of the calling thread (diagnostic: tools/mpr_stats.py, workers = 1):
@@ -1091,6 +1198,8 @@ static int hull_tie(const mpcr_model_t* m, int v, int t, double lo, const double
   return v;
 }
 
+/* world support point of geom g along dir (any length); *hint: hull vertex the
+   previous query on this geom ended at (-1: none), where the climb starts */
 static void support_rel(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint,
                         const double* org);
 static void support(const mpcr_model_t* m, const odata* d, int g, const double dir[3], double out[3], int* hint) {
@@ -1131,7 +1240,7 @@ static void support_rel(const mpcr_model_t* m, const odata* d, int g, const doub
          previous query on this pair ended) when it reaches that by the band
          -- on equal values the hint, as the kernel (after a tie walk the hint
          is the tie's lowest index) */
-      int v = m->geom_lutadr[g] >= 0 ? m->hull_lut[m->geom_lutadr[g] + lut_cell(l)] : m->geom_hulladr[g];
+      int v = t_cells && t_lutadr[g] >= 0 ? t_cells[t_lutadr[g] + lut_cell(l)] : m->geom_hulladr[g];
       double best = dot3(m->hull_vert[v], lu);
       if (*hint >= 0) {
         const double bh = dot3(m->hull_vert[*hint], lu);
@@ -2533,6 +2642,7 @@ int oracle_step(const mpcr_model_t* m, double* qpos, double* qvel, double* qacc_
                 double* bias_out, double* passive_out, double* qacc_out, double* eef_out, double* dist_out,
                 int* nefc_out) {
   odata* d = (odata*)calloc(1, sizeof(odata));
+  use_model(m);
   if (!d) return -1;
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
@@ -2566,6 +2676,7 @@ int oracle_step(const mpcr_model_t* m, double* qpos, double* qvel, double* qacc_
 int oracle_geom_poses(const mpcr_model_t* m, const double* qpos, double* xpos, double* xmat, int pair,
                       double* mpr_out) {
   odata* d = (odata*)calloc(1, sizeof(odata));
+  use_model(m);
   if (!d) return -1;
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   reset_hints(d);
@@ -2604,6 +2715,7 @@ enum { ODBG_MAXCON = 48, ODBG_ROW = 2 + 8 * ODBG_MAXCON, ODBG_MAXROW = 200, ODBG
 int oracle_step_debug(const mpcr_model_t* m, const double* qpos, const double* qvel, const double* qacc_ws,
                       double* out) {
   odata* d = (odata*)calloc(1, sizeof(odata));
+  use_model(m);
   if (!d) return -1;
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
@@ -2645,6 +2757,7 @@ int oracle_step_debug(const mpcr_model_t* m, const double* qpos, const double* q
 int oracle_ls_inputs(const mpcr_model_t* m, const double* qpos, const double* qvel, const double* qacc_ws,
                      double* out) {
   odata* d = (odata*)calloc(1, sizeof(odata));
+  use_model(m);
   if (!d) return -1;
   memcpy(d->qpos, qpos, sizeof(double) * m->nq);
   memcpy(d->qvel, qvel, sizeof(double) * m->nv);
@@ -2674,6 +2787,7 @@ int oracle_rollout(const mpcr_model_t* m, int n, int H, const double* thetadot, 
                    int index_base) {
   if (m->magic != MPCR_MODEL_MAGIC || m->nbytes != sizeof(mpcr_model_t)) return -2;
   odata* d = (odata*)calloc(1, sizeof(odata));
+  use_model(m);
   double* cprev = (double*)calloc(m->nslot > 0 ? m->nslot : 1, sizeof(double));
   if (!d || !cprev) { free(d); free(cprev); return -1; }
   int nc = m->nctrl, status = 0;

