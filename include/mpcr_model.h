@@ -41,9 +41,9 @@ extern "C" {
 /* support start table resolution: 6 cube faces x R x R cells per hull.  Not
    part of the blob since v9 -- the engine builds the table from hull_vert
    (engine.hip hull_start_table), so R is the library's build-time choice
-   (round 5: 16 -> 128, round 6: 256; DESIGN.md perf log) */
+   (round 5: 16 -> 128; 256 measured in round 6, DESIGN.md perf log) */
 #ifndef MPCR_LUT_R
-#define MPCR_LUT_R      256
+#define MPCR_LUT_R      128
 #endif
 #define MPCR_MAX_FACE   12288 /* polygon faces of the polyhedron-pair hulls and boxes */
 #define MPCR_MAX_FACEV  49152 /* face polygon vertex entries (<= MPCR_FACE_MAXV each) */

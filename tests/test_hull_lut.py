@@ -80,7 +80,7 @@ def test_table_layout_and_extremes(dual_arm):
 def test_library_resolution(dual_arm):
     adr, lut = Model(dual_arm).hull_starts()
     r = int(round(np.sqrt(lut.size / 14 / 6)))
-    assert lut.size == 14 * 6 * r * r and r >= 128  # MPCR_LUT_R (round 6: 256)
+    assert lut.size == 14 * 6 * r * r and r >= 128  # MPCR_LUT_R
 
 
 def test_blob_carries_no_table(dual_arm):
