@@ -46,6 +46,14 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise MpcrError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    # torch's HIP runtime first: torch links an unversioned libamdhip64.so of
+    # its own, libmpcr the system's libamdhip64.so.7 (the same SONAME).  Loaded
+    # in this order libmpcr binds to torch's copy; the other way round the
+    # process holds two HIP runtimes and libmpcr's finds no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     vp, i, d, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_float
     P = ctypes.POINTER
