@@ -118,10 +118,13 @@ void mpcr_model_free(mpcr_model* m);
    (2 axis + negative) R^2 + iu R + iv (rollout.hip lut_cell), each naming
    the global hull vertex extreme along the cell centre (fp64; the lowest
    index among exact ties).  geom_adr[ngeom] (nullable) receives each geom's
-   first cell (-1: no hull), cells (nullable) all of them when cap holds the
-   count.  Returns the cell count (< 0: error).  Host only, no device
+   first cell (-1: no hull), cells and exact (nullable) every cell when cap
+   holds the count -- exact[c] = 1 where the engine skips the climb (the
+   start vertex beats each neighbour along every direction of the cell by the
+   fp32 margin).  Returns the cell count (< 0: error).  Host only, no device
    (tests/test_hull_lut.py). */
-int64_t mpcr_model_hull_starts(const mpcr_model* m, int R, int32_t* geom_adr, int32_t* cells, int64_t cap);
+int64_t mpcr_model_hull_starts(const mpcr_model* m, int R, int32_t* geom_adr, int32_t* cells, uint8_t* exact,
+                               int64_t cap);
 /* Test knob (the start-independence tests): engines created while seed != 0
    start every hull climb at a vertex of its hull hashed from (seed, geom,
    cell) instead of the extreme one.  Process-wide; returns the previous seed. */

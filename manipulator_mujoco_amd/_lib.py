@@ -102,7 +102,7 @@ def load():
     lib.mpcr_comm_allreduce_key.argtypes = [vp, vp, i, vp]
     lib.mpcr_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
     lib.mpcr_comm_gather_elites.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
-    lib.mpcr_model_hull_starts.argtypes = [vp, i, P(ctypes.c_int32), P(ctypes.c_int32), ctypes.c_int64]
+    lib.mpcr_model_hull_starts.argtypes = [vp, i, P(ctypes.c_int32), P(ctypes.c_int32), P(ctypes.c_uint8), ctypes.c_int64]
     lib.mpcr_set_hull_start_scramble.argtypes = [u64]
     for name in EXPORTS + ("mpcr_rollout_trace", "mpcr_plant_step_debug", "mpcr_plant_dbg_size"):
         if name not in _VOID:

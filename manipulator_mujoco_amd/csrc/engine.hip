@@ -406,12 +406,66 @@ static int64_t hull_start_table(const mpcr_model_t& m, int R, uint64_t scramble,
   return n;
 }
 
-extern "C" int64_t mpcr_model_hull_starts(const mpcr_model* m, int R, int32_t* geom_adr, int32_t* cells, int64_t cap) {
+// exact[c] = 1 when cell c's start vertex is the support of every direction
+// in the cell: the kernel's climb from it would end where it starts (no
+// neighbour beats it, and no hint vertex beats the start), so the kernel skips
+// the hint load and the climb -- bitwise the same support point, one
+// dependent load instead of two or more.  A cube-map cell is the convex cone
+// of its 4 corner rays and the directions a hull vertex is extreme for are a
+// convex cone, bounded by its neighbours: the start vertex beats each
+// neighbour by more than the margin along each corner ray (fp32 coordinates,
+// as the kernel reads them), so along every direction of the cell.  The
+// margin, max(1e-6 m, 32 FLT_EPSILON max|x|), scales with the hull's extent:
+// the kernel's fp32 projections err by a few ulp of the largest coordinate
+// (~1e-8 m on the gripper's cm-sized hulls, whose margin stays 1e-6 m;
+// tests/test_hull_lut.py checks sampled directions on metre-sized hulls).
+static void hull_exact_cells(const mpcr_model_t& m, int R, const int32_t* geom_adr, const int32_t* cells,
+                             uint8_t* exact) {
+  constexpr double kExactGap = 1e-6;
+  std::vector<int> hulls;
+  for (int g = 0; g < m.ngeom; g++)
+    if (geom_adr[g] >= 0) hulls.push_back(g);
+  auto xf = [&](int v, int k) { return (double)(float)m.hull_vert[v][k]; };
+  for_each_hull_parallel(hulls, [&](int g) {
+    double gap_min = kExactGap;
+    for (int v = m.geom_hulladr[g]; v < m.geom_hulladr[g] + m.geom_hullnum[g]; v++)
+      gap_min = std::max(gap_min, 32.0 * FLT_EPSILON * std::sqrt(xf(v, 0) * xf(v, 0) + xf(v, 1) * xf(v, 1) + xf(v, 2) * xf(v, 2)));
+    for (int64_t c = 0, nc = 6LL * R * R; c < nc; c++) {
+      const int v = cells[geom_adr[g] + c];
+      const int f = (int)(c / ((int64_t)R * R)), iu = (int)((c / R) % R), iv = (int)(c % R), ax = f / 2;
+      bool ok = true;
+      for (int du = 0; du < 2 && ok; du++)
+        for (int dv = 0; dv < 2 && ok; dv++) {
+          double d[3];
+          d[ax] = (f & 1) ? -1.0 : 1.0;
+          d[(ax + 1) % 3] = -1.0 + 2.0 * (iu + du) / R;
+          d[(ax + 2) % 3] = -1.0 + 2.0 * (iv + dv) / R;
+          const double dn = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+          for (int k = m.hull_adjadr[v]; k < m.hull_adjadr[v] + m.hull_adjnum[v] && ok; k++) {
+            const int u = m.hull_adj[k];
+            const double gap = (xf(v, 0) - xf(u, 0)) * d[0] + (xf(v, 1) - xf(u, 1)) * d[1] + (xf(v, 2) - xf(u, 2)) * d[2];
+            ok = gap > gap_min * dn;
+          }
+        }
+      exact[geom_adr[g] + c] = ok;
+    }
+  });
+}
+
+extern "C" int64_t mpcr_model_hull_starts(const mpcr_model* m, int R, int32_t* geom_adr, int32_t* cells,
+                                          uint8_t* exact, int64_t cap) {
   if (!m) return fail(MPCR_EINVAL, "null model");
   if (R == 0) R = MPCR_LUT_R;
   if (R < 1 || R > 1024) return fail(MPCR_EINVAL, "table resolution %d outside 1..1024", R);
-  const int64_t n = hull_start_table(m->m, R, 0, geom_adr, nullptr);
-  if (cells && cap >= n) hull_start_table(m->m, R, 0, nullptr, cells);
+  std::vector<int32_t> adr(std::max(1, m->m.ngeom));
+  const int64_t n = hull_start_table(m->m, R, 0, adr.data(), nullptr);
+  if (geom_adr) std::copy(adr.begin(), adr.begin() + m->m.ngeom, geom_adr);
+  if ((cells || exact) && cap >= n) {
+    std::vector<int32_t> own;
+    if (!cells) own.resize(n), cells = own.data();
+    hull_start_table(m->m, R, 0, nullptr, cells);
+    if (exact) hull_exact_cells(m->m, R, adr.data(), cells, exact);
+  }
   return n;
 }
 
@@ -938,59 +992,18 @@ extern "C" int mpcr_engine_create(const mpcr_model* m, int device, int max_n, in
     e->dev.hull_info = as_gmem(e->d_hull_info);
     e->dev.hull_adjv = as_gmem(e->d_hull_adjv);
     e->dev.hull_head = as_gmem(e->d_hull_head);
-    // the support start table; a cell whose start vertex is the support of
-    // every direction in it is marked exact (bit 15 of the record's index
-    // half: vertex indices are < 32768): the kernel's climb from that vertex
-    // would end where it starts (no neighbour beats it, and no hint vertex
-    // beats the start), so the kernel skips the hint load and the climb --
-    // bitwise the same support point, one dependent load instead of two or
-    // more.  A cube-map cell is the convex cone of its 4 corner rays and the
-    // directions a hull vertex is extreme for are a convex cone, bounded by
-    // its neighbours: the start vertex beats each neighbour by > kExactGap m
-    // (fp32 coordinates) along each corner ray, so along every direction of
-    // the cell.  The margin scales with the hull's extent: the kernel's fp32
-    // projections err by a few ulp of the largest coordinate (~1e-8 m on the
-    // gripper's cm-sized hulls, whose margin stays 1e-6 m)
-    constexpr double kExactGap = 1e-6;
-    std::vector<double> hull_gap(h.ngeom, kExactGap);
-    for (int g = 0; g < h.ngeom; g++)
-      if (h.geom_hulladr[g] >= 0)
-        for (int v = h.geom_hulladr[g]; v < h.geom_hulladr[g] + h.geom_hullnum[g]; v++) {
-          const double r = std::sqrt((double)hv[v].x * hv[v].x + (double)hv[v].y * hv[v].y + (double)hv[v].z * hv[v].z);
-          hull_gap[g] = std::max(hull_gap[g], 32.0 * FLT_EPSILON * r);
-        }
-    auto cell_exact = [&](int g, int c, int v) {
-      const int R = MPCR_LUT_R, f = c / (R * R), iu = (c / R) % R, iv = c % R, ax = f / 2;
-      const double gap_min = hull_gap[g];
-      const float* x = &hv[v].x;
-      for (int du = 0; du < 2; du++)
-        for (int dv = 0; dv < 2; dv++) {
-          double d[3];
-          d[ax] = (f & 1) ? -1.0 : 1.0;
-          d[(ax + 1) % 3] = -1.0 + 2.0 * (iu + du) / R;
-          d[(ax + 2) % 3] = -1.0 + 2.0 * (iv + dv) / R;
-          const double dn = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-          for (int k = h.hull_adjadr[v]; k < h.hull_adjadr[v] + h.hull_adjnum[v]; k++) {
-            const float* y = &hv[h.hull_adj[k]].x;
-            const double gap = ((double)x[0] - y[0]) * d[0] + ((double)x[1] - y[1]) * d[1] + ((double)x[2] - y[2]) * d[2];
-            if (!(gap > gap_min * dn)) return false;
-          }
-        }
-      return true;
-    };
+    // the support start table, exact cells flagged in bit 15 of the record's
+    // index half (vertex indices are < 32768; hull_exact_cells)
     std::vector<int32_t> cells(nlut);
+    std::vector<uint8_t> exact(nlut);
     hull_start_table(h, MPCR_LUT_R, g_start_scramble.load(), nullptr, cells.data());
+    hull_exact_cells(h, MPCR_LUT_R, lutadr.data(), cells.data(), exact.data());
     std::vector<float4> hl(nlut > 0 ? nlut : 1);
-    std::vector<int> hulls;
-    for (int g = 0; g < h.ngeom; g++)
-      if (lutadr[g] >= 0) hulls.push_back(g);
-    for_each_hull_parallel(hulls, [&](int g) {
-      for (int64_t c = lutadr[g], c1 = c + 6LL * MPCR_LUT_R * MPCR_LUT_R; c < c1; c++) {
-        const int v = cells[c];
-        hl[c] = rec(v);
-        if (cell_exact(g, (int)(c - lutadr[g]), v)) hl[c].w = bitsf(v | 0x8000 | (h.hull_adjnum[v] << 16));
-      }
-    });
+    for (int64_t c = 0; c < nlut; c++) {
+      const int v = cells[c];
+      hl[c] = rec(v);
+      if (exact[c]) hl[c].w = bitsf(v | 0x8000 | (h.hull_adjnum[v] << 16));
+    }
     if (hipMalloc(&e->d_hull_lut, sizeof(float4) * (nlut ? nlut : 1)) != hipSuccess ||
         (nlut && hipMemcpy(e->d_hull_lut, hl.data(), sizeof(float4) * nlut, hipMemcpyHostToDevice) != hipSuccess)) {
       mpcr_engine_free(e);

@@ -32,18 +32,22 @@ class Model:
         check(lib.mpcr_model_from_blob(self._blob, len(blob), ctypes.byref(h)))
         self.handle = h
 
-    def hull_starts(self, R: int = 0):
+    def hull_starts(self, R: int = 0, exact: bool = False):
         """The support start table engines build for this model
         (mpcr_model_hull_starts; R = 0: the library's MPCR_LUT_R): per-geom
-        first cell (-1: no hull) and the global hull vertex of every cell."""
+        first cell (-1: no hull), the global hull vertex of every cell and,
+        with exact, the cells whose climb the engine skips."""
         lib = _lib.load()
         adr = np.empty(max(1, self.compiled.ngeom), dtype=np.int32)
-        i32p = ctypes.POINTER(ctypes.c_int32)
-        n = lib.mpcr_model_hull_starts(self.handle, R, adr.ctypes.data_as(i32p), None, 0)
+        i32p, u8p = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint8)
+        n = lib.mpcr_model_hull_starts(self.handle, R, adr.ctypes.data_as(i32p), None, None, 0)
         check(int(min(n, 0)))
         cells = np.empty(max(1, n), dtype=np.int32)
-        check(int(min(lib.mpcr_model_hull_starts(self.handle, R, None, cells.ctypes.data_as(i32p), n), 0)))
-        return adr[:self.compiled.ngeom], cells[:n]
+        ex = np.empty(max(1, n), dtype=np.uint8)
+        check(int(min(lib.mpcr_model_hull_starts(self.handle, R, None, cells.ctypes.data_as(i32p),
+                                                 ex.ctypes.data_as(u8p) if exact else None, n), 0)))
+        out = (adr[:self.compiled.ngeom], cells[:n])
+        return out + (ex[:n].astype(bool),) if exact else out
 
     def __del__(self):
         try:

@@ -94,3 +94,48 @@ def test_models_without_hulls_have_no_table():
     m = models.load("scene_mjx", 0.05)
     adr, lut = Model(m).hull_starts()
     assert lut.size == 0 and (adr == -1).all()
+
+
+def _kernel_dot(x, d):
+    """x . d in fp32 as the kernel forms it (products and sums in float)."""
+    x, d = x.astype(np.float32), d.astype(np.float32)
+    return (x[..., 0] * d[..., 0] + x[..., 1] * d[..., 1]) + x[..., 2] * d[..., 2]
+
+
+@pytest.mark.parametrize("scale", [1.0, 40.0])
+def test_exact_cells_hold_along_sampled_directions(dual_arm, scale):
+    """a cell the engine marks exact skips the climb, so its start
+    vertex must beat every neighbour along every direction in the cell as the
+    kernel computes the projections (fp32).  Checked on the dual arm's hulls
+    and on the same hulls scaled to metres (scale 40: the 2691-vertex hull
+    spans ~4 m, where a fixed 1e-6 m margin would be below fp32 rounding):
+    the cell corners and random interior directions of every 5th exact cell,
+    normalised in fp32 as the kernel's local direction is."""
+    import copy
+    m = copy.copy(dual_arm)
+    m.hull_vert = np.asarray(dual_arm.hull_vert, dtype=np.float64) * scale
+    adr, lut, exact = Model(m).hull_starts(R, exact=True)
+    assert exact.mean() > 0.3  # many cells skip the climb (more at the library's finer cells)
+    verts = np.asarray(m.hull_vert).reshape(-1, 3)
+    adjadr, adjnum, adj = (np.asarray(m.hull_adjadr), np.asarray(m.hull_adjnum), np.asarray(m.hull_adj))
+    rng = np.random.default_rng(3)
+    c = -1.0 + 2.0 * np.arange(R + 1) / R  # cell edges
+    checked = 0
+    for g in np.where(adr >= 0)[0]:
+        cells = np.where(exact[adr[g]:adr[g] + 6 * R * R])[0][::5]
+        for cc in cells:
+            f, iu, iv = cc // (R * R), (cc // R) % R, cc % R
+            ax = f // 2
+            t = np.concatenate([np.array([[0, 0], [0, 1], [1, 0], [1, 1]], float), rng.random((4, 2))])
+            d = np.zeros((len(t), 3))
+            d[:, ax] = -1.0 if f % 2 else 1.0
+            d[:, (ax + 1) % 3] = c[iu] + (c[iu + 1] - c[iu]) * t[:, 0]
+            d[:, (ax + 2) % 3] = c[iv] + (c[iv + 1] - c[iv]) * t[:, 1]
+            d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+            v = int(lut[adr[g] + cc])
+            nb = adj[adjadr[v]:adjadr[v] + adjnum[v]]
+            best = _kernel_dot(verts[v][None, :], d)  # (dirs,)
+            other = _kernel_dot(verts[nb][None, :, :], d[:, None, :])  # (dirs, nb)
+            assert (other <= best[:, None]).all(), (g, cc, v, float((other - best[:, None]).max()))
+            checked += 1
+    assert checked > 1000
