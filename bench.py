@@ -46,7 +46,7 @@ PT = (-0.3, -0.3, 0.5)
 QT = (0.0, 1.0, 0.0, 0.0)
 PEAK_F32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (FMA) peak
 PEAK_HBM_GBS = 8000.0
-PROFILE_TAG = "r06i"  # the final round-6 build (source 19338102)
+PROFILE_TAG = "r06j"  # the final round-6 build (source 77733f95)
 
 # BASELINE.json configs; c3 is the metric's workload (default)
 CONFIGS = {
