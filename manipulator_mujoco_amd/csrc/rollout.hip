@@ -1848,11 +1848,6 @@ __device__ __forceinline__ int narrow_lane(const DevModel* __restrict__ m, const
     for (int c = 0; c < 3; c++) { A[c] = x1[c] - hl * ax[c] - x2[c]; B[c] = 2 * hl * ax[c]; }
     mtv(a, R2, A);
     mtv(dd, R2, B);
-    // within 1e-6 rad of parallel to a face pair is parallel (the oracle's
-    // rule): the squared distance is flat along the segment there, and the
-    // rounding sign of dd_k would pick the minimiser
-#pragma unroll
-    for (int c = 0; c < 3; c++) dd[c] = fabsf(dd[c]) <= 2e-6f * hl ? 0.f : dd[c];
     float tlo = -1.f, thi = 2.f, flo = 0.f, fhi = 0.f;
     // knots: 0, 1, (+-h_k - a_k)/dd_k inside (0,1), where the squared
     // distance's derivative fp (piecewise linear, non-decreasing: the

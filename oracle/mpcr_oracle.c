@@ -699,15 +699,6 @@ static void col_capsule_box(const odata* d, int gc, int gb, const double* sc, co
   }
   mulmtv(a, Rb, A);
   mulmtv(dd, Rb, B);
-  /* A segment within 1e-6 rad of parallel to a face pair is parallel (round
-     6): the squared distance below is then flat along it, and the sign of the
-     rounding in dd_k decided where its minimiser lands -- the resting second
-     arm's capsules level in the table, where fp64 kept the first end and
-     fp32 a point past the table's edge, so the far-end contact took the face
-     normal instead of the edge's (tools/c5_tick_triage.py --own,
-     profiles/r06_capsule_box_parallel.txt).  The kernel snaps alike. */
-  for (int k = 0; k < 3; k++)
-    if (fabs(dd[k]) <= 1e-6 * 2 * hl) dd[k] = 0;
   /* f(t) = sum_k max(|a_k + t dd_k| - h_k, 0)^2 is convex, C1, piecewise
      quadratic; f'(t) is monotone and piecewise linear between the knots
      t in {0, 1, (+-h_k - a_k)/dd_k}. */
