@@ -264,7 +264,11 @@ def test_dual_arm_c5_thirty_ticks(torch_cuda):
     the plant -- the rollout kernel with n = 1 stepping the closed loop --
     stays on the fp64 oracle's replay of the 30 applied joint velocities from
     the initial state (joint positions within 1e-4 rad or twice the spread of
-    8 fp32-sized noise draws)."""
+    8 fp32-sized noise draws).  One trajectory: over twelve planner seeds
+    13 of 360 selections miss the oracle by more than 1e-4 and 3 of the 12
+    trajectories have no miss (tools/c5_ticks_survey.py,
+    profiles/r06j_c5_ticks_survey.txt) -- a build whose costs move in the
+    last ulp can land this test on another trajectory."""
     import parity_util as pu
     n, H, ticks = 8192, 50, 30
     from manipulator_mujoco_amd.engine import Plant
